@@ -1,0 +1,294 @@
+// ndfl_capi.cpp -- host side of the C ABI declared in include/ndfl.h.
+// Compiled as HIP for gfx950 together with the kernels (single translation unit).
+#include "../../../include/ndfl.h"
+#include "../hip/deflate_kernels.hip"
+#include "../hip/inflate_kernels.hip"
+
+#include <hip/hip_runtime.h>
+#include <string.h>
+#include <stdlib.h>
+#include <vector>
+
+namespace {
+
+struct DevBuf {
+    void* p = nullptr;
+    size_t cap = 0;
+    hipError_t ensure(size_t n) {
+        if (n <= cap) return hipSuccess;
+        if (p) { hipFree(p); p = nullptr; cap = 0; }
+        size_t want = n < 4096 ? 4096 : n;
+        hipError_t e = hipMalloc(&p, want);
+        if (e == hipSuccess) cap = want;
+        return e;
+    }
+    void release() { if (p) hipFree(p); p = nullptr; cap = 0; }
+    template <class T> T* as() const { return (T*)p; }
+};
+
+uint32_t host_crc_tab[1024];
+uint32_t host_crc_x[64 + 1024];
+bool host_tabs_ready = false;
+
+void init_host_tables() {
+    if (host_tabs_ready) return;
+    for (uint32_t i = 0; i < 256; i++) {
+        uint32_t c = i;
+        for (int k = 0; k < 8; k++) c = (c & 1) ? (c >> 1) ^ NDFL_CRC_POLY : c >> 1;
+        host_crc_tab[i] = c;
+    }
+    for (int t = 1; t < 4; t++)
+        for (uint32_t i = 0; i < 256; i++) {
+            uint32_t c = host_crc_tab[(t - 1) * 256 + i];
+            host_crc_tab[t * 256 + i] = (c >> 8) ^ host_crc_tab[c & 0xFF];
+        }
+    for (uint32_t k = 0; k < 64; k++) host_crc_x[k] = crc_x8n(k);
+    for (uint32_t k = 0; k < 1024; k++) host_crc_x[64 + k] = crc_x8n((uint64_t)k * 64);
+    host_tabs_ready = true;
+}
+
+}  // namespace
+
+struct ndfl_ctx {
+    int device = 0;
+    hipStream_t own = nullptr;
+    hipStream_t stream = nullptr;
+    hipEvent_t ev0 = nullptr, ev1 = nullptr;
+    double last_ms = 0;
+    DevBuf d_in, d_out, d_status, d_ticket, d_edge_w, d_edge_v, d_crc, d_crc1, d_tabs, d_hostio;
+    InflateScratch inf;
+    uint32_t* h_pinned = nullptr;   // small pinned area for results
+};
+
+#define HIPCHK(x) do { hipError_t _e = (x); if (_e != hipSuccess) return NDFL_E_DEVICE; } while (0)
+
+extern "C" {
+
+uint32_t ndfl_abi_version(void) { return NDFL_ABI_VERSION; }
+
+const char* ndfl_error_string(int code) {
+    static const char* reasons[] = {
+        "Unexpected end of stream", "Reserved block type", "len/nlen mismatch in uncompressed block",
+        "This canonical code produces an under-full Huffman code tree",
+        "This canonical code produces an over-full Huffman code tree", "No code length value to copy",
+        "Run exceeds number of codes", "End-of-block symbol has zero code length", "Reserved run length symbol",
+        "Reserved distance symbol", "Length symbol encountered with empty distance code",
+        "Attempting to copy from before start of dictionary", "Header checksum mismatch",
+        "Unsupported compression method", "Decompression checksum mismatch", "Decompressed size mismatch",
+        "Invalid GZIP magic number", "Reserved flags are set", "Unsupported operating system value"};
+    if (code == 0) return "ok";
+    if (code >= 1 && code <= 19) return reasons[code - 1];
+    switch (code) {
+        case NDFL_E_ARG: return "invalid argument";
+        case NDFL_E_UNSUPPORTED: return "configuration not supported on the GPU path";
+        case NDFL_E_CAPACITY: return "output buffer too small";
+        case NDFL_E_DEVICE: return "HIP device error";
+        case NDFL_E_STATE: return "invalid state";
+        default: return "internal error";
+    }
+}
+
+int ndfl_ctx_create(ndfl_ctx** out, int device, uint32_t flags) {
+    (void)flags;
+    if (!out) return NDFL_E_ARG;
+    *out = nullptr;
+    int n = 0;
+    if (hipGetDeviceCount(&n) != hipSuccess || n <= device || device < 0) return NDFL_E_DEVICE;
+    HIPCHK(hipSetDevice(device));
+    init_host_tables();
+    ndfl_ctx* c = new ndfl_ctx();
+    c->device = device;
+    if (hipStreamCreateWithFlags(&c->own, hipStreamNonBlocking) != hipSuccess) { delete c; return NDFL_E_DEVICE; }
+    c->stream = c->own;
+    hipEventCreate(&c->ev0);
+    hipEventCreate(&c->ev1);
+    if (c->d_tabs.ensure(sizeof(host_crc_tab) + sizeof(host_crc_x)) != hipSuccess) { delete c; return NDFL_E_DEVICE; }
+    hipMemcpy(c->d_tabs.p, host_crc_tab, sizeof(host_crc_tab), hipMemcpyHostToDevice);
+    hipMemcpy((char*)c->d_tabs.p + sizeof(host_crc_tab), host_crc_x, sizeof(host_crc_x), hipMemcpyHostToDevice);
+    if (hipHostMalloc((void**)&c->h_pinned, 4096, 0) != hipSuccess) { delete c; return NDFL_E_DEVICE; }
+    *out = c;
+    return NDFL_OK;
+}
+
+int ndfl_ctx_destroy(ndfl_ctx* c) {
+    if (!c) return NDFL_OK;
+    hipSetDevice(c->device);
+    hipStreamSynchronize(c->stream);
+    DevBuf* bufs[] = {&c->d_in, &c->d_out, &c->d_status, &c->d_ticket, &c->d_edge_w, &c->d_edge_v,
+                      &c->d_crc, &c->d_crc1, &c->d_tabs, &c->d_hostio};
+    for (DevBuf* b : bufs) b->release();
+    c->inf.release();
+    if (c->h_pinned) hipHostFree(c->h_pinned);
+    if (c->ev0) hipEventDestroy(c->ev0);
+    if (c->ev1) hipEventDestroy(c->ev1);
+    if (c->own) hipStreamDestroy(c->own);
+    delete c;
+    return NDFL_OK;
+}
+
+int ndfl_ctx_set_stream(ndfl_ctx* c, void* s) {
+    if (!c) return NDFL_E_ARG;
+    c->stream = s ? (hipStream_t)s : c->own;
+    return NDFL_OK;
+}
+
+double ndfl_ctx_last_kernel_ms(ndfl_ctx* c) { return c ? c->last_ms : 0.0; }
+
+uint64_t ndfl_deflate_bound(uint64_t len, uint32_t chunk_len) {
+    if (chunk_len == 0) return 0;
+    uint64_t nch = len / chunk_len + 1;
+    // per chunk: <= 9 bits per byte (+ EOB) + header (<= 4,500 bits) + word alignment slack
+    return (9 * len + nch * 4640) / 8 + 64;
+}
+
+uint32_t ndfl_crc32_combine(uint32_t a, uint32_t b, uint64_t len_b) {
+    return crc_multmodp(crc_x8n(len_b), a) ^ b;
+}
+
+int ndfl_deflate_chunks(ndfl_ctx* c, const uint8_t* hist, uint32_t hist_len, uint32_t hist_limit,
+                        const uint8_t* data, uint64_t len, uint32_t chunk_len, int strategy,
+                        int final_flag, uint32_t start_bitpos, uint8_t* out, uint64_t out_cap,
+                        uint64_t* out_end_bits, uint32_t* crc_inout, uint32_t flags) {
+    if (!c || !out_end_bits || (!data && len) || (!hist && hist_len) || !out) return NDFL_E_ARG;
+    if (start_bitpos > 7 || hist_limit > 32768 || hist_len > hist_limit || chunk_len == 0) return NDFL_E_ARG;
+    if (!final_flag && (len == 0 || len % chunk_len != 0)) return NDFL_E_ARG;
+    int rle, dyn;
+    switch (strategy) {
+        case NDFL_LITERAL_STATIC: rle = 0; dyn = 0; break;
+        case NDFL_LITERAL_DYNAMIC: rle = 0; dyn = 1; break;
+        case NDFL_RLE_STATIC: rle = 1; dyn = 0; break;
+        case NDFL_RLE_DYNAMIC: rle = 1; dyn = 1; break;
+        case NDFL_FULL_STATIC: case NDFL_FULL_DYNAMIC: case NDFL_UNCOMPRESSED: return NDFL_E_UNSUPPORTED;
+        default: return NDFL_E_ARG;
+    }
+    if (chunk_len > (uint32_t)MAX_CHUNK) return NDFL_E_UNSUPPORTED;
+    HIPCHK(hipSetDevice(c->device));
+    const uint64_t nch64 = final_flag ? (len == 0 ? 1 : (len + chunk_len - 1) / chunk_len) : len / chunk_len;
+    if (nch64 > 0xFFFFFFFFull) return NDFL_E_UNSUPPORTED;
+    const uint32_t nch = (uint32_t)nch64;
+    hipStream_t s = c->stream;
+
+    // input
+    const uint8_t* d_data = data;
+    int prev_byte = -1;
+    if (hist_len > 0) {
+        if (flags & NDFL_IN_DEVICE) {
+            uint8_t pb = 0;
+            HIPCHK(hipMemcpyAsync(&pb, hist + hist_len - 1, 1, hipMemcpyDeviceToHost, s));
+            HIPCHK(hipStreamSynchronize(s));
+            prev_byte = pb;
+        } else {
+            prev_byte = hist[hist_len - 1];
+        }
+    }
+    if (!(flags & NDFL_IN_DEVICE) && len) {
+        HIPCHK(c->d_in.ensure(len));
+        HIPCHK(hipMemcpyAsync(c->d_in.p, data, len, hipMemcpyHostToDevice, s));
+        d_data = c->d_in.as<uint8_t>();
+    }
+    // output
+    const uint64_t bound = ndfl_deflate_bound(len, chunk_len);
+    const uint64_t bound_words = (bound + 3) / 4 + 2;
+    uint32_t* d_out;
+    bool direct = (flags & NDFL_OUT_DEVICE) && (((uintptr_t)out & 3) == 0) && out_cap >= bound_words * 4;
+    if (direct) d_out = (uint32_t*)out;
+    else { HIPCHK(c->d_out.ensure(bound_words * 4)); d_out = c->d_out.as<uint32_t>(); }
+    HIPCHK(c->d_status.ensure(nch * sizeof(uint64_t)));
+    HIPCHK(c->d_ticket.ensure(64));
+    HIPCHK(c->d_edge_w.ensure(2ull * nch * sizeof(uint64_t)));
+    HIPCHK(c->d_edge_v.ensure(2ull * nch * sizeof(uint32_t)));
+    if (crc_inout) { HIPCHK(c->d_crc.ensure(nch * sizeof(uint32_t))); HIPCHK(c->d_crc1.ensure(64)); }
+    HIPCHK(hipMemsetAsync(c->d_status.p, 0, nch * sizeof(uint64_t), s));
+    HIPCHK(hipMemsetAsync(c->d_ticket.p, 0, 64, s));
+
+    Args a;
+    a.in = d_data; a.n = len; a.chunk_len = chunk_len; a.nchunks = nch;
+    a.prev_byte = prev_byte; a.hist_enabled = hist_limit > 0; a.final_last = final_flag ? 1 : 0;
+    a.rle = rle; a.dynamic = dyn; a.base_bit = start_bitpos;
+    a.out = d_out; a.status = c->d_status.as<uint64_t>(); a.ticket = c->d_ticket.as<uint32_t>();
+    a.edge_w = c->d_edge_w.as<uint64_t>(); a.edge_v = c->d_edge_v.as<uint32_t>();
+    a.chunk_bits = nullptr;
+    a.crc_raw = crc_inout ? c->d_crc.as<uint32_t>() : nullptr;
+    a.crc_tab = c->d_tabs.as<uint32_t>();
+    a.crc_x = c->d_tabs.as<uint32_t>() + 1024;
+    HIPCHK(hipEventRecord(c->ev0, s));
+    hipLaunchKernelGGL(ndfl_deflate_chunks_kernel, dim3(nch), dim3(1024), 0, s, a);
+    HIPCHK(hipGetLastError());
+    HIPCHK(hipEventRecord(c->ev1, s));
+    const uint32_t ne = 2 * nch;
+    hipLaunchKernelGGL(ndfl_edge_fixup_kernel, dim3((ne + 255) / 256), dim3(256), 0, s,
+                       (const uint64_t*)a.edge_w, (const uint32_t*)a.edge_v, ne, d_out);
+    HIPCHK(hipGetLastError());
+    if (crc_inout) {
+        hipLaunchKernelGGL(ndfl_crc_combine_kernel, dim3(1), dim3(1024), 0, s,
+                           (const uint32_t*)a.crc_raw, nch, chunk_len, len, c->d_crc1.as<uint32_t>());
+        HIPCHK(hipGetLastError());
+        HIPCHK(hipMemcpyAsync(c->h_pinned + 4, c->d_crc1.p, 4, hipMemcpyDeviceToHost, s));
+    }
+    HIPCHK(hipMemcpyAsync(c->h_pinned, a.status + (nch - 1), 8, hipMemcpyDeviceToHost, s));
+    HIPCHK(hipStreamSynchronize(s));
+    float ms = 0;
+    hipEventElapsedTime(&ms, c->ev0, c->ev1);
+    c->last_ms = ms;
+    uint64_t st;
+    memcpy(&st, c->h_pinned, 8);
+    const uint64_t end_bits = st & ST_VAL;
+    *out_end_bits = end_bits;
+    const uint64_t nbytes = (end_bits + 7) / 8;
+    if (crc_inout) {
+        uint32_t raw = c->h_pinned[4];
+        uint32_t dc = ~(crc_multmodp(crc_x8n(len), 0xFFFFFFFFu) ^ raw);
+        *crc_inout = ndfl_crc32_combine(*crc_inout, dc, len);
+    }
+    if (!direct) {
+        if (nbytes > out_cap) return NDFL_E_CAPACITY;
+        HIPCHK(hipMemcpyAsync(out, d_out, nbytes,
+                              (flags & NDFL_OUT_DEVICE) ? hipMemcpyDeviceToDevice : hipMemcpyDeviceToHost, s));
+        HIPCHK(hipStreamSynchronize(s));
+    }
+    return NDFL_OK;
+}
+
+int ndfl_crc32(ndfl_ctx* c, uint32_t* crc_inout, const uint8_t* data, uint64_t len, uint32_t flags) {
+    if (!c || !crc_inout || (!data && len)) return NDFL_E_ARG;
+    if (len == 0) return NDFL_OK;
+    HIPCHK(hipSetDevice(c->device));
+    hipStream_t s = c->stream;
+    const uint8_t* d = data;
+    if (!(flags & NDFL_IN_DEVICE)) {
+        HIPCHK(c->d_in.ensure(len));
+        HIPCHK(hipMemcpyAsync(c->d_in.p, data, len, hipMemcpyHostToDevice, s));
+        d = c->d_in.as<uint8_t>();
+    }
+    const uint64_t nseg = (len + 65535) / 65536;
+    HIPCHK(c->d_crc.ensure(nseg * 4));
+    HIPCHK(c->d_crc1.ensure(64));
+    HIPCHK(hipEventRecord(c->ev0, s));
+    hipLaunchKernelGGL(ndfl_crc_segments_kernel, dim3((uint32_t)nseg), dim3(1024), 0, s, d, len,
+                       (const uint32_t*)c->d_tabs.as<uint32_t>(), (const uint32_t*)(c->d_tabs.as<uint32_t>() + 1024),
+                       c->d_crc.as<uint32_t>());
+    HIPCHK(hipGetLastError());
+    HIPCHK(hipEventRecord(c->ev1, s));
+    hipLaunchKernelGGL(ndfl_crc_combine_kernel, dim3(1), dim3(1024), 0, s, (const uint32_t*)c->d_crc.as<uint32_t>(),
+                       (uint32_t)nseg, 65536u, len, c->d_crc1.as<uint32_t>());
+    HIPCHK(hipGetLastError());
+    HIPCHK(hipMemcpyAsync(c->h_pinned, c->d_crc1.p, 4, hipMemcpyDeviceToHost, s));
+    HIPCHK(hipStreamSynchronize(s));
+    float ms = 0;
+    hipEventElapsedTime(&ms, c->ev0, c->ev1);
+    c->last_ms = ms;
+    uint32_t raw = c->h_pinned[0];
+    uint32_t dc = ~(crc_multmodp(crc_x8n(len), 0xFFFFFFFFu) ^ raw);
+    *crc_inout = ndfl_crc32_combine(*crc_inout, dc, len);
+    return NDFL_OK;
+}
+
+int ndfl_inflate(ndfl_ctx* c, const uint8_t* in, uint64_t in_len, uint8_t* out, uint64_t out_cap,
+                 uint64_t* out_len, uint64_t* consumed_bits, uint32_t flags) {
+    if (!c || !out_len || !consumed_bits || (!in && in_len)) return NDFL_E_ARG;
+    HIPCHK(hipSetDevice(c->device));
+    return inflate_run(c->inf, c->stream, in, in_len, out, out_cap, out_len, consumed_bits, flags,
+                       c->ev0, c->ev1, &c->last_ms);
+}
+
+}  // extern "C"

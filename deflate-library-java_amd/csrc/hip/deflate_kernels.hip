@@ -1,0 +1,738 @@
+// deflate_kernels.hip -- MI355X (gfx950) DEFLATE block encoder.
+//
+// Replaces the per-chunk loop DeflaterOutputStream.writeBuffer -> Lz77Huffman.decide/compressTo
+// -> BitOut.writeBits (D/DeflaterOutputStream.java:119-171, D/comp/Lz77Huffman.java:42-286) for
+// the RLE_* and LITERAL_* presets.  One 1024-thread workgroup encodes one chunk (<= 64 KiB) in a
+// single pass over HBM:
+//   1. the chunk is loaded once into registers (64 B per lane, 16-B loads) and CRC-32'd there;
+//   2. run pieces are found with a ballot-free bitmask per lane + a block suffix-min;
+//   3. the greedy RLE parse is evaluated in closed form per run piece into LDS
+//      histograms;
+//   4. length-limited package-merge (exact reference tie order: packages before leaves on equal
+//      frequency, D/comp/Lz77Huffman.java:319-333) runs as parallel merge-path levels + a prefix
+//      backtrack; canonical codes are built from per-length bitmasks;
+//   5. each lane's token bits are block-scanned; the chunk's global bit offset comes from a
+//      decoupled look-back over per-chunk status words (chunk ids from an atomic ticket, so a
+//      workgroup only ever waits on workgroups that already started);
+//   6. tokens are packed into a word-aligned LDS bit buffer with LDS atomicOr and streamed out
+//      with coalesced stores; the two boundary words of each chunk go to an edge list merged by
+//      ndfl_edge_fixup.
+// D/ = /root/reference/src/io/nayuki/deflate/
+#include "ndfl_common.hpp"
+
+namespace {
+
+constexpr int DT = 1024;                  // threads per workgroup
+constexpr int NW = DT / 64;               // waves per workgroup
+constexpr int MAX_CHUNK = 65536;
+constexpr int OUTW = 18600;               // LDS bit-buffer words (>= 594,362 bits)
+
+constexpr uint64_t ST_AGG = 1ull << 62;
+constexpr uint64_t ST_PRE = 2ull << 62;
+constexpr uint64_t ST_VAL = (1ull << 62) - 1;
+
+// ---- LDS layout (bytes) -------------------------------------------------------------------
+// [0, OUTW*4)          bit buffer; during code construction it is overlaid by scratch below
+// then persistent small arrays.
+constexpr int SCR_HLIT = 0;                         // u32[288] literal/length histogram
+constexpr int SCR_HDIST = SCR_HLIT + 288 * 4;       // u32[32]
+constexpr int SCR_LAST = SCR_HDIST + 32 * 4;        // u8[1024] last byte of each lane
+constexpr int SCR_KEY = SCR_LAST + 1024;            // u32[288]
+constexpr int SCR_LF = SCR_KEY + 288 * 4;           // u32[288] sorted leaf freq
+constexpr int SCR_LS = SCR_LF + 288 * 4;            // u32[288] sorted leaf symbol
+constexpr int SCR_PFA = SCR_LS + 288 * 4;           // u32[304] packages
+constexpr int SCR_PFB = SCR_PFA + 304 * 4;          // u32[304]
+constexpr int SCR_MF = SCR_PFB + 304 * 4;           // u32[608] merged list
+constexpr int SCR_MPK = SCR_MF + 608 * 4;           // u32[15][20] is-package bits per level
+constexpr int SCR_LVL = SCR_MPK + 15 * 20 * 4;      // u32[16] leaves per level
+constexpr int SCR_LEN = SCR_LVL + 16 * 4;           // u8[320] code lengths (lit ++ dist)
+constexpr int SCR_CLLEN = SCR_LEN + 320;            // u8[32] code-length-code lengths
+constexpr int SCR_BLC = SCR_CLLEN + 32;             // u32[16] bl_count
+constexpr int SCR_NXC = SCR_BLC + 16 * 4;           // u32[16] next code
+constexpr int SCR_MASK = SCR_NXC + 16 * 4;          // u32[16][10] symbols-by-length bitmask
+constexpr int SCR_CLH = SCR_MASK + 16 * 10 * 4;     // u32[20] code-length histogram
+constexpr int SCR_MISC = SCR_CLH + 20 * 4;          // u32[16]
+constexpr int SCR_END = SCR_MISC + 16 * 4;
+static_assert(SCR_END <= OUTW * 4, "scratch must fit in the bit buffer");
+
+struct Persist {
+    uint32_t litCode[288];    // rev(code) | len << 16
+    uint32_t distCode[32];
+    uint32_t clCode[20];
+    uint8_t clSym[320];
+    uint8_t clExtra[320];
+    uint16_t clOff[320];      // bit offset of each code-length symbol inside the header body
+    uint64_t scan64[NW];
+    uint32_t scan32[NW];
+    uint32_t chunk;           // ticket
+    uint32_t nsym, ncl, hlit, hdist;
+    uint32_t hdrBits;         // total header bits (incl. bfinal/btype)
+    uint32_t clBodyBits;
+    uint64_t P;               // chunk global bit offset
+    uint32_t crcAcc[NW];
+};
+
+struct Args {
+    const uint8_t* in;        // data region of this call (device)
+    uint64_t n;
+    uint32_t chunk_len;
+    uint32_t nchunks;
+    int32_t prev_byte;        // byte preceding chunk 0, or -1 if none (no history)
+    int32_t hist_enabled;     // historyLookbehindLimit > 0
+    int32_t final_last;       // last chunk is bfinal
+    int32_t rle;              // 1: RLE preset (dist 1, runs 3..258); 0: LITERAL preset
+    int32_t dynamic;
+    uint32_t base_bit;        // bit offset of chunk 0 in `out` (0..7)
+    uint32_t* out;            // word-aligned output, words [0, ...)
+    uint64_t* status;         // [nchunks], zeroed
+    uint32_t* ticket;         // zeroed
+    uint64_t* edge_w;         // [2*nchunks]
+    uint32_t* edge_v;         // [2*nchunks]
+    uint64_t* chunk_bits;     // optional [nchunks]
+    uint32_t* crc_raw;        // optional [nchunks]
+    const uint32_t* crc_tab;  // slicing-by-4 tables (1024 u32)
+    const uint32_t* crc_x;    // x^(8k) k<64 then x^(8*64k) k<1024
+};
+
+__device__ __forceinline__ uint32_t byte_at(const uint32_t (&w)[16], int i) {
+    // select tree over 16 registers (i is lane-divergent)
+    const int wi = i >> 2;
+    uint32_t a0 = (wi & 1) ? w[1] : w[0],  a1 = (wi & 1) ? w[3] : w[2];
+    uint32_t a2 = (wi & 1) ? w[5] : w[4],  a3 = (wi & 1) ? w[7] : w[6];
+    uint32_t a4 = (wi & 1) ? w[9] : w[8],  a5 = (wi & 1) ? w[11] : w[10];
+    uint32_t a6 = (wi & 1) ? w[13] : w[12], a7 = (wi & 1) ? w[15] : w[14];
+    uint32_t b0 = (wi & 2) ? a1 : a0, b1 = (wi & 2) ? a3 : a2, b2 = (wi & 2) ? a5 : a4, b3 = (wi & 2) ? a7 : a6;
+    uint32_t c0 = (wi & 4) ? b1 : b0, c1 = (wi & 4) ? b3 : b2;
+    uint32_t d = (wi & 8) ? c1 : c0;
+    return (d >> ((i & 3) * 8)) & 0xFFu;
+}
+
+// Length symbol / extra bits of a run 3..258 (D/comp/Lz77Huffman.java:92-111).
+__device__ __forceinline__ void run_sym(uint32_t run, uint32_t& sym, uint32_t& ne, uint32_t& ex) {
+    if (run < 11) { sym = run + 254; ne = 0; ex = 0; }
+    else if (run == 258) { sym = 285; ne = 0; ex = 0; }
+    else {
+        uint32_t r = run - 3;
+        ne = 29 - __clz(r);
+        sym = (ne << 2) + (r >> ne) + 257;
+        ex = r & ((1u << ne) - 1);
+    }
+}
+
+// ---- Package-merge code lengths (D/comp/Lz77Huffman.java:309-335) ---------------------------
+// hist: n entries (LDS).  Writes lens[0..n) (LDS, u8).  All threads must call.
+__device__ void pm_lengths(const uint32_t* hist, int n, int L, uint8_t* lens, char* s) {
+    uint32_t* key = (uint32_t*)(s + SCR_KEY);
+    uint32_t* lf = (uint32_t*)(s + SCR_LF);
+    uint32_t* ls = (uint32_t*)(s + SCR_LS);
+    uint32_t* pfA = (uint32_t*)(s + SCR_PFA);
+    uint32_t* pfB = (uint32_t*)(s + SCR_PFB);
+    uint32_t* mf = (uint32_t*)(s + SCR_MF);
+    uint32_t* mpk = (uint32_t*)(s + SCR_MPK);
+    uint32_t* lvl = (uint32_t*)(s + SCR_LVL);
+    uint32_t* misc = (uint32_t*)(s + SCR_MISC);
+    const int tid = threadIdx.x;
+    if (tid < n) {
+        uint32_t f = hist[tid];
+        key[tid] = f ? (f << 9 | (uint32_t)tid) : 0xFFFFFFFFu;
+    }
+    if (tid < 15 * 20) mpk[tid] = 0;
+    __syncthreads();
+    // leaves sorted by (freq, symbol): rank by counting (n <= 288, broadcast LDS reads)
+    uint32_t nl = 0;
+    for (int j = 0; j < n; j++) nl += key[j] != 0xFFFFFFFFu;   // uniform
+    if (tid < n) {
+        uint32_t k = key[tid];
+        if (k != 0xFFFFFFFFu) {
+            uint32_t r = 0;
+            for (int j = 0; j < n; j++) r += key[j] < k;
+            lf[r] = k >> 9;
+            ls[r] = (uint32_t)tid;
+        }
+        lens[tid] = 0;
+    }
+    __syncthreads();
+    if (nl < 2) return;   // all zero lengths (callers never reach this for litlen/dist)
+    uint32_t np = 0;
+    uint32_t* pf = pfA;
+    uint32_t* pfn = pfB;
+    for (int it = 0; it < L; it++) {
+        const uint32_t m = np + nl;
+        if ((uint32_t)tid < m) {
+            uint32_t f, pos;
+            bool isp = (uint32_t)tid < np;
+            if (isp) {
+                f = pf[tid];
+                // # leaves with freq < f
+                uint32_t lo = 0, hi = nl;
+                while (lo < hi) { uint32_t mid = (lo + hi) >> 1; if (lf[mid] < f) lo = mid + 1; else hi = mid; }
+                pos = (uint32_t)tid + lo;
+            } else {
+                uint32_t r = (uint32_t)tid - np;
+                f = lf[r];
+                // # packages with freq <= f
+                uint32_t lo = 0, hi = np;
+                while (lo < hi) { uint32_t mid = (lo + hi) >> 1; if (pf[mid] <= f) lo = mid + 1; else hi = mid; }
+                pos = r + lo;
+            }
+            mf[pos] = f;
+            if (isp) atomicOr(&mpk[it * 20 + (pos >> 5)], 1u << (pos & 31));
+        }
+        __syncthreads();
+        const uint32_t np2 = m >> 1;
+        if ((uint32_t)tid < np2) pfn[tid] = mf[2 * tid] + mf[2 * tid + 1];
+        __syncthreads();
+        np = np2;
+        uint32_t* t = pf; pf = pfn; pfn = t;
+    }
+    // backtrack: prefix of 2(nl-1) items at the last level; leaves in the prefix of each level.
+    if (tid < 64) {
+        uint32_t m = 2 * (nl - 1);
+        for (int it = L - 1; it >= 0; it--) {
+            uint32_t cnt = 0;
+            if (tid < 20) {
+                uint32_t w = mpk[it * 20 + tid];
+                uint32_t lo = (uint32_t)tid * 32;
+                if (lo + 32 <= m) cnt = __popc(w);
+                else if (lo < m) cnt = __popc(w & ((1u << (m - lo)) - 1));
+            }
+            cnt = wave_sum(cnt);
+            if (tid == 0) lvl[it] = m - cnt;
+            m = 2 * cnt;
+        }
+    }
+    __syncthreads();
+    if ((uint32_t)tid < nl) {
+        uint32_t c = 0;
+        for (int it = 0; it < L; it++) c += (uint32_t)tid < lvl[it];
+        lens[ls[tid]] = (uint8_t)c;
+    }
+    (void)misc;
+    __syncthreads();
+}
+
+// Canonical codes (D/comp/Lz77Huffman.java:368-391): rev(code) | len << 16.
+__device__ void canon_codes(const uint8_t* lens, int n, uint32_t* codes, char* s) {
+    uint32_t* blc = (uint32_t*)(s + SCR_BLC);
+    uint32_t* nxc = (uint32_t*)(s + SCR_NXC);
+    uint32_t* mask = (uint32_t*)(s + SCR_MASK);
+    const int tid = threadIdx.x;
+    if (tid < 16) blc[tid] = 0;
+    if (tid < 160) mask[tid] = 0;
+    __syncthreads();
+    if (tid < n) {
+        uint32_t l = lens[tid];
+        if (l) {
+            atomicAdd(&blc[l], 1u);
+            atomicOr(&mask[l * 10 + (tid >> 5)], 1u << (tid & 31));
+        }
+    }
+    __syncthreads();
+    if (tid == 0) {
+        uint32_t code = 0;
+        blc[0] = 0;
+        for (int b = 1; b < 16; b++) { code = (code + blc[b - 1]) << 1; nxc[b] = code; }
+    }
+    __syncthreads();
+    if (tid < n) {
+        uint32_t l = lens[tid];
+        uint32_t c = 0;
+        if (l) {
+            uint32_t rank = 0;
+            const int wi = tid >> 5;
+            for (int w = 0; w < wi; w++) rank += __popc(mask[l * 10 + w]);
+            rank += __popc(mask[l * 10 + wi] & ((1u << (tid & 31)) - 1));
+            uint32_t code = nxc[l] + rank;
+            c = (__brev(code) >> (32 - l)) | (l << 16);
+        }
+        codes[tid] = c;
+    }
+    __syncthreads();
+}
+
+struct BitPut {
+    uint64_t acc;
+    uint32_t nb;
+    uint32_t wi;
+    uint32_t* buf;
+    __device__ __forceinline__ void init(uint32_t* b, uint32_t bitpos) { buf = b; wi = bitpos >> 5; nb = bitpos & 31; acc = 0; }
+    __device__ __forceinline__ void put(uint32_t v, uint32_t n) {
+        acc |= (uint64_t)v << nb;
+        nb += n;
+        if (nb >= 32) {
+            atomicOr(&buf[wi], (uint32_t)acc);
+            wi++;
+            acc >>= 32;
+            nb -= 32;
+        }
+    }
+    __device__ __forceinline__ void flush() {
+        if (nb) atomicOr(&buf[wi], (uint32_t)acc);
+    }
+};
+
+constexpr uint32_t CL_EXTRA_BITS[3] = {2, 3, 7};
+
+}  // namespace
+
+extern "C" __global__ void __launch_bounds__(DT, 8)
+ndfl_deflate_chunks_kernel(Args a) {
+    __shared__ __attribute__((aligned(16))) uint32_t obuf[OUTW];
+    __shared__ Persist ps;
+    char* scr = (char*)obuf;
+    uint32_t* hlit = (uint32_t*)(scr + SCR_HLIT);
+    uint32_t* hdist = (uint32_t*)(scr + SCR_HDIST);
+    uint8_t* lastb = (uint8_t*)(scr + SCR_LAST);
+    uint8_t* lens = (uint8_t*)(scr + SCR_LEN);
+    uint8_t* clLen = (uint8_t*)(scr + SCR_CLLEN);
+    uint32_t* clh = (uint32_t*)(scr + SCR_CLH);
+    uint32_t* misc = (uint32_t*)(scr + SCR_MISC);
+
+    const int tid = threadIdx.x;
+    const int lane = tid & 63, wid = tid >> 6;
+
+    if (tid == 0) ps.chunk = atomicAdd(a.ticket, 1u);
+    if (tid < 288) hlit[tid] = 0;
+    if (tid < 32) hdist[tid] = 0;
+    __syncthreads();
+    const uint32_t c = ps.chunk;
+    const uint64_t cs = (uint64_t)c * a.chunk_len;
+    const uint32_t len_c = (uint32_t)min((uint64_t)a.chunk_len, a.n - cs);
+    const bool is_final = a.final_last && (c + 1 == a.nchunks);
+    const uint8_t* src = a.in + cs;
+
+    // ---- 1. load 64 bytes per lane into registers --------------------------------------------
+    uint32_t w[16];
+    const uint32_t t0 = (uint32_t)tid * 64;
+    const int vcnt = (int)min(64u, len_c > t0 ? len_c - t0 : 0u);
+    if (vcnt == 64 && (((uintptr_t)(src + t0)) & 15) == 0) {
+        const u32x4* p = (const u32x4*)(src + t0);
+#pragma unroll
+        for (int k = 0; k < 4; k++) {
+            u32x4 v = __builtin_nontemporal_load(p + k);
+            w[4 * k] = v.x; w[4 * k + 1] = v.y; w[4 * k + 2] = v.z; w[4 * k + 3] = v.w;
+        }
+    } else {
+#pragma unroll
+        for (int k = 0; k < 16; k++) {
+            uint32_t x = 0;
+#pragma unroll
+            for (int b = 0; b < 4; b++) {
+                int i = 4 * k + b;
+                if (i < vcnt) x |= (uint32_t)src[t0 + i] << (8 * b);
+            }
+            w[k] = x;
+        }
+    }
+    if (vcnt > 0) lastb[tid] = (uint8_t)byte_at(w, vcnt - 1);
+
+    // ---- CRC-32 (raw, init 0) of this lane's bytes, combined across the chunk ----------------
+    if (a.crc_raw) {
+        uint32_t cr = 0;
+        const uint32_t* T0 = a.crc_tab;
+        const uint32_t* T1 = a.crc_tab + 256;
+        const uint32_t* T2 = a.crc_tab + 512;
+        const uint32_t* T3 = a.crc_tab + 768;
+        const int nfull = vcnt >> 2;
+#pragma unroll
+        for (int k = 0; k < 16; k++) {
+            if (k < nfull) {
+                uint32_t x = cr ^ w[k];
+                cr = T3[x & 0xFF] ^ T2[(x >> 8) & 0xFF] ^ T1[(x >> 16) & 0xFF] ^ T0[x >> 24];
+            }
+        }
+        for (int i = nfull * 4; i < vcnt; i++) cr = T0[(cr ^ byte_at(w, i)) & 0xFF] ^ (cr >> 8);
+        uint32_t contrib = 0;
+        if (vcnt > 0) {
+            // shift by the bytes that follow this lane inside the chunk
+            const uint32_t after = len_c - (t0 + (uint32_t)vcnt);
+            const uint32_t q = after & 63, k64 = after >> 6;
+            uint32_t sh = a.crc_x[64 + k64];
+            if (q) sh = crc_multmodp(a.crc_x[q], sh);
+            contrib = crc_multmodp(sh, cr);
+        }
+        contrib = wave_xor(contrib);
+        if (lane == 0) ps.crcAcc[wid] = contrib;
+    }
+    __syncthreads();
+    if (a.crc_raw && tid == 0) {
+        uint32_t x = 0;
+        for (int k = 0; k < NW; k++) x ^= ps.crcAcc[k];
+        a.crc_raw[c] = x;
+    }
+
+    // ---- 2. run pieces ------------------------------------------------------------------------
+    const bool has_prev0 = (c > 0) ? (a.hist_enabled != 0) : (a.prev_byte >= 0);
+    const uint32_t prev0 = (c > 0) ? (uint32_t)src[-1] : (uint32_t)(a.prev_byte & 0xFF);
+    uint64_t F = 0;
+    if (vcnt > 0) {
+        uint32_t prev = tid > 0 ? (uint32_t)lastb[tid - 1] : 0u;
+        if (!a.rle) {
+            F = vcnt == 64 ? ~0ull : ((1ull << vcnt) - 1);
+        } else {
+#pragma unroll
+            for (int i = 0; i < 64; i++) {
+                uint32_t b = (w[i >> 2] >> ((i & 3) * 8)) & 0xFF;
+                bool st = (i == 0 && tid == 0) || b != prev;
+                if (i < vcnt && st) F |= 1ull << i;
+                prev = b;
+            }
+        }
+    }
+    const uint32_t firstStart = F ? t0 + (uint32_t)__builtin_ctzll(F) : 0xFFFFFFFFu;
+    const uint32_t nextStart = min(block_excl_suffix_min<NW>(firstStart, 0xFFFFFFFFu, ps.scan32), len_c);
+
+    // piece visitor: (start_local, length, value, lead)
+    auto lead_of = [&](uint32_t gpos, uint32_t v) -> uint32_t {
+        if (!a.rle) return 1u;
+        if (gpos == 0) return (has_prev0 && prev0 == v) ? 0u : 1u;
+        return 1u;
+    };
+
+    // ---- 3. histograms (closed-form greedy parse per piece, App. A.2) -------------------------
+    {
+        uint64_t Fm = F;
+        while (Fm) {
+            const int i = __builtin_ctzll(Fm);
+            Fm &= Fm - 1;
+            const uint32_t pend = Fm ? t0 + (uint32_t)__builtin_ctzll(Fm) : nextStart;
+            const uint32_t gpos = t0 + (uint32_t)i;
+            const uint32_t v = byte_at(w, i);
+            const uint32_t plen = pend - gpos;
+            const uint32_t lead = lead_of(gpos, v);
+            if (!a.rle) { atomicAdd(&hlit[v], 1u); continue; }
+            const uint32_t R = plen - lead;
+            const uint32_t n258 = R / 258, m = R % 258;
+            uint32_t nlit = lead + (m < 3 ? m : 0);
+            if (nlit) atomicAdd(&hlit[v], nlit);
+            if (n258) atomicAdd(&hlit[285], n258);
+            uint32_t nd = n258;
+            if (m >= 3) {
+                uint32_t sym, ne, ex; run_sym(m, sym, ne, ex);
+                atomicAdd(&hlit[sym], 1u);
+                nd++;
+            }
+            if (nd) atomicAdd(&hdist[0], nd);
+        }
+    }
+    if (tid == 0) {
+        atomicAdd(&hlit[256], 1u);                          // end of block (:131-132)
+        if (a.dynamic && len_c == 0) atomicAdd(&hlit[0], 1u);  // (:146-147)
+    }
+    __syncthreads();
+
+    // ---- 4. code construction -------------------------------------------------------------------
+    if (!a.dynamic) {
+        // fixed codes (D/comp/Lz77Huffman.java:394-410)
+        if (tid < 288) {
+            uint32_t l = tid < 144 ? 8 : tid < 256 ? 9 : tid < 280 ? 7 : 8;
+            uint32_t code = tid < 144 ? 0x30 + tid : tid < 256 ? 0x190 + (tid - 144) : tid < 280 ? (tid - 256) : 0xC0 + (tid - 280);
+            ps.litCode[tid] = (__brev(code) >> (32 - l)) | (l << 16);
+        }
+        if (tid < 32) ps.distCode[tid] = (__brev((uint32_t)tid) >> 27) | (5u << 16);
+        if (tid == 0) { ps.hdrBits = 3; ps.nsym = 0; }
+        __syncthreads();
+    } else {
+        // trim litlen histogram, keep >= 257 (:148-151)
+        if (tid == 0) {
+            int ln = 286;
+            while (ln > 257 && hlit[ln - 1] == 0) ln--;
+            misc[0] = (uint32_t)ln;
+            // single used distance code -> dummy neighbour (:155-171)
+            int used = 0, first = -1;
+            for (int i = 0; i < 30; i++) if (hdist[i]) { used++; if (first < 0) first = i; }
+            if (used == 1) { if (first < 29) hdist[first + 1] = 1; else hdist[first - 1] = 1; }
+            int dn = 30;
+            while (dn > 1 && hdist[dn - 1] == 0) dn--;
+            misc[1] = (uint32_t)dn;
+            misc[2] = (dn == 1 && hdist[0] == 0) ? 1u : 0u;   // empty distance code
+        }
+        __syncthreads();
+        const int ln = (int)misc[0], dn = (int)misc[1];
+        const bool emptyDist = misc[2] != 0;
+        pm_lengths(hlit, ln, 15, lens, scr);
+        if (emptyDist) { if (tid == 0) lens[ln] = 0; __syncthreads(); }
+        else pm_lengths(hdist, dn, 15, lens + ln, scr);
+        canon_codes(lens, ln, ps.litCode, scr);
+        canon_codes(lens + ln, dn, ps.distCode, scr);
+        // code-length sequence RLE (:187-223) as maximal-run decomposition
+        const int nc = ln + dn;
+        uint32_t rstart = 0xFFFFFFFFu;
+        uint32_t v = 0;
+        if (tid < nc) {
+            v = lens[tid];
+            if (tid == 0 || lens[tid - 1] != v) rstart = (uint32_t)tid;
+        }
+        uint32_t rnext = min(block_excl_suffix_min<NW>(rstart, 0xFFFFFFFFu, ps.scan32), (uint32_t)nc);
+        uint32_t cnt = 0, Z = 0;
+        if (rstart != 0xFFFFFFFFu) {
+            Z = rnext - rstart;
+            if (v == 0) {
+                uint32_t q = Z / 138, r = Z % 138;
+                cnt = q + (r >= 3 ? 1 : r);
+            } else {
+                uint32_t rest = Z - 1, q = rest / 6, r = rest % 6;
+                cnt = 1 + q + (r >= 3 ? 1 : r);
+            }
+        }
+        uint32_t tot;
+        uint32_t off = block_excl_scan<uint32_t, NW>(cnt, ps.scan32, tot);
+        if (rstart != 0xFFFFFFFFu) {
+            uint32_t k = off;
+            if (v == 0) {
+                uint32_t L = Z;
+                while (L > 0) {
+                    uint32_t r = min(L, 138u);
+                    if (r < 3) { ps.clSym[k] = 0; ps.clExtra[k++] = 0; L -= 1; }
+                    else if (r < 11) { ps.clSym[k] = 17; ps.clExtra[k++] = (uint8_t)(r - 3); L -= r; }
+                    else { ps.clSym[k] = 18; ps.clExtra[k++] = (uint8_t)(r - 11); L -= r; }
+                }
+            } else {
+                ps.clSym[k] = (uint8_t)v; ps.clExtra[k++] = 0;
+                uint32_t L = Z - 1;
+                while (L >= 3) { uint32_t r = min(L, 6u); ps.clSym[k] = 16; ps.clExtra[k++] = (uint8_t)(r - 3); L -= r; }
+                while (L > 0) { ps.clSym[k] = (uint8_t)v; ps.clExtra[k++] = 0; L--; }
+            }
+        }
+        if (tid < 20) clh[tid] = 0;
+        __syncthreads();
+        if ((uint32_t)tid < tot) atomicAdd(&clh[ps.clSym[tid]], 1u);
+        __syncthreads();
+        pm_lengths(clh, 19, 7, clLen, scr);
+        canon_codes(clLen, 19, ps.clCode, scr);
+        // per-symbol header bit offsets
+        uint32_t sb = 0;
+        if ((uint32_t)tid < tot) {
+            uint32_t sy = ps.clSym[tid];
+            sb = (ps.clCode[sy] >> 16) + (sy >= 16 ? CL_EXTRA_BITS[sy - 16] : 0);
+        }
+        uint32_t body;
+        uint32_t so = block_excl_scan<uint32_t, NW>(sb, ps.scan32, body);
+        if ((uint32_t)tid < tot) ps.clOff[tid] = (uint16_t)so;
+        if (tid == 0) {
+            const int order[19] = {16, 17, 18, 0, 8, 7, 9, 6, 10, 5, 11, 4, 12, 3, 13, 2, 14, 1, 15};
+            int ncl = 19;
+            while (ncl > 4 && clLen[order[ncl - 1]] == 0) ncl--;    // (:230-234)
+            ps.ncl = (uint32_t)ncl;
+            ps.nsym = tot;
+            ps.hlit = (uint32_t)(ln - 257);
+            ps.hdist = (uint32_t)(dn - 1);
+            ps.clBodyBits = body;
+            ps.hdrBits = 3 + 14 + 3 * (uint32_t)ncl + body;
+            // stash reordered code-length-code lengths in misc[4..] (3 bits each, packed)
+            uint64_t packed = 0;
+            for (int i = 0; i < ncl; i++) packed |= (uint64_t)clLen[order[i]] << (3 * i);
+            misc[4] = (uint32_t)packed; misc[5] = (uint32_t)(packed >> 32);
+        }
+        __syncthreads();
+    }
+    const uint32_t packedLo = misc[4], packedHi = misc[5];
+    __syncthreads();
+
+    // ---- 5. token bits per lane, chunk size, decoupled look-back ------------------------------
+    const uint32_t d0 = ps.distCode[0];
+    const uint32_t c285 = ps.litCode[285];
+    uint32_t mybits = 0;
+    {
+        uint64_t Fm = F;
+        while (Fm) {
+            const int i = __builtin_ctzll(Fm);
+            Fm &= Fm - 1;
+            const uint32_t pend = Fm ? t0 + (uint32_t)__builtin_ctzll(Fm) : nextStart;
+            const uint32_t gpos = t0 + (uint32_t)i;
+            const uint32_t v = byte_at(w, i);
+            const uint32_t lv = ps.litCode[v] >> 16;
+            if (!a.rle) { mybits += lv; continue; }
+            const uint32_t lead = lead_of(gpos, v);
+            const uint32_t R = pend - gpos - lead;
+            const uint32_t n258 = R / 258, m = R % 258;
+            mybits += lead * lv + n258 * ((c285 >> 16) + (d0 >> 16));
+            if (m >= 3) {
+                uint32_t sym, ne, ex; run_sym(m, sym, ne, ex);
+                mybits += (ps.litCode[sym] >> 16) + ne + (d0 >> 16);
+            } else {
+                mybits += m * lv;
+            }
+        }
+    }
+    uint32_t tokTotal;
+    const uint32_t myoff = block_excl_scan<uint32_t, NW>(mybits, ps.scan32, tokTotal);
+    const uint32_t eobLen = ps.litCode[256] >> 16;
+    const uint32_t hdrBits = ps.hdrBits;
+    const uint64_t S = (uint64_t)hdrBits + tokTotal + eobLen;
+    if (tid == 0) {
+        uint64_t P;
+        if (c == 0) {
+            P = a.base_bit;
+            st_agent(&a.status[0], ST_PRE | (P + S));
+        } else {
+            st_agent(&a.status[c], ST_AGG | S);
+            uint64_t acc = 0;
+            int64_t j = (int64_t)c - 1;
+            for (;;) {
+                uint64_t st = ld_agent(&a.status[j]);
+                if (st & ST_PRE) { acc += st & ST_VAL; break; }
+                if (st & ST_AGG) { acc += st & ST_VAL; j--; continue; }
+                __builtin_amdgcn_s_sleep(1);
+            }
+            P = acc;
+            st_agent(&a.status[c], ST_PRE | (P + S));
+        }
+        ps.P = P;
+        if (a.chunk_bits) a.chunk_bits[c] = S;
+    }
+    // zero the bit buffer (scratch is dead from here on)
+    const uint32_t nwords = 0;  (void)nwords;
+    __syncthreads();
+    const uint64_t P = ps.P;
+    const uint32_t bit0 = (uint32_t)(P & 31);
+    const uint32_t nw = (uint32_t)((bit0 + S + 31) >> 5);
+    for (uint32_t k = (uint32_t)tid; k < nw; k += DT) obuf[k] = 0;
+    __syncthreads();
+
+    // ---- 6. emit ------------------------------------------------------------------------------
+    if (tid == 0) {
+        BitPut bp; bp.init(obuf, bit0);
+        bp.put(is_final ? 1u : 0u, 1);
+        bp.put(a.dynamic ? 2u : 1u, 2);
+        if (a.dynamic) {
+            bp.put(ps.hlit, 5);
+            bp.put(ps.hdist, 5);
+            bp.put(ps.ncl - 4, 4);
+            uint64_t packed = (uint64_t)packedLo | (uint64_t)packedHi << 32;
+            for (uint32_t i = 0; i < ps.ncl; i++) bp.put((uint32_t)(packed >> (3 * i)) & 7u, 3);
+        }
+        bp.flush();
+        // end-of-block symbol
+        BitPut be; be.init(obuf, bit0 + hdrBits + tokTotal);
+        be.put(ps.litCode[256] & 0xFFFF, eobLen);
+        be.flush();
+    }
+    if (a.dynamic && (uint32_t)tid < ps.nsym) {
+        const uint32_t sy = ps.clSym[tid];
+        BitPut bp; bp.init(obuf, bit0 + 17 + 3 * ps.ncl + ps.clOff[tid]);
+        bp.put(ps.clCode[sy] & 0xFFFF, ps.clCode[sy] >> 16);
+        if (sy >= 16) bp.put(ps.clExtra[tid], CL_EXTRA_BITS[sy - 16]);
+        bp.flush();
+    }
+    {
+        BitPut bp; bp.init(obuf, bit0 + hdrBits + myoff);
+        const uint32_t d0c = d0 & 0xFFFF, d0l = d0 >> 16;
+        const uint32_t m258 = (c285 & 0xFFFF) | (d0c << (c285 >> 16));
+        const uint32_t m258l = (c285 >> 16) + d0l;
+        uint64_t Fm = F;
+        while (Fm) {
+            const int i = __builtin_ctzll(Fm);
+            Fm &= Fm - 1;
+            const uint32_t pend = Fm ? t0 + (uint32_t)__builtin_ctzll(Fm) : nextStart;
+            const uint32_t gpos = t0 + (uint32_t)i;
+            const uint32_t v = byte_at(w, i);
+            const uint32_t lc = ps.litCode[v];
+            if (!a.rle) { bp.put(lc & 0xFFFF, lc >> 16); continue; }
+            const uint32_t lead = lead_of(gpos, v);
+            const uint32_t R = pend - gpos - lead;
+            const uint32_t n258 = R / 258, m = R % 258;
+            if (lead) bp.put(lc & 0xFFFF, lc >> 16);
+            for (uint32_t k = 0; k < n258; k++) bp.put(m258, m258l);
+            if (m >= 3) {
+                uint32_t sym, ne, ex; run_sym(m, sym, ne, ex);
+                const uint32_t sc = ps.litCode[sym];
+                bp.put(sc & 0xFFFF, sc >> 16);
+                bp.put(ex, ne);
+                bp.put(d0c, d0l);
+            } else {
+                for (uint32_t k = 0; k < m; k++) bp.put(lc & 0xFFFF, lc >> 16);
+            }
+        }
+        bp.flush();
+    }
+    __syncthreads();
+
+    // ---- 7. store: interior words directly, boundary words to the edge list ------------------
+    const uint64_t W0 = P >> 5;
+    for (uint32_t k = (uint32_t)tid + 1; k + 1 < nw; k += DT) a.out[W0 + k] = obuf[k];
+    if (tid == 0) {
+        a.edge_w[2 * c] = W0;
+        a.edge_v[2 * c] = obuf[0];
+        a.edge_w[2 * c + 1] = W0 + nw - 1;
+        a.edge_v[2 * c + 1] = nw > 1 ? obuf[nw - 1] : 0u;
+    }
+}
+
+// Merge the boundary words: every word touched by more than one chunk is the OR of all of them.
+extern "C" __global__ void ndfl_edge_fixup_kernel(const uint64_t* edge_w, const uint32_t* edge_v, uint32_t n_edges,
+                                                  uint32_t* out) {
+    uint32_t e = blockIdx.x * blockDim.x + threadIdx.x;
+    if (e >= n_edges) return;
+    uint64_t wv = edge_w[e];
+    if (e > 0 && edge_w[e - 1] == wv) return;
+    uint32_t v = 0;
+    for (uint32_t k = e; k < n_edges && edge_w[k] == wv; k++) v |= edge_v[k];
+    out[wv] = v;
+}
+
+// Combine per-chunk raw CRCs into the raw CRC of the call's data (x^(8*after) shifts).
+extern "C" __global__ void ndfl_crc_combine_kernel(const uint32_t* crc_raw, uint32_t nchunks, uint32_t chunk_len,
+                                                   uint64_t n, uint32_t* out_raw) {
+    __shared__ uint32_t red[16];
+    uint32_t acc = 0;
+    for (uint32_t c = threadIdx.x; c < nchunks; c += blockDim.x) {
+        uint64_t end = min((uint64_t)(c + 1) * chunk_len, n);
+        acc ^= crc_multmodp(crc_x8n(n - end), crc_raw[c]);
+    }
+    acc = wave_xor(acc);
+    if ((threadIdx.x & 63) == 0) red[threadIdx.x >> 6] = acc;
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        uint32_t x = 0;
+        for (uint32_t k = 0; k < blockDim.x / 64; k++) x ^= red[k];
+        *out_raw = x;
+    }
+}
+
+// Standalone CRC-32 (raw, init 0) of a device buffer: one 1024-thread workgroup per 64 KiB
+// segment, combined by ndfl_crc_combine_kernel.  Used on the decompress side (gunzip trailer).
+extern "C" __global__ void __launch_bounds__(1024)
+ndfl_crc_segments_kernel(const uint8_t* in, uint64_t n, const uint32_t* crc_tab, const uint32_t* crc_x,
+                         uint32_t* seg_raw) {
+    __shared__ uint32_t red[16];
+    const uint32_t seg = blockIdx.x;
+    const uint64_t s0 = (uint64_t)seg * 65536;
+    const uint32_t len = (uint32_t)min((uint64_t)65536, n - s0);
+    const uint32_t t0 = threadIdx.x * 64;
+    const int vcnt = (int)min(64u, len > t0 ? len - t0 : 0u);
+    const uint8_t* src = in + s0 + t0;
+    uint32_t cr = 0;
+    const uint32_t* T0 = crc_tab; const uint32_t* T1 = crc_tab + 256;
+    const uint32_t* T2 = crc_tab + 512; const uint32_t* T3 = crc_tab + 768;
+    if (vcnt == 64 && (((uintptr_t)src) & 15) == 0) {
+        const u32x4* p = (const u32x4*)src;
+#pragma unroll
+        for (int k = 0; k < 4; k++) {
+            u32x4 v = __builtin_nontemporal_load(p + k);
+            uint32_t ww[4] = {v.x, v.y, v.z, v.w};
+#pragma unroll
+            for (int j = 0; j < 4; j++) {
+                uint32_t x = cr ^ ww[j];
+                cr = T3[x & 0xFF] ^ T2[(x >> 8) & 0xFF] ^ T1[(x >> 16) & 0xFF] ^ T0[x >> 24];
+            }
+        }
+    } else {
+        for (int i = 0; i < vcnt; i++) cr = T0[(cr ^ src[i]) & 0xFF] ^ (cr >> 8);
+    }
+    uint32_t contrib = 0;
+    if (vcnt > 0) {
+        const uint32_t after = len - (t0 + (uint32_t)vcnt);
+        uint32_t sh = crc_x[64 + (after >> 6)];
+        if (after & 63) sh = crc_multmodp(crc_x[after & 63], sh);
+        contrib = crc_multmodp(sh, cr);
+    }
+    contrib = wave_xor(contrib);
+    if ((threadIdx.x & 63) == 0) red[threadIdx.x >> 6] = contrib;
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        uint32_t x = 0;
+        for (int k = 0; k < 16; k++) x ^= red[k];
+        seg_raw[seg] = x;
+    }
+}

@@ -1,0 +1,112 @@
+// ndfl_common.hpp -- shared device helpers for the MI355X (gfx950) DEFLATE kernels.
+// Wave64 throughout: every cross-lane idiom below assumes 64 lanes.
+#pragma once
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+#define NDFL_WAVE 64
+
+typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
+
+// CRC-32/ISO-HDLC (java.util.zip.CRC32) in the reflected domain.
+#define NDFL_CRC_POLY 0xEDB88320u
+
+// a*b mod P for reflected 32-bit polynomials (x^0 is the MSB).
+__host__ __device__ inline uint32_t crc_multmodp(uint32_t a, uint32_t b) {
+    uint32_t m = 1u << 31, p = 0;
+    for (;;) {
+        if (a & m) {
+            p ^= b;
+            if ((a & (m - 1)) == 0) break;
+        }
+        m >>= 1;
+        b = (b & 1) ? (b >> 1) ^ NDFL_CRC_POLY : b >> 1;
+    }
+    return p;
+}
+
+// x^(8*n) mod P.
+__host__ __device__ inline uint32_t crc_x8n(uint64_t n) {
+    uint32_t p = 1u << 31;          // x^0
+    uint32_t sq = 1u << 23;         // x^8
+    while (n) {
+        if (n & 1) p = crc_multmodp(sq, p);
+        sq = crc_multmodp(sq, sq);
+        n >>= 1;
+    }
+    return p;
+}
+
+// Wave-level inclusive scan (sum) over 64 lanes.
+template <typename T>
+__device__ inline T wave_incl_scan(T x) {
+    const int lane = threadIdx.x & 63;
+#pragma unroll
+    for (int o = 1; o < 64; o <<= 1) {
+        T y = __shfl_up(x, o, 64);
+        if (lane >= o) x += y;
+    }
+    return x;
+}
+
+template <typename T>
+__device__ inline T wave_sum(T x) {
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) x += __shfl_xor(x, o, 64);
+    return x;
+}
+
+template <typename T>
+__device__ inline T wave_xor(T x) {
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) x ^= __shfl_xor(x, o, 64);
+    return x;
+}
+
+// Block-wide exclusive scan.  `sh` needs NWAVES entries.  All threads must call.
+template <typename T, int NWAVES>
+__device__ inline T block_excl_scan(T v, T* sh, T& total) {
+    const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
+    T x = wave_incl_scan(v);
+    if (lane == 63) sh[wid] = x;
+    __syncthreads();
+    if (wid == 0) {
+        T w = lane < NWAVES ? sh[lane] : T(0);
+        w = wave_incl_scan(w);
+        if (lane < NWAVES) sh[lane] = w;
+    }
+    __syncthreads();
+    T pre = (wid > 0 ? sh[wid - 1] : T(0)) + x - v;
+    total = sh[NWAVES - 1];
+    __syncthreads();
+    return pre;
+}
+
+// Block-wide exclusive suffix minimum: min over threads t' > t of v[t'] (or `ident`).
+template <int NWAVES>
+__device__ inline uint32_t block_excl_suffix_min(uint32_t v, uint32_t ident, uint32_t* sh) {
+    const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
+    // inclusive suffix min within the wave
+    uint32_t x = v;
+#pragma unroll
+    for (int o = 1; o < 64; o <<= 1) {
+        uint32_t y = __shfl_down(x, o, 64);
+        if (lane + o < 64) x = min(x, y);
+    }
+    if (lane == 0) sh[wid] = x;       // wave's min
+    __syncthreads();
+    uint32_t after = ident;           // min over later waves
+    for (int w = wid + 1; w < NWAVES; w++) after = min(after, sh[w]);
+    uint32_t nxt = __shfl_down(x, 1, 64);
+    uint32_t r = (lane == 63) ? after : min(nxt, after);
+    __syncthreads();
+    return r;
+}
+
+// Agent-scope relaxed atomics on 64-bit status words (decoupled look-back).
+__device__ inline uint64_t ld_agent(const uint64_t* p) {
+    return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+__device__ inline void st_agent(uint64_t* p, uint64_t v) {
+    __hip_atomic_store(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}

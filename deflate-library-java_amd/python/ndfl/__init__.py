@@ -1,0 +1,202 @@
+"""ndfl -- MI355X-native DEFLATE codec, host-side mirror of io.nayuki.deflate.
+
+The classes here mirror the reference's public API (same names, argument meaning and error
+behaviour) on top of the C ABI in include/ndfl.h.  All codec work happens in libndfl.so's HIP
+kernels; this module only buffers bytes, writes container headers and raises exceptions.
+
+    DeflaterOutputStream   D/DeflaterOutputStream.java
+    InflaterInputStream    D/InflaterInputStream.java
+    DataFormatException    D/DataFormatException.java (with Reason)
+    GzipMetadata           D/GzipMetadata.java
+    GzipOutputStream       D/GzipOutputStream.java
+    GzipInputStream        D/GzipInputStream.java
+    ZlibOutputStream/ZlibInputStream/ZlibMetadata   D/Zlib*.java
+"""
+import ctypes
+import enum
+import io
+
+from . import _lib
+from ._lib import IN_DEVICE, OUT_DEVICE, STRATEGIES, NdflError, check, load, reason_name
+
+__all__ = ["Context", "Reason", "DataFormatException", "DeflaterOutputStream", "InflaterInputStream",
+           "GzipMetadata", "GzipOutputStream", "GzipInputStream", "ZlibMetadata", "ZlibOutputStream",
+           "ZlibInputStream", "Strategy", "default_context", "compress", "decompress", "crc32_combine"]
+
+
+class Reason(enum.Enum):
+    """DataFormatException.Reason (D/DataFormatException.java:61-83), same ordinal order."""
+    UNEXPECTED_END_OF_STREAM = 0
+    RESERVED_BLOCK_TYPE = 1
+    UNCOMPRESSED_BLOCK_LENGTH_MISMATCH = 2
+    HUFFMAN_CODE_UNDER_FULL = 3
+    HUFFMAN_CODE_OVER_FULL = 4
+    NO_PREVIOUS_CODE_LENGTH_TO_COPY = 5
+    CODE_LENGTH_CODE_OVER_FULL = 6
+    END_OF_BLOCK_CODE_ZERO_LENGTH = 7
+    RESERVED_LENGTH_SYMBOL = 8
+    RESERVED_DISTANCE_SYMBOL = 9
+    LENGTH_ENCOUNTERED_WITH_EMPTY_DISTANCE_CODE = 10
+    COPY_FROM_BEFORE_DICTIONARY_START = 11
+    HEADER_CHECKSUM_MISMATCH = 12
+    UNSUPPORTED_COMPRESSION_METHOD = 13
+    DECOMPRESSED_CHECKSUM_MISMATCH = 14
+    DECOMPRESSED_SIZE_MISMATCH = 15
+    GZIP_INVALID_MAGIC_NUMBER = 16
+    GZIP_RESERVED_FLAGS_SET = 17
+    GZIP_UNSUPPORTED_OPERATING_SYSTEM = 18
+
+
+class DataFormatException(Exception):
+    """Unchecked in the reference (extends RuntimeException, D/DataFormatException.java:15): it is
+    not made sticky by InflaterInputStream and not caught by the CLIs."""
+
+    def __init__(self, reason, msg=None):
+        self.reason = reason
+        super().__init__(msg or load().ndfl_error_string(reason.value + 1).decode())
+
+    def getReason(self):
+        return self.reason
+
+
+class Strategy(enum.Enum):
+    """Lz77Huffman presets (D/comp/Lz77Huffman.java:298-305) and Uncompressed."""
+    LITERAL_STATIC = 0
+    LITERAL_DYNAMIC = 1
+    RLE_STATIC = 2
+    RLE_DYNAMIC = 3
+    FULL_STATIC = 4
+    FULL_DYNAMIC = 5
+    UNCOMPRESSED = 6
+
+
+def _ptr(obj):
+    """(address, keepalive) of bytes-like / torch tensor."""
+    if hasattr(obj, "data_ptr"):
+        return obj.data_ptr(), obj
+    if isinstance(obj, (bytes, bytearray, memoryview)):
+        b = bytes(obj)
+        buf = ctypes.create_string_buffer(b, max(1, len(b)))
+        return ctypes.addressof(buf), buf
+    raise TypeError(type(obj))
+
+
+class Context:
+    """One device context (HIP stream + device scratch).  Not reentrant."""
+
+    def __init__(self, device=0):
+        L = load()
+        h = ctypes.c_void_p()
+        check(L.ndfl_ctx_create(ctypes.byref(h), device, 0), "ndfl_ctx_create")
+        self._h = h
+        self.device = device
+
+    def close(self):
+        if getattr(self, "_h", None):
+            load().ndfl_ctx_destroy(self._h)
+            self._h = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+    def set_stream(self, stream_handle):
+        check(load().ndfl_ctx_set_stream(self._h, ctypes.c_void_p(stream_handle)))
+
+    def last_kernel_ms(self):
+        return load().ndfl_ctx_last_kernel_ms(self._h)
+
+    # -- raw C-ABI wrappers ------------------------------------------------------------------
+    def deflate_chunks_raw(self, hist_addr, hist_len, hist_limit, data_addr, n, chunk_len, strategy, final,
+                           start_bitpos, out_addr, out_cap, flags, crc=None):
+        L = load()
+        endbits = ctypes.c_uint64(0)
+        crcv = ctypes.c_uint32(crc if crc is not None else 0)
+        r = L.ndfl_deflate_chunks(self._h, hist_addr, hist_len, hist_limit, data_addr, n, chunk_len, strategy,
+                                  int(final), start_bitpos, out_addr, out_cap, ctypes.byref(endbits),
+                                  ctypes.byref(crcv) if crc is not None else None, flags)
+        check(r, "ndfl_deflate_chunks")
+        return endbits.value, (crcv.value if crc is not None else None)
+
+    def deflate(self, data, strategy=Strategy.RLE_DYNAMIC, chunk_len=65536, hist_limit=32768, with_crc=False):
+        """Whole-stream compress of host bytes (DeflaterOutputStream write-all + finish)."""
+        data = bytes(data)
+        L = load()
+        cap = L.ndfl_deflate_bound(len(data), chunk_len) + 16
+        out = ctypes.create_string_buffer(cap)
+        src = ctypes.create_string_buffer(data, max(1, len(data)))
+        endbits, crc = self.deflate_chunks_raw(None, 0, hist_limit, ctypes.addressof(src), len(data), chunk_len,
+                                               _strategy_id(strategy), True, 0, ctypes.addressof(out), cap, 0,
+                                               crc=0 if with_crc else None)
+        comp = out.raw[:(endbits + 7) // 8]
+        return (comp, crc) if with_crc else comp
+
+    def inflate_raw(self, in_addr, in_len, out_addr, out_cap, flags):
+        """Returns (code, out_len, consumed_bits); code = 0 / reason+1 / <0 error."""
+        L = load()
+        olen = ctypes.c_uint64(0)
+        bits = ctypes.c_uint64(0)
+        r = L.ndfl_inflate(self._h, in_addr, in_len, out_addr, out_cap, ctypes.byref(olen), ctypes.byref(bits),
+                           flags)
+        return r, olen.value, bits.value
+
+    def inflate(self, data, out_cap=None):
+        """Decode a whole raw DEFLATE stream held in host memory.  Returns (reason|None, bytes, bits)."""
+        data = bytes(data)
+        src = ctypes.create_string_buffer(data, max(1, len(data)))
+        cap = out_cap if out_cap is not None else 4 * len(data) + 65536
+        while True:
+            out = ctypes.create_string_buffer(max(1, cap))
+            r, olen, bits = self.inflate_raw(ctypes.addressof(src), len(data), ctypes.addressof(out), cap, 0)
+            if r == _lib.E_CAPACITY and out_cap is None:
+                cap = olen + 16
+                continue
+            check(r, "ndfl_inflate")
+            reason = None if r == 0 else Reason(r - 1)
+            return reason, out.raw[:olen], bits
+
+    def crc32(self, data, crc=0, flags=0):
+        addr, keep = _ptr(data)
+        n = data.numel() * data.element_size() if hasattr(data, "numel") else len(data)
+        v = ctypes.c_uint32(crc)
+        check(load().ndfl_crc32(self._h, ctypes.byref(v), addr, n, flags), "ndfl_crc32")
+        return v.value
+
+
+def _strategy_id(s):
+    if isinstance(s, Strategy):
+        return s.value
+    if isinstance(s, str):
+        return STRATEGIES[s]
+    return int(s)
+
+
+def crc32_combine(a, b, len_b):
+    return load().ndfl_crc32_combine(a, b, len_b)
+
+
+_default = None
+
+
+def default_context():
+    global _default
+    if _default is None:
+        _default = Context(0)
+    return _default
+
+
+def compress(data, strategy=Strategy.RLE_DYNAMIC):
+    return default_context().deflate(data, strategy)
+
+
+def decompress(data):
+    reason, out, _ = default_context().inflate(data)
+    if reason is not None:
+        raise DataFormatException(reason)
+    return out
+
+
+from .streams import (DeflaterOutputStream, InflaterInputStream, GzipMetadata, GzipOutputStream,  # noqa: E402
+                      GzipInputStream, ZlibMetadata, ZlibOutputStream, ZlibInputStream)

@@ -1,0 +1,82 @@
+"""ctypes binding of libndfl.so (include/ndfl.h).  Fails loudly if the HIP library is missing:
+there is no CPU fallback on the product path."""
+import ctypes
+import os
+
+_HERE = os.path.dirname(os.path.abspath(__file__))
+PKG_ROOT = os.path.dirname(os.path.dirname(_HERE))          # deflate-library-java_amd/
+LIB_PATH = os.path.join(PKG_ROOT, "lib", "libndfl.so")
+
+IN_DEVICE = 1
+OUT_DEVICE = 2
+
+STRATEGIES = {"LITERAL_STATIC": 0, "LITERAL_DYNAMIC": 1, "RLE_STATIC": 2, "RLE_DYNAMIC": 3,
+              "FULL_STATIC": 4, "FULL_DYNAMIC": 5, "UNCOMPRESSED": 6}
+
+REASONS = [
+    "UNEXPECTED_END_OF_STREAM", "RESERVED_BLOCK_TYPE", "UNCOMPRESSED_BLOCK_LENGTH_MISMATCH",
+    "HUFFMAN_CODE_UNDER_FULL", "HUFFMAN_CODE_OVER_FULL", "NO_PREVIOUS_CODE_LENGTH_TO_COPY",
+    "CODE_LENGTH_CODE_OVER_FULL", "END_OF_BLOCK_CODE_ZERO_LENGTH", "RESERVED_LENGTH_SYMBOL",
+    "RESERVED_DISTANCE_SYMBOL", "LENGTH_ENCOUNTERED_WITH_EMPTY_DISTANCE_CODE",
+    "COPY_FROM_BEFORE_DICTIONARY_START", "HEADER_CHECKSUM_MISMATCH", "UNSUPPORTED_COMPRESSION_METHOD",
+    "DECOMPRESSED_CHECKSUM_MISMATCH", "DECOMPRESSED_SIZE_MISMATCH", "GZIP_INVALID_MAGIC_NUMBER",
+    "GZIP_RESERVED_FLAGS_SET", "GZIP_UNSUPPORTED_OPERATING_SYSTEM",
+]
+
+E_ARG, E_UNSUPPORTED, E_CAPACITY, E_DEVICE, E_STATE, E_INTERNAL = -1, -2, -3, -4, -5, -6
+
+# Every symbol include/ndfl.h declares (checked by tests/test_capi_symbols.py).
+EXPORTS = ["ndfl_abi_version", "ndfl_error_string", "ndfl_ctx_create", "ndfl_ctx_destroy",
+           "ndfl_ctx_set_stream", "ndfl_ctx_last_kernel_ms", "ndfl_deflate_chunks", "ndfl_deflate_bound",
+           "ndfl_inflate", "ndfl_crc32", "ndfl_crc32_combine"]
+
+_lib = None
+
+
+def load():
+    global _lib
+    if _lib is not None:
+        return _lib
+    if not os.path.exists(LIB_PATH):
+        raise RuntimeError(f"libndfl.so not built ({LIB_PATH}); run `make -C deflate-library-java_amd`")
+    L = ctypes.CDLL(LIB_PATH)
+    vp, u64, u32, i32 = ctypes.c_void_p, ctypes.c_uint64, ctypes.c_uint32, ctypes.c_int
+    L.ndfl_abi_version.restype = u32
+    L.ndfl_error_string.restype = ctypes.c_char_p
+    L.ndfl_error_string.argtypes = [i32]
+    L.ndfl_ctx_create.argtypes = [ctypes.POINTER(vp), i32, u32]
+    L.ndfl_ctx_destroy.argtypes = [vp]
+    L.ndfl_ctx_set_stream.argtypes = [vp, vp]
+    L.ndfl_ctx_last_kernel_ms.restype = ctypes.c_double
+    L.ndfl_ctx_last_kernel_ms.argtypes = [vp]
+    L.ndfl_deflate_chunks.argtypes = [vp, vp, u32, u32, vp, u64, u32, i32, i32, u32, vp, u64,
+                                      ctypes.POINTER(u64), ctypes.POINTER(u32), u32]
+    L.ndfl_deflate_bound.restype = u64
+    L.ndfl_deflate_bound.argtypes = [u64, u32]
+    L.ndfl_inflate.argtypes = [vp, vp, u64, vp, u64, ctypes.POINTER(u64), ctypes.POINTER(u64), u32]
+    L.ndfl_crc32.argtypes = [vp, ctypes.POINTER(u32), vp, u64, u32]
+    L.ndfl_crc32_combine.restype = u32
+    L.ndfl_crc32_combine.argtypes = [u32, u32, u64]
+    _lib = L
+    return L
+
+
+def reason_name(code):
+    if code == 0:
+        return None
+    if 1 <= code <= len(REASONS):
+        return REASONS[code - 1]
+    return None
+
+
+class NdflError(RuntimeError):
+    def __init__(self, code, what=""):
+        self.code = code
+        msg = load().ndfl_error_string(code).decode()
+        super().__init__(f"{what}: {msg} ({code})" if what else f"{msg} ({code})")
+
+
+def check(code, what=""):
+    if code < 0:
+        raise NdflError(code, what)
+    return code

@@ -1,0 +1,429 @@
+"""Stream classes mirroring io.nayuki.deflate's public API on top of libndfl.so.
+
+Java exception mapping: IllegalArgumentException -> ValueError, IllegalStateException ->
+RuntimeError, IOException -> OSError, DataFormatException -> ndfl.DataFormatException.
+"""
+import ctypes
+import dataclasses
+import os
+from typing import Optional
+
+from . import _lib
+from ._lib import check, load
+
+INT_MAX = 2**31 - 1
+
+
+def _ctx(context):
+    from . import default_context
+    return context if context is not None else default_context()
+
+
+class DeflaterOutputStream:
+    """D/DeflaterOutputStream.java:30-173.  Chunks of `dataLookaheadLimit` bytes from stream start
+    become one block each; a chunk is flushed only once more data arrives (so the final block holds
+    1..limit bytes, or 0 for empty input).  Many chunks are batched into one GPU call."""
+
+    def __init__(self, out, dataLookaheadLimit=64 * 1024, historyLookbehindLimit=32 * 1024, strategy=None,
+                 context=None, batch_bytes=64 << 20):
+        from . import Strategy, _strategy_id
+        if out is None:
+            raise TypeError("out")
+        if (dataLookaheadLimit < 1 or historyLookbehindLimit < 0 or historyLookbehindLimit > 32 * 1024
+                or dataLookaheadLimit + historyLookbehindLimit > INT_MAX):
+            raise ValueError("Invalid capacities")
+        self._out = out
+        self._chunk = dataLookaheadLimit
+        self._hist_limit = historyLookbehindLimit
+        self._strategy = _strategy_id(strategy if strategy is not None else Strategy.RLE_DYNAMIC)
+        self._ctx = _ctx(context)
+        self._batch = max(batch_bytes, dataLookaheadLimit + 1)
+        self._pending = bytearray()
+        self._hist = b""
+        self._bitbuf = 0          # pending partial byte
+        self._bitlen = 0          # 0..7
+        self._ended = False
+        self._crc = None          # GzipOutputStream asks for a CRC pass fused into the encoder
+
+    def getUnderlyingStream(self):
+        if self._out is None:
+            raise RuntimeError("Stream already closed")
+        return self._out
+
+    def write(self, b, off=0, length=None):
+        if self._ended:
+            raise RuntimeError("Stream already ended")
+        if isinstance(b, int):
+            self._pending.append(b & 0xFF)
+        else:
+            mv = memoryview(bytes(b))
+            if length is None:
+                length = len(mv) - off
+            if off < 0 or length < 0 or off + length > len(mv):
+                raise IndexError("Range out of bounds")
+            self._pending += mv[off:off + length]
+        if len(self._pending) > self._batch:
+            self._flush(False)
+
+    def _flush(self, final):
+        n = len(self._pending)
+        if final:
+            take = n
+        else:
+            k = (n - 1) // self._chunk
+            take = k * self._chunk
+            if take == 0:
+                return
+        data = bytes(self._pending[:take])
+        L = load()
+        cap = L.ndfl_deflate_bound(take, self._chunk) + 16
+        out = ctypes.create_string_buffer(cap)
+        src = ctypes.create_string_buffer(data, max(1, len(data)))
+        hist = ctypes.create_string_buffer(self._hist, max(1, len(self._hist)))
+        endbits, crc = self._ctx.deflate_chunks_raw(
+            ctypes.addressof(hist) if self._hist else None, len(self._hist), self._hist_limit,
+            ctypes.addressof(src), take, self._chunk, self._strategy, final, self._bitlen,
+            ctypes.addressof(out), cap, 0, crc=self._crc)
+        if self._crc is not None:
+            self._crc = crc
+        nbytes = (endbits + 7) // 8
+        raw = bytearray(out.raw[:nbytes])
+        if raw:
+            raw[0] |= self._bitbuf
+        whole = endbits // 8
+        self._out.write(bytes(raw[:whole]))
+        self._bitlen = endbits % 8
+        self._bitbuf = raw[whole] if self._bitlen else 0
+        del self._pending[:take]
+        if self._hist_limit:
+            self._hist = (self._hist + data)[-self._hist_limit:]
+
+    def finish(self):
+        if self._ended:
+            raise RuntimeError("Stream already ended")
+        self._flush(True)
+        if self._bitlen:
+            self._out.write(bytes([self._bitbuf]))   # BitOut.finish zero-pads (:164-169)
+            self._bitbuf = 0
+            self._bitlen = 0
+        self._ended = True
+
+    def close(self):
+        if not self._ended:
+            self.finish()
+        if self._out is not None:
+            self._out.close()
+            self._out = None
+
+    def __enter__(self):
+        return self
+
+    def __exit__(self, *exc):
+        self.close()
+
+
+class InflaterInputStream:
+    """D/InflaterInputStream.java:26-181.  The whole remaining underlying stream is handed to the GPU
+    decoder on the first read; decoded bytes are then served with the reference's read contract:
+    read(b, off, len) returns -1..len and 0 only when len == 0; -1 at end of stream."""
+
+    def __init__(self, inp, endExactly=False, inBufLen=16 * 1024, context=None):
+        if inp is None:
+            raise TypeError("in")
+        if inBufLen <= 0:
+            raise ValueError("Non-positive input buffer size")
+        if endExactly and not (hasattr(inp, "seek") and hasattr(inp, "tell") and _seekable(inp)):
+            raise ValueError("Input stream not markable, cannot support detachment")
+        self._in = inp
+        self._end_exactly = endExactly
+        self._ctx = _ctx(context)
+        self._state = "open"
+        self._buf = None
+        self._pos = 0
+        self._error = None
+        self._sticky = None
+
+    def _decode(self):
+        from . import DataFormatException, Reason
+        start = self._in.tell() if self._end_exactly else 0
+        try:
+            data = self._in.read()
+        except OSError as e:
+            self._sticky = e
+            raise
+        reason, out, bits = self._ctx.inflate(data)
+        self._buf = out
+        if reason is not None:
+            self._error = DataFormatException(reason)
+        elif self._end_exactly:
+            self._in.seek(start + (bits + 7) // 8)
+
+    def read(self, b=None, off=0, length=None):
+        """read() -> int byte or -1;  read(bytearray, off, len) -> count or -1."""
+        if self._state == "closed":
+            raise RuntimeError("Stream already closed")
+        if self._sticky is not None:
+            raise self._sticky
+        if self._buf is None:
+            self._decode()
+        if b is None:
+            if self._pos < len(self._buf):
+                v = self._buf[self._pos]
+                self._pos += 1
+                return v
+            if self._error is not None:
+                raise self._error
+            return -1
+        if length is None:
+            length = len(b) - off
+        if off < 0 or length < 0 or off + length > len(b):
+            raise IndexError("Range out of bounds")
+        avail = len(self._buf) - self._pos
+        if avail == 0 and length > 0 and self._error is not None:
+            raise self._error
+        n = min(avail, length)
+        b[off:off + n] = self._buf[self._pos:self._pos + n]
+        self._pos += n
+        if n == 0 and self._error is None and avail == 0:
+            return -1          # also for len == 0 at end of stream (D/decomp/Open.java:109)
+        return n
+
+    def readall(self):
+        if self._buf is None:
+            self._decode()
+        out = self._buf[self._pos:]
+        self._pos = len(self._buf)
+        if self._error is not None:
+            raise self._error
+        return out
+
+    def close(self):
+        if self._state != "closed" and self._in is not None:
+            self._in.close()
+        self._state = "closed"
+
+
+def _seekable(f):
+    try:
+        return f.seekable()
+    except Exception:
+        return False
+
+
+# ---- gzip container (RFC 1952) --------------------------------------------------------------
+
+OS_NAMES = ["FAT_FILESYSTEM", "AMIGA", "VMS", "UNIX", "VM_CMS", "ATARI_TOS", "HPFS_FILESYSTEM", "MACINTOSH",
+            "Z_SYSTEM", "CPM", "TOPS_20", "NTFS_FILESYSTEM", "QDOS", "ACORN_RISCOS", "UNKNOWN"]
+
+
+@dataclasses.dataclass
+class GzipMetadata:
+    """D/GzipMetadata.java:30-242 (record components in the same order)."""
+    compressionMethod: str = "DEFLATE"
+    isFileText: bool = False
+    modificationTimeUnixS: Optional[int] = None
+    extraFlags: int = 0
+    operatingSystem: str = "UNIX"
+    extraField: Optional[bytes] = None
+    fileName: Optional[str] = None
+    comment: Optional[str] = None
+    hasHeaderCrc: bool = False
+
+    def __post_init__(self):
+        if self.modificationTimeUnixS == 0:
+            raise ValueError("Modification timestamp is zero")
+        if self.extraFlags >> 8 != 0:
+            raise ValueError("Invalid extra flags value")
+        if self.extraField is not None and len(self.extraField) > 0xFFFF:
+            raise ValueError("Extra field too long")
+        if self.operatingSystem not in OS_NAMES:
+            raise ValueError("operatingSystem")
+
+    def header_bytes(self):
+        flags = ((1 if self.isFileText else 0) | (2 if self.hasHeaderCrc else 0) |
+                 (4 if self.extraField is not None else 0) | (8 if self.fileName is not None else 0) |
+                 (16 if self.comment is not None else 0))
+        mt = self.modificationTimeUnixS or 0
+        osb = 0xFF if self.operatingSystem == "UNKNOWN" else OS_NAMES.index(self.operatingSystem)
+        h = bytearray([0x1F, 0x8B, 8, flags]) + (mt & 0xFFFFFFFF).to_bytes(4, "little") + bytes([self.extraFlags, osb])
+        if self.extraField is not None:
+            h += len(self.extraField).to_bytes(2, "little") + self.extraField
+        if self.fileName is not None:
+            h += self.fileName.encode("latin-1") + b"\0"
+        if self.comment is not None:
+            h += self.comment.encode("latin-1") + b"\0"
+        return h
+
+    def write(self, out, context=None):
+        h = self.header_bytes()
+        if self.hasHeaderCrc:
+            crc = _ctx(context).crc32(bytes(h)) & 0xFFFF
+            h += crc.to_bytes(2, "little")
+        out.write(bytes(h))
+
+    @staticmethod
+    def read(inp, context=None):
+        """GzipMetadata.read (D/GzipMetadata.java:73-146); raises DataFormatException(reason)."""
+        from . import DataFormatException, Reason
+        got = bytearray()
+
+        def rd(n):
+            b = inp.read(n)
+            if b is None or len(b) < n:
+                raise DataFormatException(Reason.UNEXPECTED_END_OF_STREAM)
+            got.extend(b)
+            return b
+
+        if rd(2) != b"\x1f\x8b":
+            raise DataFormatException(Reason.GZIP_INVALID_MAGIC_NUMBER, "Invalid GZIP magic number")
+        cm = rd(1)[0]
+        if cm != 8:
+            raise DataFormatException(Reason.UNSUPPORTED_COMPRESSION_METHOD, f"Unsupported compression method: {cm}")
+        flags = rd(1)[0]
+        if flags & 0xE0:
+            raise DataFormatException(Reason.GZIP_RESERVED_FLAGS_SET, "Reserved flags are set")
+        mt = int.from_bytes(rd(4), "little")
+        xfl = rd(1)[0]
+        osv = rd(1)[0]
+        if osv < 14:
+            osname = OS_NAMES[osv]
+        elif osv == 0xFF:
+            osname = "UNKNOWN"
+        else:
+            raise DataFormatException(Reason.GZIP_UNSUPPORTED_OPERATING_SYSTEM, "Unsupported operating system value")
+        extra = None
+        if flags & 4:
+            ln = int.from_bytes(rd(2), "little")
+            extra = bytes(rd(ln))
+        name = comment = None
+        if flags & 8:
+            s = bytearray()
+            while (c := rd(1)[0]) != 0:
+                s.append(c)
+            name = s.decode("latin-1")
+        if flags & 16:
+            s = bytearray()
+            while (c := rd(1)[0]) != 0:
+                s.append(c)
+            comment = s.decode("latin-1")
+        hcrc = bool(flags & 2)
+        if hcrc:
+            expect = _ctx(context).crc32(bytes(got)) & 0xFFFF
+            actual = int.from_bytes(rd(2), "little")
+            if actual != expect:
+                raise DataFormatException(Reason.HEADER_CHECKSUM_MISMATCH, "Header CRC-16 mismatch")
+        return GzipMetadata("DEFLATE", bool(flags & 1), mt if mt != 0 else None, xfl, osname, extra, name, comment,
+                            hcrc)
+
+
+class GzipOutputStream:
+    """D/GzipOutputStream.java:19-80.  The CRC-32 pass is fused into the GPU encoder kernel."""
+
+    def __init__(self, out, meta, context=None):
+        dout = out if isinstance(out, DeflaterOutputStream) else DeflaterOutputStream(out, context=context)
+        if meta is None:
+            raise TypeError("meta")
+        meta.write(dout.getUnderlyingStream(), context=dout._ctx)
+        self._d = dout
+        self._d._crc = 0
+        self._len = 0
+        self._ended = False
+
+    def write(self, b, off=0, length=None):
+        if self._ended:
+            raise RuntimeError("Stream already ended")
+        if isinstance(b, int):
+            b = bytes([b & 0xFF])
+        mv = memoryview(bytes(b))
+        if length is None:
+            length = len(mv) - off
+        self._d.write(mv, off, length)
+        self._len += length
+
+    def finish(self):
+        if self._ended:
+            raise RuntimeError("Stream already ended")
+        self._d.finish()
+        crc = self._d._crc
+        out = self._d.getUnderlyingStream()
+        out.write(crc.to_bytes(4, "little"))
+        out.write((self._len & 0xFFFFFFFF).to_bytes(4, "little"))
+        self._ended = True
+
+    def close(self):
+        if not self._ended:
+            self.finish()
+        self._d.close()
+
+    def __enter__(self):
+        return self
+
+    def __exit__(self, *exc):
+        self.close()
+
+
+class GzipInputStream:
+    """D/GzipInputStream.java:22-100.  Single member; trailing bytes ignored."""
+
+    def __init__(self, inp, context=None):
+        self._ctx = _ctx(context)
+        self.metadata = GzipMetadata.read(inp, self._ctx)
+        self._raw = inp
+        self._inf = InflaterInputStream(inp, True, context=self._ctx)
+        self._done = False
+        self._crc = 0
+        self._len = 0
+
+    def getMetadata(self):
+        return self.metadata
+
+    def _trailer(self):
+        from . import DataFormatException, Reason
+        t = self._raw.read(8)
+        if t is None or len(t) < 8:
+            raise DataFormatException(Reason.UNEXPECTED_END_OF_STREAM)
+        if int.from_bytes(t[:4], "little") != self._crc:
+            raise DataFormatException(Reason.DECOMPRESSED_CHECKSUM_MISMATCH, "Decompression CRC-32 mismatch")
+        if int.from_bytes(t[4:], "little") != (self._len & 0xFFFFFFFF):
+            raise DataFormatException(Reason.DECOMPRESSED_SIZE_MISMATCH, "Decompressed size mismatch")
+
+    def readall(self):
+        if self._done:
+            return b""
+        out = self._inf.readall()
+        self._crc = self._ctx.crc32(out)
+        self._len = len(out)
+        self._done = True
+        self._trailer()
+        return out
+
+    def read(self, b=None, off=0, length=None):
+        if self._done:
+            return -1
+        if self._inf._buf is None:
+            self._inf._decode()
+            if self._inf._error is None:
+                self._crc = self._ctx.crc32(self._inf._buf)
+                self._len = len(self._inf._buf)
+        r = self._inf.read(b, off, length)
+        if r == -1:
+            self._done = True
+            self._trailer()
+        return r
+
+    def close(self):
+        self._raw.close()
+
+
+class ZlibMetadata:
+    pass
+
+
+class ZlibOutputStream:
+    def __init__(self, *a, **k):
+        raise NotImplementedError("zlib container: SURVEY §8f row 3 (not yet on the GPU path)")
+
+
+class ZlibInputStream:
+    def __init__(self, *a, **k):
+        raise NotImplementedError("zlib container: SURVEY §8f row 3 (not yet on the GPU path)")

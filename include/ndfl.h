@@ -1,0 +1,114 @@
+/*
+ * ndfl.h -- C ABI of the MI355X-native DEFLATE codec (libndfl.so).
+ *
+ * This is the drop-in boundary for nayuki/DEFLATE-library-Java's encode/decode hot path.  Each
+ * entry point names the reference interface it replaces (D/ = src/io/nayuki/deflate/ in the
+ * reference).  Plain pointers and sizes only; no torch types.  Buffers are caller-owned; the
+ * library never keeps a pointer past return.  A context owns device scratch and one HIP stream;
+ * calls on one context are not reentrant, calls on different contexts are.
+ *
+ * Return convention (all int-returning calls):
+ *     0                 success
+ *     1 .. 19           DataFormatException.Reason ordinal + 1 (D/DataFormatException.java:61-83)
+ *     < 0               NDFL_E_* (usage / device errors; map to IllegalArgument/IOException)
+ */
+#ifndef NDFL_H
+#define NDFL_H
+#include <stdint.h>
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define NDFL_ABI_VERSION 1u
+
+/* error codes */
+#define NDFL_OK               0
+#define NDFL_E_ARG          (-1)   /* IllegalArgumentException / NullPointerException */
+#define NDFL_E_UNSUPPORTED  (-2)   /* configuration not implemented on the GPU path */
+#define NDFL_E_CAPACITY     (-3)   /* output buffer too small; required size reported */
+#define NDFL_E_DEVICE       (-4)   /* HIP runtime error (IOException) */
+#define NDFL_E_STATE        (-5)   /* IllegalStateException (use after finish/close) */
+#define NDFL_E_INTERNAL     (-6)
+
+/* DataFormatException.Reason ordinal + 1 */
+enum ndfl_reason {
+    NDFL_UNEXPECTED_END_OF_STREAM = 1, NDFL_RESERVED_BLOCK_TYPE, NDFL_UNCOMPRESSED_BLOCK_LENGTH_MISMATCH,
+    NDFL_HUFFMAN_CODE_UNDER_FULL, NDFL_HUFFMAN_CODE_OVER_FULL, NDFL_NO_PREVIOUS_CODE_LENGTH_TO_COPY,
+    NDFL_CODE_LENGTH_CODE_OVER_FULL, NDFL_END_OF_BLOCK_CODE_ZERO_LENGTH, NDFL_RESERVED_LENGTH_SYMBOL,
+    NDFL_RESERVED_DISTANCE_SYMBOL, NDFL_LENGTH_ENCOUNTERED_WITH_EMPTY_DISTANCE_CODE,
+    NDFL_COPY_FROM_BEFORE_DICTIONARY_START, NDFL_HEADER_CHECKSUM_MISMATCH, NDFL_UNSUPPORTED_COMPRESSION_METHOD,
+    NDFL_DECOMPRESSED_CHECKSUM_MISMATCH, NDFL_DECOMPRESSED_SIZE_MISMATCH, NDFL_GZIP_INVALID_MAGIC_NUMBER,
+    NDFL_GZIP_RESERVED_FLAGS_SET, NDFL_GZIP_UNSUPPORTED_OPERATING_SYSTEM
+};
+
+/* Strategy ids: the Lz77Huffman presets (D/comp/Lz77Huffman.java:298-305) and Uncompressed. */
+enum ndfl_strategy {
+    NDFL_LITERAL_STATIC = 0, NDFL_LITERAL_DYNAMIC = 1, NDFL_RLE_STATIC = 2, NDFL_RLE_DYNAMIC = 3,
+    NDFL_FULL_STATIC = 4, NDFL_FULL_DYNAMIC = 5, NDFL_UNCOMPRESSED = 6
+};
+
+/* memory flags */
+#define NDFL_IN_DEVICE   1u    /* input pointers (data, hist) are device memory */
+#define NDFL_OUT_DEVICE  2u    /* output pointer is device memory */
+
+typedef struct ndfl_ctx ndfl_ctx;
+
+uint32_t ndfl_abi_version(void);
+const char* ndfl_error_string(int code);
+
+/* Create a context on HIP device `device`.  Fails with NDFL_E_DEVICE if no GPU. */
+int ndfl_ctx_create(ndfl_ctx** out, int device, uint32_t flags);
+int ndfl_ctx_destroy(ndfl_ctx* ctx);
+/* Use the caller's hipStream_t (NULL restores the context's own stream). */
+int ndfl_ctx_set_stream(ndfl_ctx* ctx, void* hip_stream);
+/* Average device time (ms) of the last call's dominant kernel, measured with HIP events. */
+double ndfl_ctx_last_kernel_ms(ndfl_ctx* ctx);
+
+/*
+ * Compress K consecutive chunks of one DEFLATE stream.
+ * Replaces K iterations of DeflaterOutputStream.writeBuffer (D/DeflaterOutputStream.java:119-137),
+ * i.e. Strategy.decide(b, off, historyLen, dataLen) + Decision.compressTo(bitOut, isFinal)
+ * (D/comp/Strategy.java:14, D/comp/Decision.java:16-19, D/comp/Lz77Huffman.java:42-286) and the
+ * BitOut packing (D/DeflaterOutputStream.java:141-171).  Batching is exact because the default
+ * decisions depend only on raw input, never on earlier output.
+ *   hist/hist_len   the min(historyLookbehindLimit, pos) raw bytes preceding `data`
+ *   data/len        K chunks: chunk_len bytes each, the last one 0..chunk_len bytes
+ *   final_flag      1 if the last chunk is the stream's final chunk (bfinal=1); if 0, every
+ *                   chunk must be full (len % chunk_len == 0, len > 0)
+ *   hist_limit      historyLookbehindLimit (0..32768) -- decides whether history exists
+ *   start_bitpos    BitOutputStream.getBitPosition() before the first block (0..7): the output
+ *                   begins at that bit of out[0]; bits below it are written as 0 (caller ORs)
+ *   out/out_cap     output bytes; on success *out_end_bits = start_bitpos + bits written
+ *   crc_inout       optional: java.util.zip.CRC32 value updated with `data` (GzipOutputStream)
+ * Returns 0, NDFL_E_UNSUPPORTED (FULL_* and UNCOMPRESSED are CPU-only in the reference-parity
+ * sense and not yet on the GPU path), NDFL_E_CAPACITY (*out_end_bits = bits required), ...
+ */
+int ndfl_deflate_chunks(ndfl_ctx* ctx, const uint8_t* hist, uint32_t hist_len, uint32_t hist_limit,
+                        const uint8_t* data, uint64_t len, uint32_t chunk_len, int strategy,
+                        int final_flag, uint32_t start_bitpos, uint8_t* out, uint64_t out_cap,
+                        uint64_t* out_end_bits, uint32_t* crc_inout, uint32_t flags);
+
+/* Upper bound of output bytes of ndfl_deflate_chunks for `len` bytes. */
+uint64_t ndfl_deflate_bound(uint64_t len, uint32_t chunk_len);
+
+/*
+ * Decompress one raw DEFLATE stream held entirely in `in`.
+ * Replaces InflaterInputStream.read / Open.read (D/InflaterInputStream.java:147-164,
+ * D/decomp/Open.java:83-124) run to end of stream.  Trailing bytes after the final block are
+ * ignored; *consumed_bits is the bit position just after the final block (endExactly
+ * repositioning uses ceil(consumed_bits/8), D/decomp/Open.java:113-124).
+ * Returns 0, a Reason code (with *out_len = bytes decoded before the error), NDFL_E_CAPACITY
+ * (*out_len = bytes required), or a negative error.
+ */
+int ndfl_inflate(ndfl_ctx* ctx, const uint8_t* in, uint64_t in_len, uint8_t* out, uint64_t out_cap,
+                 uint64_t* out_len, uint64_t* consumed_bits, uint32_t flags);
+
+/* java.util.zip.CRC32.update over a buffer, on the GPU (flags: NDFL_IN_DEVICE). */
+int ndfl_crc32(ndfl_ctx* ctx, uint32_t* crc_inout, const uint8_t* data, uint64_t len, uint32_t flags);
+/* crc of A||B from crc(A), crc(B), |B| (host arithmetic). */
+uint32_t ndfl_crc32_combine(uint32_t crc_a, uint32_t crc_b, uint64_t len_b);
+
+#ifdef __cplusplus
+}
+#endif
+#endif

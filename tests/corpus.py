@@ -1,0 +1,122 @@
+"""Seeded synthetic corpora of SURVEY.md §8d, generated with torch on any device.
+
+    c4_mixed(n, seed=0xC4)   Silesia-style mix in 1 MiB segments: ~40 % text/XML-ish, ~35 % binary
+                             tables (LE int32 with small deltas, skewed byte soup), ~10 % random,
+                             ~15 % byte runs.
+    c3_text(n, seed=0xC3)    enwik-style text: Zipf(1.07) words over a 65,536-word vocabulary,
+                             punctuation/newlines, [[link]] and <tag> markup.
+
+Deterministic per (seed, device type).  Test/bench infrastructure, not product code.
+"""
+import math
+
+import torch
+
+SEG = 1 << 20
+
+
+def _vocab(g, nwords, device, maxlen=12):
+    lens = torch.randint(2, maxlen + 1, (nwords,), generator=g, device=device)
+    letters = torch.randint(97, 123, (nwords, maxlen + 1), generator=g, device=device, dtype=torch.int64)
+    letters[:, -1] = 32
+    idx = torch.arange(maxlen + 1, device=device)
+    words = torch.where(idx[None, :] < lens[:, None], letters, torch.full_like(letters, 32))
+    # word bytes followed by one space; length = lens + 1
+    return words.to(torch.uint8), lens + 1
+
+
+def _zipf_ids(g, count, nwords, s, device):
+    ranks = torch.arange(1, nwords + 1, device=device, dtype=torch.float64)
+    p = ranks.pow(-s)
+    cdf = torch.cumsum(p, 0)
+    cdf = cdf / cdf[-1]
+    u = torch.rand(count, generator=g, device=device, dtype=torch.float64)
+    return torch.searchsorted(cdf, u).clamp_(max=nwords - 1)
+
+
+def _text(g, n, device, nwords=4096, s=1.07, markup=True):
+    words, wl = _vocab(g, nwords, device)
+    avg = float(wl.float().mean())
+    count = int(n / avg * 1.1) + 64
+    ids = _zipf_ids(g, count, nwords, s, device)
+    if markup:
+        # every ~40 words: newline word, "[[" link, "<tag>" -- emulate by special vocab entries
+        special = torch.tensor([list(b"\n" + b" " * 12), list(b"[[link]] " + b" " * 4), list(b"<tag> " + b" " * 7)],
+                               dtype=torch.uint8, device=device)
+        slen = torch.tensor([1, 9, 6], device=device)
+        words = torch.cat([words, special])
+        wl = torch.cat([wl, slen])
+        mark = torch.rand(count, generator=g, device=device) < (1.0 / 40)
+        kind = torch.randint(0, 3, (count,), generator=g, device=device)
+        ids = torch.where(mark, nwords + kind, ids)
+    L = wl[ids]
+    total = int(L.sum())
+    while total < n:   # rare
+        extra = _zipf_ids(g, count // 4 + 16, nwords, s, device)
+        ids = torch.cat([ids, extra])
+        L = wl[ids]
+        total = int(L.sum())
+    starts = torch.cumsum(L, 0) - L
+    rep = torch.repeat_interleave(torch.arange(ids.numel(), device=device), L)[:n]
+    off = torch.arange(n, device=device) - starts[rep]
+    return words[ids[rep], off]
+
+
+def _runs(g, n, device):
+    # run lengths ~ geometric (mean ~ 300), values from a small alphabet with some random bytes
+    count = n // 150 + 64
+    u = torch.rand(count, generator=g, device=device)
+    lens = (torch.log1p(-u) / math.log1p(-1 / 300.0)).long() + 1
+    vals = torch.randint(0, 256, (count,), generator=g, device=device)
+    small = torch.rand(count, generator=g, device=device) < 0.7
+    vals = torch.where(small, vals % 4, vals).to(torch.uint8)
+    while int(lens.sum()) < n:
+        lens = torch.cat([lens, lens])
+        vals = torch.cat([vals, vals.flip(0)])
+    return torch.repeat_interleave(vals, lens)[:n]
+
+
+def _binary(g, n, device):
+    half = n // 2
+    # LE int32 with small deltas
+    k = (half + 3) // 4
+    d = torch.randint(-3, 4, (k,), generator=g, device=device, dtype=torch.int32)
+    base = torch.randint(0, 1 << 20, (1,), generator=g, device=device, dtype=torch.int32)
+    v = torch.cumsum(d, 0, dtype=torch.int32) + base
+    tab = v.view(torch.uint8)[:half]
+    # skewed byte soup: geometric-ish byte values
+    m = n - half
+    u = torch.rand(m, generator=g, device=device)
+    soup = (torch.log1p(-u) / math.log1p(-0.15)).clamp_(max=255).to(torch.uint8)
+    return torch.cat([tab, soup])
+
+
+def c4_mixed(n, seed=0xC4, device="cpu"):
+    g = torch.Generator(device=device).manual_seed(seed)
+    nseg = max(1, -(-n // SEG))
+    probs = torch.tensor([0.40, 0.35, 0.10, 0.15], device=device)
+    types = torch.multinomial(probs, nseg, replacement=True, generator=g).tolist()
+    out = torch.empty(nseg * SEG, dtype=torch.uint8, device=device)
+    for t in range(4):
+        segs = [i for i, x in enumerate(types) if x == t]
+        # generate in batches of <= 256 segments to bound temporaries
+        for b0 in range(0, len(segs), 256):
+            sl = segs[b0:b0 + 256]
+            m = len(sl) * SEG
+            if t == 0:
+                blob = _text(g, m, device)
+            elif t == 1:
+                blob = _binary(g, m, device)
+            elif t == 2:
+                blob = torch.randint(0, 256, (m,), generator=g, device=device, dtype=torch.uint8)
+            else:
+                blob = _runs(g, m, device)
+            blob = blob.view(len(sl), SEG)
+            idx = torch.tensor(sl, device=device)
+            out.view(nseg, SEG)[idx] = blob
+    return out[:n]
+
+
+def c3_text(n, seed=0xC3, device="cpu"):
+    g = torch.Generator(device=device).manual_seed(seed)
+    return _text(g, n, device, nwords=65536)

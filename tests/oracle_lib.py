@@ -84,13 +84,13 @@ def _buf(data):
     return ctypes.create_string_buffer(b, max(1, len(b))), len(b)
 
 
-def deflate_bound(n):
-    return n + n // 4 + 4096 + (n // 65535 + 1) * 8
+def deflate_bound(n, chunk_len=65536):
+    return n + n // 4 + 4096 + (n // min(chunk_len, 65535) + 1) * 600
 
 
 def deflate(data, strategy="RLE_DYNAMIC", chunk_len=65536, hist_limit=32768, brute=False):
     src, n = _buf(data)
-    cap = deflate_bound(n)
+    cap = deflate_bound(n, chunk_len)
     out = ctypes.create_string_buffer(cap)
     r = lib().or_deflate(src, n, chunk_len, hist_limit, STRATEGIES.index(strategy), int(brute), out, cap)
     if r < 0:
@@ -100,7 +100,7 @@ def deflate(data, strategy="RLE_DYNAMIC", chunk_len=65536, hist_limit=32768, bru
 
 def deflate_lz(data, dynamic, min_run, max_run, min_dist, max_dist, chunk_len=65536, hist_limit=32768, brute=False):
     src, n = _buf(data)
-    cap = deflate_bound(n) * 2
+    cap = deflate_bound(n, chunk_len) * 2
     out = ctypes.create_string_buffer(cap)
     r = lib().or_deflate_lz(src, n, chunk_len, hist_limit, int(dynamic), min_run, max_run, min_dist, max_dist,
                             int(brute), out, cap)
