@@ -440,6 +440,32 @@ int64_t or_deflate(const uint8_t* data, uint64_t len, uint32_t chunk_len, uint32
     return (int64_t)w.n;
 }
 
+int64_t or_deflate_mixed(const uint8_t* data, uint64_t len, uint32_t chunk_len, uint32_t hist_limit,
+                         const int8_t* strat, uint32_t nstrat, uint8_t* out, uint64_t out_cap) {
+    /* Fixture generator: chunk i is encoded with strategy strat[i % nstrat] (a mix of stored,
+     * fixed and dynamic blocks, e.g. config 2's "stored + fixed-Huffman" stream). */
+    if (chunk_len < 1 || hist_limit > 32768 || nstrat == 0) return OR_ERR_ARG;
+    bw_t w = {out, out_cap, 0, 0, 0, 0};
+    uint64_t pos = 0, ci = 0;
+    for (;;) {
+        uint64_t dlen = len - pos; int fin = 1;
+        if (dlen > chunk_len) { dlen = chunk_len; fin = 0; }
+        else if (dlen == chunk_len && pos + dlen < len) fin = 0;
+        uint64_t hlen = pos < hist_limit ? pos : hist_limit;
+        const uint8_t* base = data + (pos - hlen);
+        sink_t sk = { &w, 0 };
+        int st = strat[ci % nstrat];
+        if (st == OR_UNCOMPRESSED) unc_compress(base, 0, (int64_t)hlen, (int64_t)dlen, fin, &sk);
+        else if (st >= 0 && st < 6) lz_compress(base, 0, (int64_t)hlen, (int64_t)dlen, &PRESETS[st], fin, &sk, 0);
+        else return OR_ERR_ARG;
+        pos += dlen; ci++;
+        if (fin) break;
+    }
+    bw_finish(&w);
+    if (w.overflow) return OR_ERR_CAPACITY;
+    return (int64_t)w.n;
+}
+
 int64_t or_deflate_block_bits(const uint8_t* data, uint64_t len, uint32_t chunk_len, uint32_t hist_limit,
                               int strategy, uint64_t* bits, uint64_t cap) {
     if (strategy < 0 || strategy > 6) return OR_ERR_ARG;

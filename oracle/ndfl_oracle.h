@@ -61,6 +61,10 @@ int64_t or_deflate_lz(const uint8_t* data, uint64_t len, uint32_t chunk_len, uin
 int64_t or_deflate_block_bits(const uint8_t* data, uint64_t len, uint32_t chunk_len, uint32_t hist_limit,
                               int strategy, uint64_t* bits, uint64_t cap);
 
+/* Fixture generator: chunk i uses strategy strat[i % nstrat]. */
+int64_t or_deflate_mixed(const uint8_t* data, uint64_t len, uint32_t chunk_len, uint32_t hist_limit,
+                         const int8_t* strat, uint32_t nstrat, uint8_t* out, uint64_t out_cap);
+
 /* InflaterInputStream over the whole of `in` (D/decomp/Open.java).  Returns 0 or 1+Reason.
  * *out_len = bytes produced before success/error; *consumed_bits = bit position after the
  * final block (meaningful on success).  OR_ERR_CAPACITY if out_cap is too small. */

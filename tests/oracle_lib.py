@@ -59,6 +59,9 @@ def lib():
         L.or_deflate_block_bits.restype = ctypes.c_int64
         L.or_deflate_block_bits.argtypes = [u8p, ctypes.c_uint64, ctypes.c_uint32, ctypes.c_uint32,
                                             ctypes.c_int, ctypes.POINTER(ctypes.c_uint64), ctypes.c_uint64]
+        L.or_deflate_mixed.restype = ctypes.c_int64
+        L.or_deflate_mixed.argtypes = [u8p, ctypes.c_uint64, ctypes.c_uint32, ctypes.c_uint32, u8p, ctypes.c_uint32,
+                                       u8p, ctypes.c_uint64]
         L.or_inflate.restype = ctypes.c_int
         L.or_inflate.argtypes = [u8p, ctypes.c_uint64, u8p, ctypes.c_uint64,
                                  ctypes.POINTER(ctypes.c_uint64), ctypes.POINTER(ctypes.c_uint64)]
@@ -106,6 +109,18 @@ def deflate_lz(data, dynamic, min_run, max_run, min_dist, max_dist, chunk_len=65
                             int(brute), out, cap)
     if r < 0:
         raise ValueError(f"or_deflate_lz failed: {r}")
+    return out.raw[:r]
+
+
+def deflate_mixed(data, strategies, chunk_len=65535, hist_limit=32768):
+    """Fixture generator: chunk i encoded with strategies[i % len]."""
+    src, n = _buf(data)
+    cap = deflate_bound(n, chunk_len) * 2
+    out = ctypes.create_string_buffer(cap)
+    st = (ctypes.c_int8 * len(strategies))(*[STRATEGIES.index(s) for s in strategies])
+    r = lib().or_deflate_mixed(src, n, chunk_len, hist_limit, st, len(strategies), out, cap)
+    if r < 0:
+        raise ValueError(f"or_deflate_mixed failed: {r}")
     return out.raw[:r]
 
 
