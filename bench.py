@@ -1,0 +1,194 @@
+"""Headline benchmark: DEFLATE round trip (compress + decompress) on MI355X.
+
+metric  "input MiB/s (compress+decompress)" (BASELINE.json): bytes fed to the two operations
+        (N uncompressed into the encoder + C compressed into the decoder) per second of the step,
+        MiB = 2^20, whole job over all ranks.
+step    one round trip over one batch: the rank's 4 GiB shard of the config-4 corpus
+        (Silesia-style mix, seed 0xC4 + rank) is compressed with the gzip default encoder
+        (RLE_DYNAMIC, 64 KiB blocks, bit-exact with the reference) into one DEFLATE stream, and that
+        stream is decompressed again.  Inputs and outputs are resident in HBM (device pointers
+        through the C ABI); no host copies inside the timed region.
+N > 1   weak scaling: rank r owns chunks [r*K, (r+1)*K) of ONE global stream.  Ranks exchange the
+        byte before their shard and their compressed bit totals (RCCL all_gather over xGMI), shift
+        their bits to the global bit offset on device, and decode their own bit range with the
+        previous rank's last 32 KiB of output as the dictionary (RCCL point-to-point).
+Run: python bench.py [--gpus N --steps K --warmup W]; multi-GPU via torch.distributed.run.
+"""
+import argparse
+import ctypes
+import json
+import os
+import sys
+import time
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, os.path.join(ROOT, "deflate-library-java_amd", "python"))
+sys.path.insert(0, os.path.join(ROOT, "tests"))
+
+HBM_PEAK = 8.0e12          # MI355X HBM3E spec, bytes/s (MI355X_MICROARCH.md)
+MIB = 1 << 20
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=5)
+    ap.add_argument("--warmup", type=int, default=2)
+    ap.add_argument("--size", type=int, default=4 << 30, help="bytes per rank")
+    ap.add_argument("--cpu-sample", type=int, default=256 << 20, help="bytes for the CPU baseline leg")
+    ap.add_argument("--no-cpu", action="store_true")
+    ap.add_argument("--no-verify", action="store_true")
+    args = ap.parse_args()
+
+    import torch
+    import ndfl
+    import corpus
+
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    torch.cuda.set_device(local)
+    dist = None
+    if world > 1:
+        import torch.distributed as dist
+        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+
+    n = args.size
+    data = corpus.c4_mixed(n, seed=0xC4 + rank, device="cuda")
+    torch.cuda.synchronize()
+    ctx = ndfl.Context(local)
+    L = ndfl._lib.load()
+    cap = L.ndfl_deflate_bound(n, 65536) + 64
+    comp = torch.empty(cap, dtype=torch.uint8, device="cuda")
+    dec = torch.empty(n + (32 << 10) + 64, dtype=torch.uint8, device="cuda")
+    RLE_DYNAMIC = 3
+    DEV = ndfl.IN_DEVICE | ndfl.OUT_DEVICE
+
+    prev_byte = None
+    if world > 1:
+        # the byte preceding this rank's shard (RLE history) -- exchanged once, it is input
+        lasts = torch.empty(world, dtype=torch.uint8, device="cuda")
+        dist.all_gather_into_tensor(lasts, data[-1:].contiguous())
+        if rank > 0:
+            prev_byte = lasts[rank - 1:rank].clone()
+
+    state = {}
+
+    def step():
+        hist_addr = prev_byte.data_ptr() if prev_byte is not None else None
+        endbits, _ = ctx.deflate_chunks_raw(hist_addr, 1 if prev_byte is not None else 0, 32768, data.data_ptr(), n,
+                                            65536, RLE_DYNAMIC, rank == world - 1, 0, comp.data_ptr(), cap, DEV)
+        t_c = ctx.timings()["deflate"]
+        cbytes = (endbits + 7) // 8
+        if world == 1:
+            r, olen, bits = ctx.inflate_raw(comp.data_ptr(), cbytes, dec.data_ptr(), dec.numel(), DEV)
+            ndfl.check(r, "inflate")
+            if r != 0:
+                raise RuntimeError(f"decode error {r}")
+        else:
+            r, olen, bits = distributed_roundtrip_decode(ctx, dist, torch, comp, endbits, dec, rank, world)
+        tm = ctx.timings()
+        state.update(endbits=endbits, cbytes=cbytes, olen=olen, t_deflate=t_c, t_emit=tm["inflate_emit"],
+                     t_find=tm["inflate_find"], t_count=tm["inflate_count"], t_inflate_span=tm["inflate_span"],
+                     chains=tm["inflate_chains"], repairs=tm["inflate_repairs"], cands=tm["inflate_candidates"])
+        return cbytes
+
+    for _ in range(args.warmup):
+        step()
+    if not args.no_verify:
+        assert state["olen"] == n, (state["olen"], n)
+        assert torch.equal(dec[:n], data), "round trip mismatch"
+
+    def barrier():
+        if dist is not None:
+            dist.barrier()
+        torch.cuda.synchronize()
+
+    barrier()
+    t0 = time.perf_counter()
+    for _ in range(args.steps):
+        step()
+    barrier()
+    t1 = time.perf_counter()
+    per = (t1 - t0) / args.steps
+    c_total = state["cbytes"]
+    if dist is not None:
+        t = torch.tensor([per], dtype=torch.float64, device="cuda")
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        per = float(t.item())
+        cb = torch.tensor([state["cbytes"]], dtype=torch.int64, device="cuda")
+        dist.all_reduce(cb)
+        c_total = int(cb.item())
+
+    total_in = world * n + c_total       # bytes fed to compress + bytes fed to decompress
+    value = total_in / per / MIB
+
+    # roofline of the dominant kernel: algorithmic bytes = N + C per launch
+    kd, ke = state["t_deflate"], state["t_emit"]
+    alg = n + state["cbytes"]
+    if ke >= kd:
+        dom, kms = "ndfl_inflate_emit_kernel", ke
+    else:
+        dom, kms = "ndfl_deflate_chunks_kernel", kd
+    achieved = alg / (kms / 1e3)
+
+    cpu = None
+    if rank == 0 and not args.no_cpu:
+        cpu = cpu_baseline(data, args.cpu_sample)
+
+    if rank == 0:
+        line = {
+            "metric": "input MiB/s (compress+decompress)",
+            "value": round(value, 1),
+            "unit": "MiB/s",
+            "n_gpus": world,
+            "steps": args.steps,
+            "warmup": args.warmup,
+            "ms_per_step": round(per * 1e3, 3),
+            "higher_is_better": True,
+            "scaling": "weak",
+            "vs_baseline": None,
+            "dtype": "u8",
+            "data": "synthetic (config-4 Silesia-style mix, seed 0xC4+rank, generated on device)",
+            "config": {"workload": "config4: gzip-default (RLE_DYNAMIC, 64 KiB blocks) compress + decompress of a "
+                                   f"{n >> 30} GiB mixed corpus per GPU, bit-exact",
+                       "bytes_per_gpu": n, "compressed_bytes": c_total, "ratio": round(c_total / (world * n), 4),
+                       "parallelism": f"shard-by-block x{world}"},
+            "phases_ms": {"deflate_kernel": round(kd, 3), "inflate_find": round(state["t_find"], 3),
+                          "inflate_count": round(state["t_count"], 3), "inflate_emit": round(ke, 3),
+                          "inflate_device_span": round(state["t_inflate_span"], 3),
+                          "inflate_chains": int(state["chains"]), "inflate_repairs": int(state["repairs"]),
+                          "inflate_candidates": int(state["cands"])},
+            "roofline": {"bound": "hbm", "kernel": dom, "achieved": round(achieved / 1e9, 2), "peak": HBM_PEAK / 1e9,
+                         "unit": "GB/s", "frac": round(achieved / HBM_PEAK, 4), "traffic": None,
+                         "algorithmic_bytes_per_launch": alg, "avg_kernel_ms": round(kms, 3)},
+            "cpu_baseline": cpu,
+        }
+        print(json.dumps(line), flush=True)
+    if dist is not None:
+        dist.destroy_process_group()
+
+
+def distributed_roundtrip_decode(ctx, dist, torch, comp, endbits, dec, rank, world):
+    raise NotImplementedError
+
+
+def cpu_baseline(data_dev, sample_bytes):
+    """The oracle (C restatement of the reference algorithm, 1 thread) on a bounded sample of the
+    same workload: compress `sample_bytes` of the corpus, decompress the result; same metric."""
+    import oracle_lib as O
+    m = min(sample_bytes, data_dev.numel())
+    host = data_dev[:m].cpu().numpy().tobytes()
+    t0 = time.perf_counter()
+    comp = O.deflate(host)
+    t1 = time.perf_counter()
+    reason, out, _ = O.inflate(comp, out_cap=m + 64)
+    t2 = time.perf_counter()
+    assert reason is None and out == host
+    return {"value": round((m + len(comp)) / (t2 - t0) / MIB, 2), "unit": "MiB/s", "cores": 1, "kind": "port",
+            "sample": f"first {m >> 20} MiB of rank 0's shard: oracle compress {t1 - t0:.2f}s + decompress {t2 - t1:.2f}s",
+            "compress_MiBps": round(m / (t1 - t0) / MIB, 2), "decompress_input_MiBps": round(len(comp) / (t2 - t1) / MIB, 2)}
+
+
+if __name__ == "__main__":
+    main()

@@ -55,6 +55,7 @@ struct ndfl_ctx {
     hipStream_t stream = nullptr;
     hipEvent_t ev0 = nullptr, ev1 = nullptr;
     double last_ms = 0;
+    double deflate_ms = 0;
     DevBuf d_in, d_out, d_status, d_ticket, d_edge_w, d_edge_v, d_crc, d_crc1, d_tabs, d_hostio;
     InflateScratch inf;
     uint32_t* h_pinned = nullptr;   // small pinned area for results
@@ -133,6 +134,14 @@ int ndfl_ctx_set_stream(ndfl_ctx* c, void* s) {
 }
 
 double ndfl_ctx_last_kernel_ms(ndfl_ctx* c) { return c ? c->last_ms : 0.0; }
+
+int ndfl_ctx_timings(ndfl_ctx* c, double* ms, int n) {
+    if (!c || !ms) return NDFL_E_ARG;
+    double v[8] = {c->deflate_ms, c->inf.last_ms_find, c->inf.last_ms_count, c->inf.last_ms_emit,
+                   c->inf.last_ms_wall, (double)c->inf.chains, (double)c->inf.repairs, (double)c->inf.candidates};
+    for (int i = 0; i < n && i < 8; i++) ms[i] = v[i];
+    return n < 8 ? n : 8;
+}
 
 uint64_t ndfl_deflate_bound(uint64_t len, uint32_t chunk_len) {
     if (chunk_len == 0) return 0;
@@ -230,6 +239,7 @@ int ndfl_deflate_chunks(ndfl_ctx* c, const uint8_t* hist, uint32_t hist_len, uin
     float ms = 0;
     hipEventElapsedTime(&ms, c->ev0, c->ev1);
     c->last_ms = ms;
+    c->deflate_ms = ms;
     uint64_t st;
     memcpy(&st, c->h_pinned, 8);
     const uint64_t end_bits = st & ST_VAL;

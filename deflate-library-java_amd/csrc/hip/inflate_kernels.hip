@@ -232,119 +232,154 @@ __device__ int read_dynamic_header(Rd& rd, const In& in, LaneTabs* tabs, bool& e
     return build_tab<true>(d32, nd, &tabs->dist);
 }
 
-// Cheap-then-strict header probe used by the finder (no table output).
-__device__ bool probe_dynamic(const In& in, uint64_t p) {
+// ---- header finder -------------------------------------------------------------------------
+// Strict check of a dynamic block header at bit p, without storing the code lengths: running
+// Kraft sums give exactly the reference's acceptance (complete litlen code with EOB present;
+// empty / single-code-padded / complete distance code), D/decomp/Open.java:336-431.
+__device__ bool strict_dynamic(const In& in, uint64_t p) {
     Rd rd; rd.init(in, p + 3);
     uint32_t hlit = rd.get(in, 5), hdist = rd.get(in, 5), hclen = rd.get(in, 4);
-    const int numLit = (int)hlit + 257, numDist = (int)hdist + 1, numCl = (int)hclen + 4;
+    const uint32_t numLit = hlit + 257, numDist = hdist + 1, numCl = hclen + 4;
+    uint32_t cnt[8], first[8], offs[8];
     uint8_t cl[19];
     for (int i = 0; i < 19; i++) cl[i] = 0;
-    uint32_t kraft = 0, ncodes = 0;
-    for (int i = 0; i < numCl; i++) {
-        uint32_t l = rd.get(in, 3);
-        cl[CL_ORDER[i]] = (uint8_t)l;
-        if (l) { kraft += 128u >> l; ncodes++; }
-    }
-    if (kraft != 128 || ncodes < 2) return false;
-    if (rd.pos > in.nbits) return false;
-    // strict: decode the code lengths with incremental over-full detection
-    rd.init(in, p + 17 + 3 * (uint64_t)numCl);
-    uint16_t cnt[16]; uint16_t first[16], offs[16]; uint16_t sorted[19];
-    for (int l = 0; l < 16; l++) cnt[l] = 0;
-    for (int s = 0; s < 19; s++) cnt[cl[s]]++;
+    for (uint32_t i = 0; i < numCl; i++) cl[CL_ORDER[i]] = (uint8_t)rd.get(in, 3);
+    for (int l = 0; l < 8; l++) cnt[l] = 0;
+    for (int s2 = 0; s2 < 19; s2++) cnt[cl[s2]]++;
     cnt[0] = 0;
+    uint32_t kr = 0;
+    for (int l = 1; l < 8; l++) kr += cnt[l] << (7 - l);
+    if (kr != 128) return false;
+    uint8_t sorted[19];
     {
-        uint32_t code = 0, off = 0;
-        uint16_t nxt[8] = {0, 0, 0, 0, 0, 0, 0, 0};
-        for (int l = 1; l < 8; l++) { code = (code + cnt[l - 1] * (l > 1)) << 1; first[l] = (uint16_t)code; offs[l] = (uint16_t)off; off += cnt[l]; }
-        for (int s = 0; s < 19; s++) if (cl[s]) sorted[offs[cl[s]] + nxt[cl[s]]++] = (uint16_t)s;
+        uint32_t code = 0, off = 0, nxt[8];
+        for (int l = 1; l < 8; l++) { code = (code + (l > 1 ? cnt[l - 1] : 0)) << 1; first[l] = code; offs[l] = off; off += cnt[l]; nxt[l] = 0; }
+        for (int s2 = 0; s2 < 19; s2++) if (cl[s2]) sorted[offs[cl[s2]] + nxt[cl[s2]]++] = (uint8_t)s2;
     }
-    uint8_t lens[320];
-    const int total = numLit + numDist;
+    const uint32_t total = numLit + numDist;
+    uint32_t i = 0;
     int runVal = -1;
-    uint32_t litKraft = 0;      // in units of 2^-15, litlen part only
-    for (int i = 0; i < total;) {
+    uint32_t litK = 0, distK = 0, ones = 0, other = 0, eob = 0, d0 = 0, d31 = 0;
+    while (i < total) {
         rd.fill(in);
-        uint32_t r15 = rev_bits(rd.peek(15), 15);
-        uint32_t sym = 0xFF, len = 0;
+        uint32_t r7 = rev_bits(rd.peek(7), 7);
+        uint32_t sym = 0, len = 0;
         for (uint32_t l = 1; l < 8; l++) {
-            uint32_t idx = (r15 >> (15 - l)) - first[l];
+            uint32_t idx = (r7 >> (7 - l)) - first[l];
             if (idx < cnt[l]) { sym = sorted[offs[l] + idx]; len = l; break; }
         }
         rd.skip(len);
-        if (rd.pos > in.nbits) return false;
-        int runLen = 1;
-        if (sym < 16) { runVal = (int)sym; }
-        else if (sym == 16) { if (runVal < 0) return false; runLen = (int)rd.get(in, 2) + 3; }
-        else if (sym == 17) { runVal = 0; runLen = (int)rd.get(in, 3) + 3; }
-        else { runVal = 0; runLen = (int)rd.get(in, 7) + 11; }
-        if (i + runLen > total) return false;
-        for (int k = 0; k < runLen; k++, i++) {
-            lens[i] = (uint8_t)runVal;
-            if (i < numLit && runVal) { litKraft += 32768u >> runVal; if (litKraft > 32768u) return false; }
+        uint32_t run = 1;
+        if (sym < 16) runVal = (int)sym;
+        else if (sym == 16) { if (runVal < 0) return false; run = rd.get(in, 2) + 3; }
+        else if (sym == 17) { runVal = 0; run = rd.get(in, 3) + 3; }
+        else { runVal = 0; run = rd.get(in, 7) + 11; }
+        if (i + run > total || rd.pos > in.nbits) return false;
+        const uint32_t v = (uint32_t)runVal;
+        const uint32_t e = i + run;
+        if (i < numLit) {
+            uint32_t c = min(e, numLit) - i;
+            if (v) { litK += c * (32768u >> v); if (litK > 32768u) return false; }
+            if (i <= 256 && 256 < e) eob = v;
         }
+        if (e > numLit) {
+            uint32_t a = max(i, numLit) - numLit, b2 = e - numLit;
+            uint32_t c = b2 - a;
+            if (v) { distK += c * (32768u >> v); if (distK > 32768u) return false; if (v == 1) ones += c; else other += c; }
+            if (a == 0) d0 = v;
+            if (a <= 31 && 31 < b2) d31 = v;
+        }
+        i = e;
     }
-    if (rd.pos > in.nbits) return false;
-    if (lens[256] == 0 || litKraft != 32768u) return false;
-    uint16_t c2[16];
-    for (int l = 0; l < 16; l++) c2[l] = 0;
-    for (int s = 0; s < numLit; s++) c2[lens[s]]++;
-    c2[0] = 0;
-    if (tree_check(c2) != 0) return false;
-    const uint8_t* dl = lens + numLit;
-    if (numDist == 1 && dl[0] == 0) return true;
-    for (int l = 0; l < 16; l++) c2[l] = 0;
-    int one = 0, other = 0;
-    for (int s = 0; s < numDist; s++) { c2[dl[s]]++; if (dl[s] == 1) one++; else if (dl[s] > 1) other++; }
-    c2[0] = 0;
-    if (one == 1 && other == 0) { if (numDist == 32 && dl[31] == 1) return false; c2[1]++; }
-    return tree_check(c2) == 0;
+    if (eob == 0 || litK != 32768u) return false;
+    if (numDist == 1 && d0 == 0) return true;
+    if (ones == 1 && other == 0) return !(numDist == 32 && d31 == 1);
+    return distK == 32768u;
 }
 
-__device__ bool probe_stored(const In& in, uint64_t p) {
-    // bits p+1..p+2 == 00 already checked; padding up to the byte boundary must be zero
-    uint64_t q = p + 3;
-    uint64_t al = (q + 7) & ~7ull;
-    Rd rd; rd.init(in, q);
-    if (al > q && rd.peek((uint32_t)(al - q)) != 0) return false;
+// Window helper: n (<= 32) bits at bit offset o of a 5-word window.
+__device__ __forceinline__ uint32_t wbits(const uint32_t (&w)[5], uint32_t o, uint32_t n) {
+    uint32_t k = o >> 5;
+    uint64_t x = (uint64_t)w[k] | ((uint64_t)w[k + 1] << 32);
+    return (uint32_t)(x >> (o & 31)) & (n >= 32 ? 0xFFFFFFFFu : ((1u << n) - 1u));
+}
+
+constexpr uint32_t SEG_CAP = 64;   // candidates kept per finder segment
+
+// A stored block at p (LEN == ~NLEN already checked) must be final or be followed by a plausible
+// header: not btype 3; stored -> LEN == ~NLEN; dynamic -> complete code-length code.
+__device__ bool strict_stored(const In& in, uint64_t p) {
+    Rd rd; rd.init(in, p);
+    const uint32_t bf = rd.get(in, 1);
+    const uint64_t al = (p + 3 + 7) & ~7ull;
     rd.init(in, al);
-    uint32_t ln = rd.peek(16);
-    rd.skip(16);
-    uint32_t nln = rd.peek(16);
-    if (ln != (nln ^ 0xFFFFu)) return false;
-    if (al + 32 + 8ull * ln > in.nbits) return false;
-    return true;
+    const uint32_t ln = rd.get(in, 16);
+    const uint64_t q = al + 32 + 8ull * ln;
+    if (bf) return true;
+    if (q + 3 > in.nbits) return false;
+    rd.init(in, q);
+    rd.get(in, 1);
+    const uint32_t bt2 = rd.get(in, 2);
+    if (bt2 == 3) return false;
+    if (bt2 == 0) {
+        const uint64_t al2 = (q + 3 + 7) & ~7ull;
+        rd.init(in, al2);
+        const uint32_t l2 = rd.get(in, 16), n2 = rd.get(in, 16);
+        return l2 == (n2 ^ 0xFFFFu);
+    }
+    if (bt2 == 2) {
+        rd.get(in, 10);
+        const uint32_t ncl = rd.get(in, 4) + 4;
+        uint32_t kr = 0, nz = 0;
+        for (uint32_t i = 0; i < ncl; i++) { uint32_t l = rd.get(in, 3); if (l) { kr += 128u >> l; nz++; } }
+        return kr == 128 && nz >= 2;
+    }
+    return true;   // fixed block: no cheap check
 }
 
 }  // namespace inf
 
-// ---- kernels --------------------------------------------------------------------------------
-
+// Quick filter over every bit position: each thread tests 32 consecutive positions from a
+// 160-bit register window.  Dynamic: btype 2 and a complete code-length code (Kraft == 1, >= 2
+// codes).  Stored: btype 0, zero padding, LEN == ~NLEN, data inside the stream.  Survivors are
+// appended to their segment's list.
 extern "C" __global__ void __launch_bounds__(256)
-ndfl_inflate_find_kernel(const uint32_t* w, uint64_t nwords, uint64_t nbits, uint32_t nseg, uint64_t* cand) {
+ndfl_inflate_find_kernel(const uint32_t* w, uint64_t nwords, uint64_t nbits, uint32_t* seg_cnt, uint64_t* seg_list) {
     using namespace inf;
-    const uint32_t seg = blockIdx.x * (blockDim.x / 64) + (threadIdx.x >> 6);
-    const int lane = threadIdx.x & 63;
-    if (seg >= nseg) return;
-    if (seg == 0) { if (lane == 0) cand[0] = 0; return; }
+    const uint64_t t = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    const uint64_t p0 = t * 32;
+    if (p0 >= nbits) return;
     In in{w, nwords, nbits};
-    const uint64_t b0 = (uint64_t)seg * SEG_BYTES * 8;
-    const uint64_t b1 = min(b0 + (uint64_t)SEG_BYTES * 8, nbits);
-    uint64_t found = NONE;
-    for (uint64_t base = b0; base < b1; base += 64) {
-        const uint64_t p = base + (uint64_t)lane;
+    uint32_t win[5];
+#pragma unroll
+    for (int k = 0; k < 5; k++) win[k] = in.ld(t + (uint64_t)k);
+    const uint32_t seg = (uint32_t)(p0 / ((uint64_t)SEG_BYTES * 8));
+    for (uint32_t o = 0; o < 32; o++) {
+        const uint64_t p = p0 + o;
+        if (p + 3 > nbits) break;
+        const uint32_t bt = wbits(win, o + 1, 2);
         bool ok = false;
-        if (p + 3 <= nbits && p < b1) {
-            uint64_t wi = p >> 5;
-            uint64_t x = ((uint64_t)in.ld(wi) | ((uint64_t)in.ld(wi + 1) << 32)) >> (p & 31);
-            uint32_t bt = (uint32_t)(x >> 1) & 3u;
-            if (bt == 2) ok = probe_dynamic(in, p);
-            else if (bt == 0) ok = probe_stored(in, p);
+        if (bt == 2) {
+            if (p + 17 > nbits) continue;
+            const uint32_t ncl = wbits(win, o + 13, 4) + 4;
+            uint32_t kr = 0, nz = 0;
+            for (uint32_t i = 0; i < ncl; i++) {
+                uint32_t l = wbits(win, o + 17 + 3 * i, 3);
+                if (l) { kr += 128u >> l; nz++; }
+            }
+            ok = kr == 128 && nz >= 2 && p + 17 + 3 * ncl <= nbits;
+        } else if (bt == 0) {
+            const uint32_t q = o + 3, al = (q + 7) & ~7u;
+            if (al > q && wbits(win, q, al - q) != 0) continue;
+            const uint32_t ln = wbits(win, al, 16), nln = wbits(win, al + 16, 16);
+            ok = ln == (nln ^ 0xFFFFu) && (p0 + al + 32 + 8ull * ln <= nbits);
         }
-        uint64_t m = __ballot(ok);
-        if (m) { found = base + (uint64_t)__builtin_ctzll(m); break; }
+        if (ok) ok = bt == 2 ? strict_dynamic(in, p) : strict_stored(in, p);
+        if (ok) {
+            uint32_t idx = atomicAdd(&seg_cnt[seg], 1u);
+            if (idx < SEG_CAP) seg_list[(uint64_t)seg * SEG_CAP + idx] = p;
+        }
     }
-    if (lane == 0) cand[seg] = found;
 }
 
 struct ChainRes {
@@ -422,7 +457,8 @@ __device__ __forceinline__ bool lane_step(inf::Lane& L, const inf::In& in, inf::
     if (L.state == 1) {
         // stored bytes: the stream is byte aligned here
         uint64_t avail = (in.nbits - min(L.rd.pos, in.nbits)) / 8;
-        uint32_t take = (uint32_t)min((uint64_t)min(L.stored_left, 64u), avail);
+        const uint32_t lim = MODE == 1 ? 32u : 0xFFFFu;
+        uint32_t take = (uint32_t)min((uint64_t)min(L.stored_left, lim), avail);
         if (MODE == 1) {
             for (uint32_t k = 0; k < take; k++) {
                 uint32_t b = L.rd.get(in, 8);
@@ -436,7 +472,7 @@ __device__ __forceinline__ bool lane_step(inf::Lane& L, const inf::In& in, inf::
         }
         L.n += take;
         L.stored_left -= take;
-        if (take < min(L.stored_left + take, 64u)) { L.status = ST_ERROR; L.reason = R_UEOS; L.state = 3; return false; }
+        if (take < min(L.stored_left + take, lim)) { L.status = ST_ERROR; L.reason = R_UEOS; L.state = 3; return false; }
         if (L.stored_left == 0) {
             if (L.last) { L.status = ST_FINAL; L.state = 3; return false; }
             L.state = 0;
@@ -488,11 +524,9 @@ do_copy:
         const uint64_t dst = out_off + L.n;
         const uint64_t src = dst - L.cp_dist;
         if (src < out_off && !(L.cp_dist == 1 && L.n > 0)) {
-            // source precedes this chain: wait for the chain that owns byte `src`
-            // (chains cover [chain_off[j], chain_off[j+1]) in order)
+            // source precedes this chain: wait for the chains that own bytes [src, min(dst, src+len))
             uint32_t lo = 0, hi = my_chain;
             while (lo + 1 < hi) { uint32_t mid = (lo + hi) >> 1; if (chain_off[mid] <= src) lo = mid; else hi = mid; }
-            // also need every chain between lo and my_chain-1 whose bytes the copy may read
             const uint64_t src_end = min(dst, src + L.cp_len);
             uint32_t need_hi = lo;
             while (need_hi + 1 < my_chain && chain_off[need_hi + 1] < src_end) need_hi++;
@@ -501,21 +535,22 @@ do_copy:
             }
             __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
         }
-        const uint32_t len = L.cp_len, dist = L.cp_dist;
-        if (dist == 1) {
-            uint32_t v = (L.n > 0) ? L.lastb : (uint32_t)out[src];
-            for (uint32_t k = 0; k < len; k++) out[dst + k] = (uint8_t)v;
+        // bounded work per step (<= 32 bytes) keeps the lanes of a wave in step
+        const uint32_t take = min(L.cp_len, 32u);
+        if (L.cp_dist == 1) {
+            const uint32_t v = (L.n > 0) ? L.lastb : (uint32_t)out[src];
+            for (uint32_t k = 0; k < take; k++) out[dst + k] = (uint8_t)v;
             L.lastb = v;
         } else {
-            uint32_t b = 0;
-            for (uint32_t k = 0; k < len; k++) {
+            uint32_t b = L.lastb;
+            for (uint32_t k = 0; k < take; k++) {
                 b = out[src + k];
                 out[dst + k] = (uint8_t)b;
             }
             L.lastb = b;
         }
-        L.n += len;
-        L.cp_len = 0;
+        L.n += take;
+        L.cp_len -= take;
     }
     return true;
 }
@@ -606,12 +641,15 @@ struct InflateScratch {
     void* d_done = nullptr; size_t d_done_cap = 0;
     void* d_ticket = nullptr;
     void* d_out = nullptr; size_t d_out_cap = 0;
-    double last_ms_find = 0, last_ms_count = 0, last_ms_emit = 0;
+    double last_ms_find = 0, last_ms_count = 0, last_ms_emit = 0, last_ms_wall = 0;
+    hipEvent_t ev[6] = {nullptr, nullptr, nullptr, nullptr, nullptr, nullptr};
     uint64_t repairs = 0, chains = 0, candidates = 0;
+    bool count_first = false;
     void release() {
         void** ps[] = {&d_in, &d_cand, &d_starts, &d_stops, &d_res, &d_tabs, &d_fixed, &d_chains, &d_off,
                        &d_done, &d_ticket, &d_out};
         for (void** p : ps) { if (*p) hipFree(*p); *p = nullptr; }
+        for (auto& e : ev) { if (e) hipEventDestroy(e); e = nullptr; }
         d_in_cap = d_cand_cap = d_starts_cap = d_stops_cap = d_res_cap = d_tabs_cap = d_chains_cap = 0;
         d_off_cap = d_done_cap = d_out_cap = 0;
     }
@@ -686,56 +724,105 @@ static int inflate_run(InflateScratch& S, hipStream_t s, const uint8_t* in, uint
         INF_CHK(hipMemcpy(S.d_fixed, h, sizeof(LaneTabs), hipMemcpyHostToDevice));
         free(h);
     }
+    if (!S.ev[0]) for (auto& e : S.ev) INF_CHK(hipEventCreate(&e));
     const uint32_t nseg = (uint32_t)std::max<uint64_t>(1, (in_len + SEG_BYTES - 1) / SEG_BYTES);
-    INF_CHK(inf_ensure(&S.d_cand, &S.d_cand_cap, nseg * 8ull));
-    INF_CHK(hipEventRecord(ev0, s));
-    hipLaunchKernelGGL(ndfl_inflate_find_kernel, dim3((nseg + 3) / 4), dim3(256), 0, s, d_w, nwords, nbits, nseg,
-                       (uint64_t*)S.d_cand);
-    INF_CHK(hipGetLastError());
-    std::vector<uint64_t> cand(nseg);
-    INF_CHK(hipMemcpyAsync(cand.data(), S.d_cand, nseg * 8ull, hipMemcpyDeviceToHost, s));
+    INF_CHK(inf_ensure(&S.d_cand, &S.d_cand_cap, (uint64_t)nseg * SEG_CAP * 8ull + (uint64_t)nseg * 4 + 64));
+    uint64_t* d_list = (uint64_t*)S.d_cand;
+    uint32_t* d_cnt = (uint32_t*)((char*)S.d_cand + (uint64_t)nseg * SEG_CAP * 8ull);
+    INF_CHK(hipMemsetAsync(d_cnt, 0, (uint64_t)nseg * 4, s));
+    INF_CHK(hipEventRecord(S.ev[0], s));
+    {
+        const uint64_t nthr = (nbits + 31) / 32;
+        if (nthr)
+            hipLaunchKernelGGL(ndfl_inflate_find_kernel, dim3((uint32_t)((nthr + 255) / 256)), dim3(256), 0, s, d_w,
+                               nwords, nbits, d_cnt, d_list);
+        INF_CHK(hipGetLastError());
+    }
+    INF_CHK(hipEventRecord(S.ev[1], s));
+    std::vector<uint32_t> hcnt(nseg);
+    std::vector<uint64_t> hlist((uint64_t)nseg * SEG_CAP);
+    INF_CHK(hipMemcpyAsync(hcnt.data(), d_cnt, nseg * 4ull, hipMemcpyDeviceToHost, s));
+    INF_CHK(hipMemcpyAsync(hlist.data(), d_list, (uint64_t)nseg * SEG_CAP * 8ull, hipMemcpyDeviceToHost, s));
     INF_CHK(hipStreamSynchronize(s));
     std::vector<uint64_t> starts;
-    starts.reserve(nseg);
-    for (uint32_t k = 0; k < nseg; k++)
-        if (cand[k] != NONE && (starts.empty() || cand[k] > starts.back())) starts.push_back(cand[k]);
+    starts.reserve((size_t)nseg * 4);
+    starts.push_back(0);
+    for (uint32_t k = 0; k < nseg; k++) {
+        const uint32_t c = std::min(hcnt[k], SEG_CAP);
+        const size_t b0 = starts.size();
+        for (uint32_t j = 0; j < c; j++) {
+            const uint64_t v = hlist[(uint64_t)k * SEG_CAP + j];
+            if (v != NONE && v != 0) starts.push_back(v);
+        }
+        std::sort(starts.begin() + b0, starts.end());
+    }
+    const std::vector<uint64_t> sorted_cand(starts);
 
-    // count pass over all candidates; repairs append single chains
-    std::vector<uint64_t> stops(starts.size());
-    for (size_t k = 0; k < starts.size(); k++) stops[k] = k + 1 < starts.size() ? starts[k + 1] : NONE;
+    auto next_after = [&](uint64_t b) -> uint64_t {
+        auto ub = std::upper_bound(sorted_cand.begin(), sorted_cand.end(), b);
+        return ub != sorted_cand.end() ? *ub : NONE;
+    };
     std::vector<ChainRes> res;
-    auto run_count = [&](const std::vector<uint64_t>& st, const std::vector<uint64_t>& sp, std::vector<ChainRes>& r) -> int {
+    auto run_count = [&](const std::vector<uint64_t>& st, std::vector<ChainRes>& r) -> int {
         const size_t n = st.size();
+        std::vector<uint64_t> sp(n);
+        for (size_t k = 0; k < n; k++) sp[k] = next_after(st[k]);
         INF_CHK(inf_ensure(&S.d_starts, &S.d_starts_cap, n * 8));
         INF_CHK(inf_ensure(&S.d_stops, &S.d_stops_cap, n * 8));
         INF_CHK(inf_ensure(&S.d_res, &S.d_res_cap, n * sizeof(ChainRes)));
         INF_CHK(inf_ensure(&S.d_tabs, &S.d_tabs_cap, n * sizeof(LaneTabs)));
         INF_CHK(hipMemcpyAsync(S.d_starts, st.data(), n * 8, hipMemcpyHostToDevice, s));
         INF_CHK(hipMemcpyAsync(S.d_stops, sp.data(), n * 8, hipMemcpyHostToDevice, s));
+        if (S.count_first) INF_CHK(hipEventRecord(S.ev[2], s));
         hipLaunchKernelGGL(ndfl_inflate_count_kernel, dim3((uint32_t)((n + 255) / 256)), dim3(256), 0, s, d_w, nwords,
                            nbits, (const uint64_t*)S.d_starts, (const uint64_t*)S.d_stops, (uint32_t)n,
                            (ChainRes*)S.d_res, (LaneTabs*)S.d_tabs, (const LaneTabs*)S.d_fixed);
         INF_CHK(hipGetLastError());
+        if (S.count_first) { INF_CHK(hipEventRecord(S.ev[3], s)); S.count_first = false; }
         r.resize(n);
         INF_CHK(hipMemcpyAsync(r.data(), S.d_res, n * sizeof(ChainRes), hipMemcpyDeviceToHost, s));
         INF_CHK(hipStreamSynchronize(s));
         return 0;
     };
     S.repairs = 0;
-    int rc = run_count(starts, stops, res);
+    S.count_first = true;
+    int rc = run_count(starts, res);
     if (rc) return rc;
+    {
+        float a = 0, b = 0;
+        hipEventElapsedTime(&a, S.ev[0], S.ev[1]);
+        hipEventElapsedTime(&b, S.ev[2], S.ev[3]);
+        S.last_ms_find = a; S.last_ms_count = b;
+    }
 
-    // link from bit 0
-    const std::vector<uint64_t> sorted_cand(starts);
+    // link from bit 0.  A boundary that is no candidate (fixed-Huffman block, header rejected by
+    // the finder) is repaired: every such boundary of every chain is decoded on in parallel
+    // rounds; a final serial fallback guarantees progress.
     std::unordered_map<uint64_t, size_t> at;
     at.reserve(starts.size() * 2);
     for (size_t k = 0; k < starts.size(); k++) at[starts[k]] = k;
+    for (int round = 0; round < 8; round++) {
+        std::vector<uint64_t> todo;
+        for (size_t k = 0; k < res.size(); k++)
+            if (res[k].status == ST_BOUNDARY && !at.count(res[k].end_bit)) {
+                at[res[k].end_bit] = NONE;          // placeholder, filled below
+                todo.push_back(res[k].end_bit);
+            }
+        if (todo.empty()) break;
+        std::vector<ChainRes> r2;
+        rc = run_count(todo, r2);
+        if (rc) return rc;
+        for (size_t k = 0; k < todo.size(); k++) {
+            starts.push_back(todo[k]);
+            res.push_back(r2[k]);
+            at[todo[k]] = starts.size() - 1;
+        }
+        S.repairs += todo.size();
+    }
     std::vector<EmitChain> chains;
     std::vector<uint64_t> offs;
     uint64_t off = 0;
     size_t cur = 0;
-    int final_status = -1;
-    uint32_t reason = 0;
     uint64_t end_bit = 0;
     for (;;) {
         const ChainRes& r = res[cur];
@@ -747,16 +834,14 @@ static int inflate_run(InflateScratch& S, hipStream_t s, const uint8_t* in, uint
         chains.push_back(ec);
         offs.push_back(off);
         off += r.out_count;
-        if (r.status == ST_FINAL) { final_status = 0; end_bit = r.end_bit; break; }
-        if (r.status == ST_ERROR) { final_status = 1; reason = r.reason; break; }
+        if (r.status == ST_FINAL) { end_bit = r.end_bit; break; }
+        if (r.status == ST_ERROR) break;
         auto it = at.find(r.end_bit);
-        if (it != at.end()) { cur = it->second; continue; }
-        // repair: decode on from this boundary up to the next candidate after it
+        if (it != at.end() && it->second != (size_t)NONE) { cur = it->second; continue; }
+        // serial fallback (beyond the parallel rounds)
         std::vector<uint64_t> st1{r.end_bit};
-        auto ub = std::upper_bound(sorted_cand.begin(), sorted_cand.end(), r.end_bit);
-        std::vector<uint64_t> sp1{ub != sorted_cand.end() ? *ub : NONE};
         std::vector<ChainRes> r1;
-        rc = run_count(st1, sp1, r1);
+        rc = run_count(st1, r1);
         if (rc) return rc;
         starts.push_back(r.end_bit);
         res.push_back(r1[0]);
@@ -786,8 +871,7 @@ static int inflate_run(InflateScratch& S, hipStream_t s, const uint8_t* in, uint
     bool direct = (flags & 2u) != 0;
     if (direct) d_out = out;
     else { INF_CHK(inf_ensure(&S.d_out, &S.d_out_cap, total + 64)); d_out = (uint8_t*)S.d_out; }
-    hipEvent_t e2, e3;
-    hipEventCreate(&e2); hipEventCreate(&e3);
+    hipEvent_t e2 = S.ev[4], e3 = S.ev[5];
     INF_CHK(hipEventRecord(e2, s));
     const uint32_t waves = (nch + 63) / 64;
     hipLaunchKernelGGL(ndfl_inflate_emit_kernel, dim3((waves + 3) / 4), dim3(256), 0, s, d_w, nwords, nbits,
@@ -803,10 +887,10 @@ static int inflate_run(InflateScratch& S, hipStream_t s, const uint8_t* in, uint
     hipEventElapsedTime(&ms, e2, e3);
     S.last_ms_emit = ms;
     float ms2 = 0;
-    hipEventElapsedTime(&ms2, ev0, e3);
+    hipEventElapsedTime(&ms2, S.ev[0], e3);
+    S.last_ms_wall = ms2;
     *last_ms = ms;
-    hipEventDestroy(e2); hipEventDestroy(e3);
-    (void)ev1;
+    (void)ev0; (void)ev1;
     // first error in stream order (the emit pass also checks the dictionary bound exactly)
     uint64_t produced = 0;
     for (uint32_t k = 0; k < nch; k++) {
@@ -818,7 +902,6 @@ static int inflate_run(InflateScratch& S, hipStream_t s, const uint8_t* in, uint
             return (int)er[k].reason;
         }
     }
-    (void)final_status; (void)reason;
     if (!direct && total) INF_CHK(hipMemcpy(out, d_out, total, hipMemcpyDeviceToHost));
     *out_len = total;
     *consumed_bits = end_bit;

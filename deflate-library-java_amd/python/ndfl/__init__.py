@@ -108,6 +108,14 @@ class Context:
     def last_kernel_ms(self):
         return load().ndfl_ctx_last_kernel_ms(self._h)
 
+    def timings(self):
+        """{'deflate', 'inflate_find', 'inflate_count', 'inflate_emit', 'inflate_span'} in ms."""
+        arr = (ctypes.c_double * 8)()
+        load().ndfl_ctx_timings(self._h, arr, 8)
+        keys = ["deflate", "inflate_find", "inflate_count", "inflate_emit", "inflate_span", "inflate_chains",
+                "inflate_repairs", "inflate_candidates"]
+        return dict(zip(keys, list(arr)))
+
     # -- raw C-ABI wrappers ------------------------------------------------------------------
     def deflate_chunks_raw(self, hist_addr, hist_len, hist_limit, data_addr, n, chunk_len, strategy, final,
                            start_bitpos, out_addr, out_cap, flags, crc=None):

@@ -27,7 +27,7 @@ E_ARG, E_UNSUPPORTED, E_CAPACITY, E_DEVICE, E_STATE, E_INTERNAL = -1, -2, -3, -4
 
 # Every symbol include/ndfl.h declares (checked by tests/test_capi_symbols.py).
 EXPORTS = ["ndfl_abi_version", "ndfl_error_string", "ndfl_ctx_create", "ndfl_ctx_destroy",
-           "ndfl_ctx_set_stream", "ndfl_ctx_last_kernel_ms", "ndfl_deflate_chunks", "ndfl_deflate_bound",
+           "ndfl_ctx_set_stream", "ndfl_ctx_last_kernel_ms", "ndfl_ctx_timings", "ndfl_deflate_chunks", "ndfl_deflate_bound",
            "ndfl_inflate", "ndfl_crc32", "ndfl_crc32_combine"]
 
 _lib = None
@@ -49,6 +49,7 @@ def load():
     L.ndfl_ctx_set_stream.argtypes = [vp, vp]
     L.ndfl_ctx_last_kernel_ms.restype = ctypes.c_double
     L.ndfl_ctx_last_kernel_ms.argtypes = [vp]
+    L.ndfl_ctx_timings.argtypes = [vp, ctypes.POINTER(ctypes.c_double), i32]
     L.ndfl_deflate_chunks.argtypes = [vp, vp, u32, u32, vp, u64, u32, i32, i32, u32, vp, u64,
                                       ctypes.POINTER(u64), ctypes.POINTER(u32), u32]
     L.ndfl_deflate_bound.restype = u64

@@ -63,6 +63,10 @@ int ndfl_ctx_destroy(ndfl_ctx* ctx);
 int ndfl_ctx_set_stream(ndfl_ctx* ctx, void* hip_stream);
 /* Average device time (ms) of the last call's dominant kernel, measured with HIP events. */
 double ndfl_ctx_last_kernel_ms(ndfl_ctx* ctx);
+/* Device-time breakdown of the last calls (ms): [0] deflate kernel, [1] inflate finder,
+ * [2] inflate count, [3] inflate emit, [4] inflate device span, [5] linked chains, [6] repaired
+ * boundaries, [7] header candidates. */
+int ndfl_ctx_timings(ndfl_ctx* ctx, double* ms, int n);
 
 /*
  * Compress K consecutive chunks of one DEFLATE stream.
