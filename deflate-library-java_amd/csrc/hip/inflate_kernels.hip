@@ -4,19 +4,23 @@
 // the end of one raw DEFLATE stream (D/InflaterInputStream.java:147-164, D/decomp/Open.java:83-620).
 //
 // A single DEFLATE stream has no block index, so the decoder speculates:
-//   1. finder   (one wave per 64 KiB of compressed input): the first bit position in the segment
-//               that starts a block header which passes the reference's own validity checks
-//               (dynamic: complete code-length code, decodable code lengths, EOB present, complete
-//               litlen/distance codes; stored: LEN == ~NLEN with zero padding) is a candidate;
+//   1. finder   every bit position is tested (32 per lane, bit-parallel btype masks); positions
+//               that start a header passing the reference's own validity checks (dynamic: complete
+//               code-length code, decodable code lengths, EOB present, complete litlen/distance
+//               codes; stored: LEN == ~NLEN, zero padding, plausible successor) are candidates;
 //   2. count    (one lane per candidate): decode blocks from the candidate until the first block
 //               boundary at or past the next candidate, recording end bit, output size, status;
-//   3. link     (host): follow end bit == candidate start from bit 0; a boundary that is not a
-//               candidate (fixed-Huffman block, shadowed header) is repaired by decoding on from it;
+//   3. link     (host): follow end bit == candidate start from bit 0; boundaries that are not
+//               candidates (fixed-Huffman blocks) are decoded on in parallel repair rounds;
 //   4. emit     (one lane per linked chain): decode again into the final output at the chain's
 //               offset.  A copy whose source precedes the chain waits (agent-scope acquire) on the
-//               owning chain's completion flag; chains are claimed in order through a ticket, so a
+//               owning chains' completion flags; chains are claimed in order through a ticket, so a
 //               lane only ever waits on chains whose lanes already run.  The loop is a per-token
-//               step machine so a waiting lane never blocks the other lanes of its wave.
+//               step machine (bounded work per step) so a waiting lane never blocks its wave.
+// Per-lane decoding is latency-bound, so: the bitstream is read through a double-buffered 16-byte
+// prefetch, every Huffman table lives in LDS (lane-interleaved: entry e of lane l at e*64+l, bank
+// conflict-free for any per-lane index), and the dynamic header is parsed in two passes over the
+// stream bits so that no per-lane array (private scratch memory) is ever needed.
 // Errors are the reference's DataFormatException Reasons, checked in the reference's order; the
 // first error in stream order wins.
 // D/ = /root/reference/src/io/nayuki/deflate/
@@ -31,46 +35,66 @@
 namespace inf {
 
 constexpr uint32_t SEG_BYTES = 65536;      // finder segment (compressed bytes)
-constexpr int PRIM = 10;                   // primary table bits
+constexpr uint32_t SEG_CAP = 256;          // candidates kept per finder segment
 constexpr uint64_t NONE = ~0ull;
+
+// per-lane LDS layout, in u16 entries (each entry is 64 lanes wide)
+constexpr uint32_t PL = 8;                 // literal/length primary bits
+constexpr uint32_t PD = 7;                 // distance primary bits (also the code-length code table)
+constexpr uint32_t O_LIT = 0;
+constexpr uint32_t O_DST = O_LIT + (1u << PL);
+constexpr uint32_t O_LF = O_DST + (1u << PD);     // lit first[16]
+constexpr uint32_t O_LC = O_LF + 16;              // lit count[16]
+constexpr uint32_t O_LO = O_LC + 16;              // lit offs[16]
+constexpr uint32_t O_DF = O_LO + 16;
+constexpr uint32_t O_DC = O_DF + 16;
+constexpr uint32_t O_DO = O_DC + 16;
+constexpr uint32_t O_NX = O_DO + 16;              // running ranks during table fill
+constexpr uint32_t LANE_ENTRIES = O_NX + 16;
+constexpr uint32_t LDS_BYTES = LANE_ENTRIES * 64 * 2;
+// global per-lane canonical symbol lists (lane-interleaved per wave): lit 288 + dist 32
+constexpr uint32_t G_SORT = 320;
 
 enum : uint32_t { ST_BOUNDARY = 0, ST_FINAL = 1, ST_ERROR = 2 };
 enum : int { R_UEOS = 1, R_RESERVED_BLOCK_TYPE, R_LEN_MISMATCH, R_UNDER_FULL, R_OVER_FULL, R_NO_PREV,
              R_CL_OVER_FULL, R_EOB_ZERO, R_RESERVED_LEN, R_RESERVED_DIST, R_EMPTY_DIST, R_COPY_BEFORE,
              R_INTERNAL = 100 };
 
-__constant__ uint16_t RUN_BASE[29] = {3,4,5,6,7,8,9,10,11,13,15,17,19,23,27,31,35,43,51,59,67,83,99,115,131,163,195,227,258};
-__constant__ uint8_t RUN_EXTRA[29] = {0,0,0,0,0,0,0,0,1,1,1,1,2,2,2,2,3,3,3,3,4,4,4,4,5,5,5,5,0};
-__constant__ uint16_t DIST_BASE[30] = {1,2,3,4,5,7,9,13,17,25,33,49,65,97,129,193,257,385,513,769,1025,1537,2049,3073,4097,6145,8193,12289,16385,24577};
-__constant__ uint8_t DIST_EXTRA[30] = {0,0,0,0,1,1,2,2,3,3,4,4,5,5,6,6,7,7,8,8,9,9,10,10,11,11,12,12,13,13};
-__constant__ uint8_t CL_ORDER[19] = {16, 17, 18, 0, 8, 7, 9, 6, 10, 5, 11, 4, 12, 3, 13, 2, 14, 1, 15};
+constexpr int CLO[19] = {16, 17, 18, 0, 8, 7, 9, 6, 10, 5, 11, 4, 12, 3, 13, 2, 14, 1, 15};
 
-// Decode table for one Huffman code: primary 2^PRIM entries (sym | len << 9; len 0 = longer
-// code), plus canonical first-code/count/offset per length and the symbols in canonical order.
-struct Tab {
-    uint16_t prim[1 << PRIM];
-    uint16_t sorted[288];
-    uint16_t first[16];
-    uint16_t count[16];
-    uint16_t offs[16];
-};
-struct LaneTabs { Tab lit, dist; };
+// RUN_LENGTH_TABLE / DISTANCE_TABLE of D/decomp/Open.java:841-886 in closed form.
+__device__ __forceinline__ void run_base(uint32_t i, uint32_t& base, uint32_t& ne) {
+    if (i < 8) { base = i + 3; ne = 0; }
+    else if (i == 28) { base = 258; ne = 0; }
+    else { ne = (i >> 2) - 1; base = ((4u + (i & 3)) << ne) + 3; }
+}
+__device__ __forceinline__ void dist_base(uint32_t d, uint32_t& base, uint32_t& ne) {
+    if (d < 4) { base = d + 1; ne = 0; }
+    else { ne = (d >> 1) - 1; base = ((2u + (d & 1)) << ne) + 1; }
+}
 
 struct In {
     const uint32_t* w;
     uint64_t nwords;
     uint64_t nbits;
     __device__ __forceinline__ uint32_t ld(uint64_t i) const { return i < nwords ? w[i] : 0u; }
+    __device__ __forceinline__ u32x4 ld4(uint64_t g) const {
+        if (g * 4 + 3 < nwords) return *(const u32x4*)(w + g * 4);
+        u32x4 r;
+        r.x = ld(g * 4); r.y = ld(g * 4 + 1); r.z = ld(g * 4 + 2); r.w = ld(g * 4 + 3);
+        return r;
+    }
 };
 
+__device__ __forceinline__ uint32_t rev_bits(uint32_t v, uint32_t n) { return __brev(v) >> (32 - n); }
+
+// Simple bit reader (finder / validation paths).
 struct Rd {
-    uint64_t pos;     // absolute position of the next unread bit
-    uint64_t bb;      // buffered bits (LSB = next)
-    uint32_t bn;      // valid bits in bb
-    uint64_t nextw;   // next word to load
+    uint64_t pos, bb;
+    uint32_t bn;
+    uint64_t nextw;
     __device__ __forceinline__ void init(const In& in, uint64_t p) {
-        pos = p;
-        nextw = p >> 5;
+        pos = p; nextw = p >> 5;
         bb = (uint64_t)(in.ld(nextw) >> (p & 31));
         bn = 32 - (uint32_t)(p & 31);
         nextw++;
@@ -89,16 +113,57 @@ struct Rd {
     }
 };
 
-__device__ __forceinline__ uint32_t rev_bits(uint32_t v, uint32_t n) { return __brev(v) >> (32 - n); }
+// Decode-lane bit reader: 64-bit active buffer refilled 32 bits at a time from a 4-word group,
+// with the next 4-word group already in flight (one 16-byte load per 128 bits consumed).
+struct Rp {
+    uint64_t bb;
+    uint32_t bn;
+    uint32_t ci;          // next word of `cur` (0..3)
+    uint64_t qw;          // group index of `cur`
+    uint64_t pos;
+    u32x4 cur, nxt;
+    __device__ __forceinline__ static uint32_t pick(const u32x4& v, uint32_t i) {
+        uint32_t a = (i & 1) ? v.y : v.x, b = (i & 1) ? v.w : v.z;
+        return (i & 2) ? b : a;
+    }
+    __device__ __forceinline__ void adv(const In& in) {
+        if (++ci == 4) { cur = nxt; qw++; nxt = in.ld4(qw + 1); ci = 0; }
+    }
+    __device__ __forceinline__ void init(const In& in, uint64_t p) {
+        pos = p;
+        qw = p >> 7;
+        cur = in.ld4(qw);
+        nxt = in.ld4(qw + 1);
+        ci = (uint32_t)(p >> 5) & 3;
+        bb = (uint64_t)(pick(cur, ci) >> (p & 31));
+        bn = 32 - (uint32_t)(p & 31);
+        adv(in);
+        fill(in);
+    }
+    __device__ __forceinline__ void fill(const In& in) {
+        if (bn <= 32) { bb |= (uint64_t)pick(cur, ci) << bn; bn += 32; adv(in); }
+    }
+    __device__ __forceinline__ uint32_t peek(uint32_t n) const { return (uint32_t)bb & ((1u << n) - 1u); }
+    __device__ __forceinline__ void skip(uint32_t n) { bb >>= n; bn -= n; pos += n; }
+    __device__ __forceinline__ uint32_t get(const In& in, uint32_t n) {
+        fill(in);
+        uint32_t v = n ? peek(n) : 0u;
+        skip(n);
+        return v;
+    }
+};
 
 // codeLengthsToCodeTree's error detection (D/decomp/Open.java:705-756) from per-length counts.
-__device__ int tree_check(const uint16_t* cnt /*[16]*/) {
+__device__ int tree_check(const uint32_t (&cnt)[16]) {
     uint32_t num = 0, maxL = 0;
+#pragma unroll
     for (int l = 1; l < 16; l++) { num += cnt[l]; if (cnt[l]) maxL = (uint32_t)l; }
     if (num < 2) return R_UNDER_FULL;
     const uint64_t R = 2ull * (num - 1);
     uint64_t next = 0, end = 2;
-    for (uint32_t l = 1; l <= maxL; l++) {
+#pragma unroll
+    for (uint32_t l = 1; l < 16; l++) {
+        if (l > maxL) break;
         if (l > 1) {
             uint64_t open = end - next;
             if (open > 0) {
@@ -116,145 +181,269 @@ __device__ int tree_check(const uint16_t* cnt /*[16]*/) {
     return 0;
 }
 
-// Build canonical decoding structure for lens[0..n).  Returns tree_check's verdict.
-template <bool PRIMARY>
-__device__ int build_tab(const uint8_t* lens, int n, Tab* t) {
-    uint16_t cnt[16];
-    for (int l = 0; l < 16; l++) cnt[l] = 0;
-    for (int s = 0; s < n; s++) cnt[lens[s]]++;
-    cnt[0] = 0;
-    int e = tree_check(cnt);
+// LDS view of one lane's tables.
+struct LT {
+    uint16_t* b;          // lane base (entry e at b[e*64])
+    __device__ __forceinline__ uint16_t& at(uint32_t e) const { return b[e * 64]; }
+};
+
+// ---- dynamic block header (D/decomp/Open.java:336-431) ---------------------------------------
+// Pass 1 decodes the code lengths into per-length counts (and validates in the reference's
+// order); pass 2 re-reads the same bits to fill the LDS primary tables and the canonical symbol
+// lists.  `gs` is this lane's canonical-list base in global memory (stride 64).
+__device__ int parse_dynamic(Rp& rd, const In& in, LT t, uint16_t* gs, bool& empty_dist) {
+    const uint32_t hlit = rd.get(in, 5), hdist = rd.get(in, 5), hclen = rd.get(in, 4);
+    if (rd.pos > in.nbits) return R_UEOS;
+    const uint32_t numLit = hlit + 257, numDist = hdist + 1, numCl = hclen + 4;
+    uint32_t cl[19];
+#pragma unroll
+    for (int i = 0; i < 19; i++) cl[i] = 0;
+#pragma unroll
+    for (int i = 0; i < 19; i++)
+        if ((uint32_t)i < numCl) cl[CLO[i]] = rd.get(in, 3);
+    if (rd.pos > in.nbits) return R_UEOS;
+    // code-length code (D/decomp/Open.java:341-344)
+    uint32_t cc[16];
+#pragma unroll
+    for (int l = 0; l < 16; l++) cc[l] = 0;
+#pragma unroll
+    for (int l = 1; l < 8; l++) {
+        uint32_t c = 0;
+#pragma unroll
+        for (int s = 0; s < 19; s++) c += cl[s] == (uint32_t)l;
+        cc[l] = c;
+    }
+    int e = tree_check(cc);
     if (e) return e;
-    uint16_t offs[16], first[16];
-    uint32_t code = 0, off = 0;
-    for (int l = 1; l < 16; l++) {
-        code = (code + (l > 1 ? cnt[l - 1] : 0)) << 1;
-        first[l] = (uint16_t)code;
-        offs[l] = (uint16_t)off;
-        off += cnt[l];
-        t->first[l] = (uint16_t)code;
-        t->count[l] = cnt[l];
-        t->offs[l] = (uint16_t)offs[l];
+    {
+        uint32_t first[8];
+        uint32_t code = 0;
+        first[0] = 0;
+#pragma unroll
+        for (int l = 1; l < 8; l++) { code = (code + (l > 1 ? cc[l - 1] : 0)) << 1; first[l] = code; }
+        for (uint32_t k = 0; k < (1u << PD); k++) t.at(O_DST + k) = 0;
+#pragma unroll
+        for (int s = 0; s < 19; s++) {
+            const uint32_t l = cl[s];
+            if (l) {
+                uint32_t rank = 0;
+#pragma unroll
+                for (int s2 = 0; s2 < s; s2++) rank += cl[s2] == l;
+                uint32_t f = 0;
+#pragma unroll
+                for (int l2 = 1; l2 < 8; l2++) f = (l == (uint32_t)l2) ? first[l2] : f;
+                const uint32_t r = rev_bits(f + rank, l);
+                const uint16_t ent = (uint16_t)(s | (l << 9));
+                for (uint32_t k = r; k < (1u << PD); k += (1u << l)) t.at(O_DST + k) = ent;
+            }
+        }
     }
-    if (PRIMARY) {
-        uint64_t* p64 = (uint64_t*)t->prim;
-        for (int i = 0; i < (1 << PRIM) / 4; i++) p64[i] = 0;
+    // pass 1
+    const Rp saved = rd;
+    for (int l = 0; l < 16; l++) { t.at(O_LC + l) = 0; t.at(O_DC + l) = 0; }
+    const uint32_t total = numLit + numDist;
+    uint32_t i = 0;
+    int runVal = -1;
+    uint32_t eob = 0, ones = 0, other = 0, d0 = 0, d31 = 0;
+    while (i < total) {
+        rd.fill(in);
+        const uint32_t ent = t.at(O_DST + rd.peek(PD));
+        rd.skip(ent >> 9);
+        const uint32_t sym = ent & 0x1FF;
+        if (rd.pos > in.nbits) return R_UEOS;
+        uint32_t run = 1, v;
+        if (sym < 16) { v = sym; runVal = (int)sym; }
+        else if (sym == 16) {
+            if (runVal == -1) return R_NO_PREV;
+            run = rd.get(in, 2) + 3; v = (uint32_t)runVal;
+        } else if (sym == 17) { runVal = 0; run = rd.get(in, 3) + 3; v = 0; }
+        else { runVal = 0; run = rd.get(in, 7) + 11; v = 0; }
+        if (rd.pos > in.nbits) return R_UEOS;
+        if (i + run > total) return R_CL_OVER_FULL;
+        const uint32_t en = i + run;
+        if (i < numLit) {
+            const uint32_t c = min(en, numLit) - i;
+            if (v) t.at(O_LC + v) += (uint16_t)c;
+            if (i <= 256 && 256 < en) eob = v;
+        }
+        if (en > numLit) {
+            const uint32_t a = max(i, numLit) - numLit, b = en - numLit, c = b - a;
+            if (v) { t.at(O_DC + v) += (uint16_t)c; if (v == 1) ones += c; else other += c; }
+            if (a == 0) d0 = v;
+            if (a <= 31 && 31 < b) d31 = v;
+        }
+        i = en;
     }
-    uint16_t nxt[16];
-    for (int l = 0; l < 16; l++) nxt[l] = 0;
-    for (int s = 0; s < n; s++) {
-        uint32_t l = lens[s];
-        if (!l) continue;
-        uint32_t rank = nxt[l]++;
-        t->sorted[offs[l] + rank] = (uint16_t)s;
-        if (PRIMARY && l <= (uint32_t)PRIM) {
-            uint32_t r = rev_bits(first[l] + rank, l);
-            uint16_t ent = (uint16_t)(s | (l << 9));
-            for (uint32_t k = r; k < (1u << PRIM); k += (1u << l)) t->prim[k] = ent;
+    if (eob == 0) return R_EOB_ZERO;
+    uint32_t lc[16], dc[16];
+#pragma unroll
+    for (int l = 0; l < 16; l++) { lc[l] = l ? t.at(O_LC + l) : 0u; dc[l] = l ? t.at(O_DC + l) : 0u; }
+    e = tree_check(lc);
+    if (e) return e;
+    bool pad31 = false;
+    empty_dist = (numDist == 1 && d0 == 0);
+    if (!empty_dist) {
+        if (ones == 1 && other == 0) { pad31 = true; dc[1] += 1; if (numDist == 32 && d31 == 1) dc[1] -= 1; }
+        e = tree_check(dc);
+        if (e) return e;
+    }
+    {
+        uint32_t code = 0, off = 0;
+#pragma unroll
+        for (int l = 1; l < 16; l++) {
+            code = (code + (l > 1 ? lc[l - 1] : 0)) << 1;
+            t.at(O_LF + l) = (uint16_t)code; t.at(O_LO + l) = (uint16_t)off; t.at(O_LC + l) = (uint16_t)lc[l];
+            off += lc[l];
+        }
+        code = 0; off = 0;
+#pragma unroll
+        for (int l = 1; l < 16; l++) {
+            code = (code + (l > 1 ? dc[l - 1] : 0)) << 1;
+            t.at(O_DF + l) = (uint16_t)code; t.at(O_DO + l) = (uint16_t)off; t.at(O_DC + l) = (uint16_t)dc[l];
+            off += dc[l];
+        }
+    }
+    // pass 2: literal/length table + canonical list; distance lengths packed into 4 registers
+    for (uint32_t k = 0; k < (1u << PL); k++) t.at(O_LIT + k) = 0;
+    for (int l = 0; l < 16; l++) t.at(O_NX + l) = 0;
+    rd = saved;
+    i = 0;
+    runVal = 0;
+    uint32_t dpk[4] = {0, 0, 0, 0};
+    while (i < total) {
+        rd.fill(in);
+        const uint32_t ent = t.at(O_DST + rd.peek(PD));
+        rd.skip(ent >> 9);
+        const uint32_t sym = ent & 0x1FF;
+        uint32_t run = 1, v;
+        if (sym < 16) { v = sym; runVal = (int)sym; }
+        else if (sym == 16) { run = rd.get(in, 2) + 3; v = (uint32_t)runVal; }
+        else if (sym == 17) { runVal = 0; run = rd.get(in, 3) + 3; v = 0; }
+        else { runVal = 0; run = rd.get(in, 7) + 11; v = 0; }
+        if (v) {
+            for (uint32_t k = 0; k < run; k++) {
+                const uint32_t idx = i + k;
+                if (idx < numLit) {
+                    const uint32_t rank = t.at(O_NX + v);
+                    t.at(O_NX + v) = (uint16_t)(rank + 1);
+                    gs[(t.at(O_LO + v) + rank) * 64] = (uint16_t)idx;
+                    if (v <= PL) {
+                        const uint32_t r = rev_bits(t.at(O_LF + v) + rank, v);
+                        const uint16_t en2 = (uint16_t)(idx | (v << 9));
+                        for (uint32_t q = r; q < (1u << PL); q += (1u << v)) t.at(O_LIT + q) = en2;
+                    }
+                } else {
+                    const uint32_t j = idx - numLit;
+                    const uint32_t sh = (j & 7) * 4, w = j >> 3;
+                    dpk[0] |= (w == 0) ? (v << sh) : 0u;
+                    dpk[1] |= (w == 1) ? (v << sh) : 0u;
+                    dpk[2] |= (w == 2) ? (v << sh) : 0u;
+                    dpk[3] |= (w == 3) ? (v << sh) : 0u;
+                }
+            }
+        }
+        i += run;
+    }
+    if (empty_dist) return 0;
+    if (pad31) dpk[3] |= 1u << 28;      // dummy code at index 31 (D/decomp/Open.java:411-425)
+    for (uint32_t k = 0; k < (1u << PD); k++) t.at(O_DST + k) = 0;
+    for (int l = 0; l < 16; l++) t.at(O_NX + l) = 0;
+#pragma unroll
+    for (int j = 0; j < 32; j++) {
+        const uint32_t v = (dpk[j >> 3] >> ((j & 7) * 4)) & 15u;
+        if (v) {
+            const uint32_t rank = t.at(O_NX + v);
+            t.at(O_NX + v) = (uint16_t)(rank + 1);
+            gs[(288 + t.at(O_DO + v) + rank) * 64] = (uint16_t)j;
+            if (v <= PD) {
+                const uint32_t r = rev_bits(t.at(O_DF + v) + rank, v);
+                const uint16_t en2 = (uint16_t)(j | (v << 9));
+                for (uint32_t q = r; q < (1u << PD); q += (1u << v)) t.at(O_DST + q) = en2;
+            }
         }
     }
     return 0;
 }
 
-// Canonical decode starting at length `from` (slow path).  Codes are complete, so it terminates.
-__device__ __forceinline__ uint32_t slow_decode(const Tab* t, uint32_t bits15, uint32_t from, uint32_t& len) {
-    uint32_t r15 = rev_bits(bits15, 15);
-    for (uint32_t l = from; l < 16; l++) {
-        uint32_t c = r15 >> (15 - l);
-        uint32_t idx = c - t->first[l];
-        if (idx < t->count[l]) { len = l; return t->sorted[t->offs[l] + idx]; }
-    }
-    len = 15;
-    return 0xFFFF;   // unreachable for complete codes
-}
-
-__device__ __forceinline__ uint32_t decode_sym(const Tab* t, Rd& rd, const In& in) {
+// Literal/length symbol: LDS primary, canonical slow path for longer codes.
+__device__ __forceinline__ uint32_t dec_lit(Rp& rd, const In& in, LT t, const uint16_t* gs) {
     rd.fill(in);
-    uint32_t e = t->prim[rd.peek(PRIM)];
-    uint32_t len = e >> 9;
-    uint32_t sym;
-    if (len) sym = e & 0x1FF;
-    else sym = slow_decode(t, rd.peek(15), PRIM + 1, len);
-    rd.skip(len);
-    return sym;
+    const uint32_t e = t.at(O_LIT + rd.peek(PL));
+    if (e >> 9) { rd.skip(e >> 9); return e & 0x1FF; }
+    const uint32_t r15 = rev_bits(rd.peek(15), 15);
+    for (uint32_t l = PL + 1; l < 16; l++) {
+        const uint32_t idx = (r15 >> (15 - l)) - t.at(O_LF + l);
+        if (idx < t.at(O_LC + l)) { rd.skip(l); return gs[(t.at(O_LO + l) + idx) * 64]; }
+    }
+    rd.skip(15);
+    return 0xFFFF;
+}
+__device__ __forceinline__ uint32_t dec_dist(Rp& rd, const In& in, LT t, const uint16_t* gs) {
+    rd.fill(in);
+    const uint32_t e = t.at(O_DST + rd.peek(PD));
+    if (e >> 9) { rd.skip(e >> 9); return e & 0x1FF; }
+    const uint32_t r15 = rev_bits(rd.peek(15), 15);
+    for (uint32_t l = PD + 1; l < 16; l++) {
+        const uint32_t idx = (r15 >> (15 - l)) - t.at(O_DF + l);
+        if (idx < t.at(O_DC + l)) { rd.skip(l); return gs[(288 + t.at(O_DO + l) + idx) * 64]; }
+    }
+    rd.skip(15);
+    return 0xFFFF;
 }
 
-// Dynamic block header (D/decomp/Open.java:336-431).  On success fills the lane's tables and
-// sets empty_dist.  Returns 0 or a Reason.
-__device__ int read_dynamic_header(Rd& rd, const In& in, LaneTabs* tabs, bool& empty_dist) {
-    uint32_t hlit = rd.get(in, 5), hdist = rd.get(in, 5), hclen = rd.get(in, 4);
-    if (rd.pos > in.nbits) return R_UEOS;
-    const int numLit = (int)hlit + 257, numDist = (int)hdist + 1, numCl = (int)hclen + 4;
-    uint8_t cl[19];
-    for (int i = 0; i < 19; i++) cl[i] = 0;
-    for (int i = 0; i < numCl; i++) {
-        cl[CL_ORDER[i]] = (uint8_t)rd.get(in, 3);
-        if (rd.pos > in.nbits) return R_UEOS;
-    }
-    // code-length code: canonical arrays only (max 7 bits), kept in the dist slot temporarily
-    Tab* ct = &tabs->dist;
-    int e = build_tab<false>(cl, 19, ct);
-    if (e) return e;
-    uint8_t lens[320];
-    const int total = numLit + numDist;
-    int runVal = -1;
-    for (int i = 0; i < total;) {
-        rd.fill(in);
-        uint32_t len;
-        uint32_t sym = slow_decode(ct, rd.peek(15), 1, len);
-        rd.skip(len);
-        if (rd.pos > in.nbits) return R_UEOS;
-        if (sym < 16) { runVal = (int)sym; lens[i++] = (uint8_t)sym; continue; }
-        int runLen;
-        if (sym == 16) {
-            if (runVal == -1) return R_NO_PREV;
-            runLen = (int)rd.get(in, 2) + 3;
-        } else if (sym == 17) { runVal = 0; runLen = (int)rd.get(in, 3) + 3; }
-        else { runVal = 0; runLen = (int)rd.get(in, 7) + 11; }
-        if (rd.pos > in.nbits) return R_UEOS;
-        for (; runLen > 0; runLen--, i++) {
-            if (i >= total) return R_CL_OVER_FULL;
-            lens[i] = (uint8_t)runVal;
-        }
-    }
-    if (lens[256] == 0) return R_EOB_ZERO;
-    e = build_tab<true>(lens, numLit, &tabs->lit);
-    if (e) return e;
-    uint8_t* dl = lens + numLit;
-    int nd = numDist;
-    if (nd == 1 && dl[0] == 0) { empty_dist = true; return 0; }
-    empty_dist = false;
-    int one = 0, other = 0;
-    for (int i = 0; i < nd; i++) { if (dl[i] == 1) one++; else if (dl[i] > 1) other++; }
-    uint8_t d32[32];
-    for (int i = 0; i < 32; i++) d32[i] = i < nd ? dl[i] : 0;
-    if (one == 1 && other == 0) { nd = 32; d32[31] = 1; }
-    return build_tab<true>(d32, nd, &tabs->dist);
-}
+// Fixed-Huffman tables (D/decomp/Open.java:812-830): 9-bit literal/length and 5-bit distance
+// primaries, shared by all lanes (global, cache-resident).
+struct FixedTabs { uint16_t lit[512]; uint16_t dist[32]; };
 
-// ---- header finder -------------------------------------------------------------------------
-// Strict check of a dynamic block header at bit p, without storing the code lengths: running
-// Kraft sums give exactly the reference's acceptance (complete litlen code with EOB present;
-// empty / single-code-padded / complete distance code), D/decomp/Open.java:336-431.
+// ---- finder ---------------------------------------------------------------------------------
+// Strict check of a dynamic block header at bit p with running Kraft sums (no arrays): accepts
+// exactly the headers the reference accepts.
 __device__ bool strict_dynamic(const In& in, uint64_t p) {
     Rd rd; rd.init(in, p + 3);
-    uint32_t hlit = rd.get(in, 5), hdist = rd.get(in, 5), hclen = rd.get(in, 4);
+    const uint32_t hlit = rd.get(in, 5), hdist = rd.get(in, 5), hclen = rd.get(in, 4);
     const uint32_t numLit = hlit + 257, numDist = hdist + 1, numCl = hclen + 4;
-    uint32_t cnt[8], first[8], offs[8];
-    uint8_t cl[19];
+    uint32_t cl[19];
+#pragma unroll
     for (int i = 0; i < 19; i++) cl[i] = 0;
-    for (uint32_t i = 0; i < numCl; i++) cl[CL_ORDER[i]] = (uint8_t)rd.get(in, 3);
-    for (int l = 0; l < 8; l++) cnt[l] = 0;
-    for (int s2 = 0; s2 < 19; s2++) cnt[cl[s2]]++;
-    cnt[0] = 0;
+#pragma unroll
+    for (int i = 0; i < 19; i++)
+        if ((uint32_t)i < numCl) cl[CLO[i]] = rd.get(in, 3);
+    uint32_t cc[8];
+#pragma unroll
+    for (int l = 0; l < 8; l++) cc[l] = 0;
+#pragma unroll
+    for (int l = 1; l < 8; l++) {
+        uint32_t c = 0;
+#pragma unroll
+        for (int s = 0; s < 19; s++) c += cl[s] == (uint32_t)l;
+        cc[l] = c;
+    }
     uint32_t kr = 0;
-    for (int l = 1; l < 8; l++) kr += cnt[l] << (7 - l);
+#pragma unroll
+    for (int l = 1; l < 8; l++) kr += cc[l] << (7 - l);
     if (kr != 128) return false;
-    uint8_t sorted[19];
+    uint32_t first[8], offs[8];
     {
-        uint32_t code = 0, off = 0, nxt[8];
-        for (int l = 1; l < 8; l++) { code = (code + (l > 1 ? cnt[l - 1] : 0)) << 1; first[l] = code; offs[l] = off; off += cnt[l]; nxt[l] = 0; }
-        for (int s2 = 0; s2 < 19; s2++) if (cl[s2]) sorted[offs[cl[s2]] + nxt[cl[s2]]++] = (uint8_t)s2;
+        uint32_t code = 0, off = 0;
+        first[0] = 0; offs[0] = 0;
+#pragma unroll
+        for (int l = 1; l < 8; l++) { code = (code + (l > 1 ? cc[l - 1] : 0)) << 1; first[l] = code; offs[l] = off; off += cc[l]; }
+    }
+    // canonical symbol list packed 6 x 5 bits per register
+    uint32_t pk[4] = {0, 0, 0, 0};
+#pragma unroll
+    for (int s = 0; s < 19; s++) {
+        const uint32_t l = cl[s];
+        if (l) {
+            uint32_t rank = 0, o = 0;
+#pragma unroll
+            for (int s2 = 0; s2 < s; s2++) rank += cl[s2] == l;
+#pragma unroll
+            for (int l2 = 1; l2 < 8; l2++) o = (l == (uint32_t)l2) ? offs[l2] : o;
+            const uint32_t pos = o + rank, wd = pos / 6, sh = (pos % 6) * 5;
+#pragma unroll
+            for (int q = 0; q < 4; q++) pk[q] |= (wd == (uint32_t)q) ? ((uint32_t)s << sh) : 0u;
+        }
     }
     const uint32_t total = numLit + numDist;
     uint32_t i = 0;
@@ -262,11 +451,18 @@ __device__ bool strict_dynamic(const In& in, uint64_t p) {
     uint32_t litK = 0, distK = 0, ones = 0, other = 0, eob = 0, d0 = 0, d31 = 0;
     while (i < total) {
         rd.fill(in);
-        uint32_t r7 = rev_bits(rd.peek(7), 7);
-        uint32_t sym = 0, len = 0;
-        for (uint32_t l = 1; l < 8; l++) {
-            uint32_t idx = (r7 >> (7 - l)) - first[l];
-            if (idx < cnt[l]) { sym = sorted[offs[l] + idx]; len = l; break; }
+        const uint32_t r7 = rev_bits(rd.peek(7), 7);
+        uint32_t sym = 0, len = 0, gi = 0;
+#pragma unroll
+        for (int l = 1; l < 8; l++) {
+            const uint32_t idx = (r7 >> (7 - l)) - first[l];
+            if (len == 0 && idx < cc[l]) { len = (uint32_t)l; gi = offs[l] + idx; }
+        }
+        {
+            const uint32_t wd = gi / 6, sh = (gi % 6) * 5;
+            uint32_t x = pk[0];
+            x = wd == 1 ? pk[1] : x; x = wd == 2 ? pk[2] : x; x = wd == 3 ? pk[3] : x;
+            sym = (x >> sh) & 31u;
         }
         rd.skip(len);
         uint32_t run = 1;
@@ -276,35 +472,25 @@ __device__ bool strict_dynamic(const In& in, uint64_t p) {
         else { runVal = 0; run = rd.get(in, 7) + 11; }
         if (i + run > total || rd.pos > in.nbits) return false;
         const uint32_t v = (uint32_t)runVal;
-        const uint32_t e = i + run;
+        const uint32_t en = i + run;
         if (i < numLit) {
-            uint32_t c = min(e, numLit) - i;
+            const uint32_t c = min(en, numLit) - i;
             if (v) { litK += c * (32768u >> v); if (litK > 32768u) return false; }
-            if (i <= 256 && 256 < e) eob = v;
+            if (i <= 256 && 256 < en) eob = v;
         }
-        if (e > numLit) {
-            uint32_t a = max(i, numLit) - numLit, b2 = e - numLit;
-            uint32_t c = b2 - a;
+        if (en > numLit) {
+            const uint32_t a = max(i, numLit) - numLit, b2 = en - numLit, c = b2 - a;
             if (v) { distK += c * (32768u >> v); if (distK > 32768u) return false; if (v == 1) ones += c; else other += c; }
             if (a == 0) d0 = v;
             if (a <= 31 && 31 < b2) d31 = v;
         }
-        i = e;
+        i = en;
     }
     if (eob == 0 || litK != 32768u) return false;
     if (numDist == 1 && d0 == 0) return true;
     if (ones == 1 && other == 0) return !(numDist == 32 && d31 == 1);
     return distK == 32768u;
 }
-
-// Window helper: n (<= 32) bits at bit offset o of a 5-word window.
-__device__ __forceinline__ uint32_t wbits(const uint32_t (&w)[5], uint32_t o, uint32_t n) {
-    uint32_t k = o >> 5;
-    uint64_t x = (uint64_t)w[k] | ((uint64_t)w[k + 1] << 32);
-    return (uint32_t)(x >> (o & 31)) & (n >= 32 ? 0xFFFFFFFFu : ((1u << n) - 1u));
-}
-
-constexpr uint32_t SEG_CAP = 64;   // candidates kept per finder segment
 
 // A stored block at p (LEN == ~NLEN already checked) must be final or be followed by a plausible
 // header: not btype 3; stored -> LEN == ~NLEN; dynamic -> complete code-length code.
@@ -339,46 +525,99 @@ __device__ bool strict_stored(const In& in, uint64_t p) {
 
 }  // namespace inf
 
-// Quick filter over every bit position: each thread tests 32 consecutive positions from a
-// 160-bit register window.  Dynamic: btype 2 and a complete code-length code (Kraft == 1, >= 2
-// codes).  Stored: btype 0, zero padding, LEN == ~NLEN, data inside the stream.  Survivors are
-// appended to their segment's list.
+// Header finder over every bit position.  Each thread tests 32 consecutive positions: btype masks
+// for all 32 come from two shifts of a 64-bit window; the per-position tests read a 128-bit
+// funnel-shifted window with compile-time offsets only (no private arrays).  Survivors are
+// gathered per workgroup in LDS and strictly validated one per lane, then appended to their
+// 64 KiB segment's list.
 extern "C" __global__ void __launch_bounds__(256)
 ndfl_inflate_find_kernel(const uint32_t* w, uint64_t nwords, uint64_t nbits, uint32_t* seg_cnt, uint64_t* seg_list) {
     using namespace inf;
+    __shared__ uint64_t cand[1024];
+    __shared__ uint32_t ncand;
+    if (threadIdx.x == 0) ncand = 0;
+    __syncthreads();
     const uint64_t t = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
     const uint64_t p0 = t * 32;
-    if (p0 >= nbits) return;
     In in{w, nwords, nbits};
-    uint32_t win[5];
-#pragma unroll
-    for (int k = 0; k < 5; k++) win[k] = in.ld(t + (uint64_t)k);
-    const uint32_t seg = (uint32_t)(p0 / ((uint64_t)SEG_BYTES * 8));
-    for (uint32_t o = 0; o < 32; o++) {
-        const uint64_t p = p0 + o;
-        if (p + 3 > nbits) break;
-        const uint32_t bt = wbits(win, o + 1, 2);
-        bool ok = false;
-        if (bt == 2) {
-            if (p + 17 > nbits) continue;
-            const uint32_t ncl = wbits(win, o + 13, 4) + 4;
+    if (p0 < nbits) {
+        const uint32_t w0 = in.ld(t), w1 = in.ld(t + 1), w2 = in.ld(t + 2), w3 = in.ld(t + 3), w4 = in.ld(t + 4);
+        const uint64_t W = (uint64_t)w0 | ((uint64_t)w1 << 32);
+        const uint32_t b1 = (uint32_t)(W >> 1), b2 = (uint32_t)(W >> 2);
+        uint32_t valid = 0xFFFFFFFFu;
+        if (p0 + 35 > nbits) valid = (nbits >= p0 + 3) ? (uint32_t)((1ull << (nbits - p0 - 2)) - 1) : 0u;
+        uint32_t m2 = ~b1 & b2 & valid;
+        uint32_t m0 = ~b1 & ~b2 & valid;
+        const uint64_t lo = W, hi = (uint64_t)w2 | ((uint64_t)w3 << 32);
+        while (m2) {
+            const uint32_t o = __builtin_ctz(m2);
+            m2 &= m2 - 1;
+            // 96 bits starting at position o: x0 = bits [o, o+64), x1 = bits [o+64, o+96)
+            const uint64_t x0 = o ? (lo >> o) | (hi << (64 - o)) : lo;
+            const uint64_t hw = (uint64_t)w3 | ((uint64_t)w4 << 32);
+            const uint32_t x1 = (uint32_t)((o ? (hi >> o) | (hw << (64 - o)) : hi));
+            const uint32_t ncl = (uint32_t)(x0 >> 13) & 15u;
+            // 19 x 3-bit lengths at offsets 17..73 (relative to o)
             uint32_t kr = 0, nz = 0;
-            for (uint32_t i = 0; i < ncl; i++) {
-                uint32_t l = wbits(win, o + 17 + 3 * i, 3);
-                if (l) { kr += 128u >> l; nz++; }
+#pragma unroll
+            for (int i = 0; i < 19; i++) {
+                const int off = 17 + 3 * i;
+                uint32_t l;
+                if (off + 3 <= 64) l = (uint32_t)(x0 >> off) & 7u;
+                else if (off >= 64) l = (x1 >> (off - 64)) & 7u;
+                else l = (uint32_t)((x0 >> off) | ((uint64_t)x1 << (64 - off))) & 7u;
+                const bool in_range = (uint32_t)i < ncl + 4;
+                kr += (in_range && l) ? (128u >> l) : 0u;
+                nz += in_range && l;
             }
-            ok = kr == 128 && nz >= 2 && p + 17 + 3 * ncl <= nbits;
-        } else if (bt == 0) {
-            const uint32_t q = o + 3, al = (q + 7) & ~7u;
-            if (al > q && wbits(win, q, al - q) != 0) continue;
-            const uint32_t ln = wbits(win, al, 16), nln = wbits(win, al + 16, 16);
-            ok = ln == (nln ^ 0xFFFFu) && (p0 + al + 32 + 8ull * ln <= nbits);
+            if (kr == 128 && nz >= 2 && p0 + o + 17 + 3 * (ncl + 4) <= nbits) {
+                uint32_t k = atomicAdd(&ncand, 1u);
+                if (k < 1024) cand[k] = (p0 + o) | (1ull << 63);
+            }
         }
-        if (ok) ok = bt == 2 ? strict_dynamic(in, p) : strict_stored(in, p);
+        while (m0) {
+            const uint32_t o = __builtin_ctz(m0);
+            m0 &= m0 - 1;
+            const uint32_t q = o + 3, al = (q + 7) & ~7u;            // al <= 40
+            const uint64_t x = al ? (lo >> al) | (hi << (64 - al)) : lo;
+            const uint32_t pad = al > q ? (uint32_t)(lo >> q) & ((1u << (al - q)) - 1u) : 0u;
+            if (pad) continue;
+            const uint32_t ln = (uint32_t)x & 0xFFFFu, nln = (uint32_t)(x >> 16) & 0xFFFFu;
+            if (ln == (nln ^ 0xFFFFu) && p0 + al + 32 + 8ull * ln <= nbits) {
+                uint32_t k = atomicAdd(&ncand, 1u);
+                if (k < 1024) cand[k] = p0 + o;
+            }
+        }
+    }
+    __syncthreads();
+    const uint32_t nc = min(ncand, 1024u);
+    for (uint32_t k = threadIdx.x; k < nc; k += blockDim.x) {
+        const uint64_t e = cand[k];
+        const uint64_t p = e & ~(1ull << 63);
+        const bool ok = (e >> 63) ? strict_dynamic(in, p) : strict_stored(in, p);
         if (ok) {
+            const uint32_t seg = (uint32_t)(p / ((uint64_t)SEG_BYTES * 8));
             uint32_t idx = atomicAdd(&seg_cnt[seg], 1u);
             if (idx < SEG_CAP) seg_list[(uint64_t)seg * SEG_CAP + idx] = p;
         }
+    }
+}
+
+// Sort each segment's candidates (arrival order is arbitrary) and compact them into one sorted
+// list at the offsets of an exclusive scan of the segment counts.
+extern "C" __global__ void __launch_bounds__(256)
+ndfl_inflate_compact_kernel(const uint32_t* seg_cnt, const uint64_t* seg_list, const uint64_t* seg_off,
+                            uint32_t nseg, uint64_t* out) {
+    using namespace inf;
+    const uint32_t seg = blockIdx.x * blockDim.x + threadIdx.x;
+    if (seg >= nseg) return;
+    const uint32_t c = min(seg_cnt[seg], SEG_CAP);
+    uint64_t* o = out + seg_off[seg];
+    for (uint32_t i = 0; i < c; i++) {
+        uint64_t v = seg_list[(uint64_t)seg * SEG_CAP + i];
+        uint32_t j = i;
+        while (j > 0 && o[j - 1] > v) { o[j] = o[j - 1]; j--; }
+        o[j] = v;
     }
 }
 
@@ -398,195 +637,275 @@ struct EmitChain {
 
 namespace inf {
 
-// Per-lane decode state machine.  MODE 0 = count, 1 = emit.
+// Huffman-block symbol decoders shared by both passes.
+__device__ __forceinline__ uint32_t lit_sym(bool fixed, Rp& rd, const In& in, LT t, const uint16_t* gs,
+                                            const FixedTabs* fx) {
+    if (fixed) {
+        rd.fill(in);
+        const uint32_t e = fx->lit[rd.peek(9)];
+        rd.skip(e >> 9);
+        return e & 0x1FF;
+    }
+    return dec_lit(rd, in, t, gs);
+}
+__device__ __forceinline__ uint32_t dist_sym(bool fixed, Rp& rd, const In& in, LT t, const uint16_t* gs,
+                                             const FixedTabs* fx) {
+    if (fixed) {
+        rd.fill(in);
+        const uint32_t e = fx->dist[rd.peek(5)];
+        rd.skip(5);
+        return e & 0x1FF;
+    }
+    return dec_dist(rd, in, t, gs);
+}
+
+// Count pass for one chain: straight-line decode, no output.  Stops at the first block boundary at
+// or past `stop`, after a final block, or at the first error (reference check order).
+__device__ void count_chain(uint64_t start, uint64_t stop, bool abs0, const In& in, LT t, uint16_t* gs,
+                            const FixedTabs* fx, ChainRes& res) {
+    Rp rd;
+    rd.init(in, start);
+    uint64_t n = 0;
+    uint32_t status = ST_BOUNDARY, reason = 0;
+#define CFAIL(r) do { status = ST_ERROR; reason = (r); goto out; } while (0)
+    for (;;) {
+        if (rd.pos >= stop) break;                       // (start < stop: first block always decoded)
+        const uint32_t bf = rd.get(in, 1), bt = rd.get(in, 2);
+        if (rd.pos > in.nbits) CFAIL(R_UEOS);
+        if (bt == 3) CFAIL(R_RESERVED_BLOCK_TYPE);
+        if (bt == 0) {
+            const uint32_t pad = (uint32_t)((8 - (rd.pos & 7)) & 7);
+            rd.get(in, pad);
+            const uint32_t ln = rd.get(in, 16), nln = rd.get(in, 16);
+            if (rd.pos > in.nbits) CFAIL(R_UEOS);
+            if (ln != (nln ^ 0xFFFFu)) CFAIL(R_LEN_MISMATCH);
+            const uint64_t avail = (in.nbits - rd.pos) / 8;
+            const uint64_t take = min((uint64_t)ln, avail);
+            n += take;
+            rd.init(in, rd.pos + 8 * take);
+            if (take < ln) CFAIL(R_UEOS);
+            if (bf) { status = ST_FINAL; break; }
+            continue;
+        }
+        const bool fixed = bt == 1;
+        bool empty_dist = false;
+        if (!fixed) {
+            const int e = parse_dynamic(rd, in, t, gs, empty_dist);
+            if (e) CFAIL((uint32_t)e);
+        }
+        for (;;) {
+            const uint32_t sym = lit_sym(fixed, rd, in, t, gs, fx);
+            if (rd.pos > in.nbits) CFAIL(R_UEOS);
+            if (sym < 256) { n++; continue; }
+            if (sym == 256) break;
+            if (sym > 285) CFAIL(R_RESERVED_LEN);
+            uint32_t base, ne;
+            run_base(sym - 257, base, ne);
+            const uint32_t run = base + rd.get(in, ne);
+            if (rd.pos > in.nbits) CFAIL(R_UEOS);
+            if (empty_dist) CFAIL(R_EMPTY_DIST);
+            const uint32_t dsym = dist_sym(fixed, rd, in, t, gs, fx);
+            if (rd.pos > in.nbits) CFAIL(R_UEOS);
+            if (dsym > 29) CFAIL(R_RESERVED_DIST);
+            dist_base(dsym, base, ne);
+            const uint32_t dist = base + rd.get(in, ne);
+            if (rd.pos > in.nbits) CFAIL(R_UEOS);
+            // the dictionary bound needs the absolute position: decidable here only at stream start
+            if (abs0 && (uint64_t)dist > n) CFAIL(R_COPY_BEFORE);
+            n += run;
+        }
+        if (bf) { status = ST_FINAL; break; }
+    }
+out:
+#undef CFAIL
+    res.end_bit = rd.pos;
+    res.out_count = n;
+    res.status = status;
+    res.reason = reason;
+}
+
+// Emit pass: per-lane state machine with a token budget per step, so a lane waiting on an earlier
+// chain never blocks its wave.  Output bytes are write-combined into aligned 32-bit stores.
 struct Lane {
-    Rd rd;
-    uint64_t n;           // bytes produced by this chain so far
-    uint64_t stop_bit;    // count: stop at first boundary >= stop_bit; emit: stop at boundary == stop_bit
-    uint32_t state;       // 0 header, 1 stored, 2 huffman, 3 done
+    Rp rd;
+    uint64_t n;                 // bytes produced by this chain so far
+    uint64_t stop_bit;          // stop at the block boundary == stop_bit
+    uint32_t state;             // 0 header, 1 stored, 2 huffman, 3 done
     uint32_t stored_left;
-    bool last;            // current block is final
-    bool fixed;
-    bool empty_dist;
+    bool last, fixed, empty_dist;
     uint32_t status, reason;
-    // pending copy (emit)
-    uint32_t cp_len, cp_dist;
-    uint32_t lastb;       // last output byte (for dist-1 copies without a load)
+    uint32_t cp_len, cp_dist;   // copy waiting for its source
+    uint32_t lastb;             // last output byte (dist-1 copies need no load)
+    uint32_t wc, wcn;           // write-combining word and its byte count
 };
+
+__device__ __forceinline__ void putb(Lane& L, uint8_t* out, uint64_t P, uint32_t b) {
+    if (L.wcn == 0 && (P & 3)) { out[P] = (uint8_t)b; return; }
+    L.wc |= b << (8 * (uint32_t)(P & 3));
+    L.wcn++;
+    if ((P & 3) == 3) { *(uint32_t*)(out + P - 3) = L.wc; L.wc = 0; L.wcn = 0; }
+}
+__device__ __forceinline__ void flushb(Lane& L, uint8_t* out, uint64_t Pnext) {
+    for (uint32_t k = 0; k < L.wcn; k++) out[Pnext - L.wcn + k] = (uint8_t)(L.wc >> (8 * k));
+    L.wc = 0; L.wcn = 0;
+}
+
+// Copy `len` bytes from src to dst (= out_off + L.n), reference byte-serial semantics.
+__device__ __forceinline__ void do_copy(Lane& L, uint8_t* out, uint64_t dst, uint64_t src, uint32_t len, uint32_t dist,
+                                        uint64_t out_off) {
+    if (dist == 1) {
+        const uint32_t v = (L.n > 0) ? L.lastb : (uint32_t)out[src];
+        uint32_t k = 0;
+        for (; k < len && (L.wcn > 0 || ((dst + k) & 3)); k++) putb(L, out, dst + k, v);
+        const uint32_t v4 = v * 0x01010101u;
+        for (; k + 4 <= len; k += 4) *(uint32_t*)(out + dst + k) = v4;
+        for (; k < len; k++) putb(L, out, dst + k, v);
+        L.lastb = v;
+        return;
+    }
+    uint32_t b = L.lastb;
+    if (dist < 4) {
+        // sources may lie in the pending word: no write-combining for short periods
+        flushb(L, out, dst);
+        for (uint32_t k = 0; k < len; k++) { b = out[src + k]; out[dst + k] = (uint8_t)b; }
+    } else {
+        // every source byte lies at least 4 bytes back, i.e. before the pending word
+        for (uint32_t k = 0; k < len; k++) { b = out[src + k]; putb(L, out, dst + k, b); }
+    }
+    L.lastb = b;
+}
 
 }  // namespace inf
 
-
-// Common per-token step.  Returns false when the lane finished (status set).
-template <int MODE>
-__device__ __forceinline__ bool lane_step(inf::Lane& L, const inf::In& in, inf::LaneTabs* mytabs,
-                                          const inf::LaneTabs* fixedTabs, uint8_t* out, uint64_t out_off,
-                                          const uint64_t* chain_off, const uint32_t* done, uint32_t nchains,
-                                          uint32_t my_chain, bool& waiting) {
+template <bool DUMMY = true>
+__device__ bool emit_step(inf::Lane& L, const inf::In& in, inf::LT t, uint16_t* gs, const inf::FixedTabs* fx,
+                          uint8_t* out, uint64_t out_off, const uint64_t* chain_off, const uint32_t* done,
+                          uint32_t my_chain, bool& waiting) {
     using namespace inf;
     waiting = false;
+#define FAIL(r) do { flushb(L, out, out_off + L.n); L.status = ST_ERROR; L.reason = (r); L.state = 3; return false; } while (0)
     if (L.state == 0) {
-        // block boundary
-        if (MODE == 0) {
-            if (L.rd.pos >= L.stop_bit && L.n >= 0) { L.status = ST_BOUNDARY; L.state = 3; return false; }
-        } else {
-            if (L.rd.pos == L.stop_bit) { L.status = ST_BOUNDARY; L.state = 3; return false; }
-        }
-        uint32_t bf = L.rd.get(in, 1), bt = L.rd.get(in, 2);
-        if (L.rd.pos > in.nbits) { L.status = ST_ERROR; L.reason = R_UEOS; L.state = 3; return false; }
+        if (L.rd.pos == L.stop_bit) { flushb(L, out, out_off + L.n); L.status = ST_BOUNDARY; L.state = 3; return false; }
+        const uint32_t bf = L.rd.get(in, 1), bt = L.rd.get(in, 2);
+        if (L.rd.pos > in.nbits) FAIL(R_UEOS);
         L.last = bf != 0;
-        if (bt == 3) { L.status = ST_ERROR; L.reason = R_RESERVED_BLOCK_TYPE; L.state = 3; return false; }
+        if (bt == 3) FAIL(R_RESERVED_BLOCK_TYPE);
         if (bt == 0) {
-            uint32_t pad = (uint32_t)((8 - (L.rd.pos & 7)) & 7);
+            const uint32_t pad = (uint32_t)((8 - (L.rd.pos & 7)) & 7);
             L.rd.get(in, pad);
-            uint32_t ln = L.rd.get(in, 16);
-            uint32_t nln = L.rd.get(in, 16);
-            if (L.rd.pos > in.nbits) { L.status = ST_ERROR; L.reason = R_UEOS; L.state = 3; return false; }
-            if (ln != (nln ^ 0xFFFFu)) { L.status = ST_ERROR; L.reason = R_LEN_MISMATCH; L.state = 3; return false; }
+            const uint32_t ln = L.rd.get(in, 16), nln = L.rd.get(in, 16);
+            if (L.rd.pos > in.nbits) FAIL(R_UEOS);
+            if (ln != (nln ^ 0xFFFFu)) FAIL(R_LEN_MISMATCH);
             L.stored_left = ln;
             L.state = 1;
             return true;
         }
         if (bt == 1) { L.fixed = true; L.empty_dist = false; L.state = 2; return true; }
         bool ed = false;
-        int e = read_dynamic_header(L.rd, in, mytabs, ed);
-        if (e) { L.status = ST_ERROR; L.reason = (uint32_t)e; L.state = 3; return false; }
+        const int e = parse_dynamic(L.rd, in, t, gs, ed);
+        if (e) FAIL((uint32_t)e);
         L.fixed = false; L.empty_dist = ed; L.state = 2;
         return true;
     }
     if (L.state == 1) {
-        // stored bytes: the stream is byte aligned here
-        uint64_t avail = (in.nbits - min(L.rd.pos, in.nbits)) / 8;
-        const uint32_t lim = MODE == 1 ? 32u : 0xFFFFu;
-        uint32_t take = (uint32_t)min((uint64_t)min(L.stored_left, lim), avail);
-        if (MODE == 1) {
-            for (uint32_t k = 0; k < take; k++) {
-                uint32_t b = L.rd.get(in, 8);
-                out[out_off + L.n + k] = (uint8_t)b;
-                L.lastb = b;
-            }
-        } else {
-            // skip whole bytes quickly
-            uint64_t np = L.rd.pos + 8ull * take;
-            L.rd.init(in, np);
+        const uint64_t avail = (in.nbits - min(L.rd.pos, in.nbits)) / 8;
+        const uint32_t want = min(L.stored_left, 64u);
+        const uint32_t take = (uint32_t)min((uint64_t)want, avail);
+        for (uint32_t k = 0; k < take; k++) {
+            const uint32_t b = L.rd.get(in, 8);
+            putb(L, out, out_off + L.n + k, b);
+            L.lastb = b;
         }
         L.n += take;
         L.stored_left -= take;
-        if (take < min(L.stored_left + take, lim)) { L.status = ST_ERROR; L.reason = R_UEOS; L.state = 3; return false; }
+        if (take < want) FAIL(R_UEOS);
         if (L.stored_left == 0) {
-            if (L.last) { L.status = ST_FINAL; L.state = 3; return false; }
+            if (L.last) { flushb(L, out, out_off + L.n); L.status = ST_FINAL; L.state = 3; return false; }
             L.state = 0;
         }
         return true;
     }
-    // state 2: one Huffman token
-    if (MODE == 1 && L.cp_len) {
-        // a copy that was waiting for its source
-        goto do_copy;
-    }
-    {
-        const Tab* lt = L.fixed ? &fixedTabs->lit : &mytabs->lit;
-        uint32_t sym = decode_sym(lt, L.rd, in);
-        if (L.rd.pos > in.nbits) { L.status = ST_ERROR; L.reason = R_UEOS; L.state = 3; return false; }
-        if (sym < 256) {
-            if (MODE == 1) out[out_off + L.n] = (uint8_t)sym;
-            L.lastb = sym;
-            L.n++;
-            return true;
+    // state 2: up to 32 tokens per step
+    for (int budget = 0; budget < 32; budget++) {
+        if (L.cp_len == 0) {
+            const uint32_t sym = lit_sym(L.fixed, L.rd, in, t, gs, fx);
+            if (L.rd.pos > in.nbits) FAIL(R_UEOS);
+            if (sym < 256) {
+                putb(L, out, out_off + L.n, sym);
+                L.lastb = sym;
+                L.n++;
+                continue;
+            }
+            if (sym == 256) {
+                if (L.last) { flushb(L, out, out_off + L.n); L.status = ST_FINAL; L.state = 3; return false; }
+                L.state = 0;
+                return true;
+            }
+            if (sym > 285) FAIL(R_RESERVED_LEN);
+            uint32_t base, ne;
+            run_base(sym - 257, base, ne);
+            const uint32_t run = base + L.rd.get(in, ne);
+            if (L.rd.pos > in.nbits) FAIL(R_UEOS);
+            if (L.empty_dist) FAIL(R_EMPTY_DIST);
+            const uint32_t dsym = dist_sym(L.fixed, L.rd, in, t, gs, fx);
+            if (L.rd.pos > in.nbits) FAIL(R_UEOS);
+            if (dsym > 29) FAIL(R_RESERVED_DIST);
+            dist_base(dsym, base, ne);
+            const uint32_t dist = base + L.rd.get(in, ne);
+            if (L.rd.pos > in.nbits) FAIL(R_UEOS);
+            if ((uint64_t)dist > out_off + L.n) FAIL(R_COPY_BEFORE);
+            L.cp_len = run;
+            L.cp_dist = dist;
         }
-        if (sym == 256) {
-            if (L.last) { L.status = ST_FINAL; L.state = 3; return false; }
-            L.state = 0;
-            return true;
-        }
-        if (sym > 285) { L.status = ST_ERROR; L.reason = R_RESERVED_LEN; L.state = 3; return false; }
-        uint32_t run = RUN_BASE[sym - 257] + L.rd.get(in, RUN_EXTRA[sym - 257]);
-        if (L.rd.pos > in.nbits) { L.status = ST_ERROR; L.reason = R_UEOS; L.state = 3; return false; }
-        if (L.empty_dist) { L.status = ST_ERROR; L.reason = R_EMPTY_DIST; L.state = 3; return false; }
-        const Tab* dt = L.fixed ? &fixedTabs->dist : &mytabs->dist;
-        uint32_t dsym = decode_sym(dt, L.rd, in);
-        if (L.rd.pos > in.nbits) { L.status = ST_ERROR; L.reason = R_UEOS; L.state = 3; return false; }
-        if (dsym > 29) { L.status = ST_ERROR; L.reason = R_RESERVED_DIST; L.state = 3; return false; }
-        uint32_t dist = DIST_BASE[dsym] + L.rd.get(in, DIST_EXTRA[dsym]);
-        if (L.rd.pos > in.nbits) { L.status = ST_ERROR; L.reason = R_UEOS; L.state = 3; return false; }
-        if (MODE == 0) {
-            // dictionary check needs the absolute position: only decidable here for chain offset 0
-            if (out_off == 0 && (uint64_t)dist > L.n) { L.status = ST_ERROR; L.reason = R_COPY_BEFORE; L.state = 3; return false; }
-            L.n += run;
-            return true;
-        }
-        if ((uint64_t)dist > out_off + L.n) { L.status = ST_ERROR; L.reason = R_COPY_BEFORE; L.state = 3; return false; }
-        L.cp_len = run;
-        L.cp_dist = dist;
-    }
-do_copy:
-    if (MODE == 1) {
         const uint64_t dst = out_off + L.n;
         const uint64_t src = dst - L.cp_dist;
         if (src < out_off && !(L.cp_dist == 1 && L.n > 0)) {
-            // source precedes this chain: wait for the chains that own bytes [src, min(dst, src+len))
+            // source precedes this chain: wait for the chains owning bytes [src, min(dst, src+len))
             uint32_t lo = 0, hi = my_chain;
-            while (lo + 1 < hi) { uint32_t mid = (lo + hi) >> 1; if (chain_off[mid] <= src) lo = mid; else hi = mid; }
+            while (lo + 1 < hi) { const uint32_t mid = (lo + hi) >> 1; if (chain_off[mid] <= src) lo = mid; else hi = mid; }
             const uint64_t src_end = min(dst, src + L.cp_len);
             uint32_t need_hi = lo;
             while (need_hi + 1 < my_chain && chain_off[need_hi + 1] < src_end) need_hi++;
-            for (uint32_t j = lo; j <= need_hi; j++) {
+            for (uint32_t j = lo; j <= need_hi; j++)
                 if (__hip_atomic_load(&done[j], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == 0) { waiting = true; return true; }
-            }
             __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
         }
-        // bounded work per step (<= 32 bytes) keeps the lanes of a wave in step
-        const uint32_t take = min(L.cp_len, 32u);
-        if (L.cp_dist == 1) {
-            const uint32_t v = (L.n > 0) ? L.lastb : (uint32_t)out[src];
-            for (uint32_t k = 0; k < take; k++) out[dst + k] = (uint8_t)v;
-            L.lastb = v;
-        } else {
-            uint32_t b = L.lastb;
-            for (uint32_t k = 0; k < take; k++) {
-                b = out[src + k];
-                out[dst + k] = (uint8_t)b;
-            }
-            L.lastb = b;
-        }
-        L.n += take;
-        L.cp_len -= take;
+        do_copy(L, out, dst, src, L.cp_len, L.cp_dist, out_off);
+        L.n += L.cp_len;
+        L.cp_len = 0;
     }
     return true;
+#undef FAIL
 }
 
 // One lane per candidate: count output bytes until the first boundary >= stop.
-extern "C" __global__ void __launch_bounds__(256)
+extern "C" __global__ void __launch_bounds__(64)
 ndfl_inflate_count_kernel(const uint32_t* w, uint64_t nwords, uint64_t nbits, const uint64_t* starts,
-                          const uint64_t* stops, uint32_t nchains, ChainRes* res, inf::LaneTabs* tabs,
-                          const inf::LaneTabs* fixedTabs) {
+                          const uint64_t* stops, uint32_t nchains, ChainRes* res, uint16_t* gsort,
+                          const inf::FixedTabs* fx) {
     using namespace inf;
-    const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
+    extern __shared__ uint16_t lds_tab[];
+    const uint32_t i = blockIdx.x * 64 + threadIdx.x;
+    const LT t{lds_tab + threadIdx.x};
+    uint16_t* gs = gsort + (uint64_t)blockIdx.x * G_SORT * 64 + threadIdx.x;
     if (i >= nchains) return;
     In in{w, nwords, nbits};
-    Lane L;
-    L.rd.init(in, starts[i]);
-    L.n = 0; L.stop_bit = stops[i]; L.state = 0; L.stored_left = 0; L.last = false; L.fixed = false;
-    L.empty_dist = false; L.status = 0; L.reason = 0; L.cp_len = 0; L.cp_dist = 0; L.lastb = 0;
-    // starts[i] < stops[i], so the first block is always decoded
-    bool waiting;
-    while (lane_step<0>(L, in, &tabs[i], fixedTabs, nullptr, starts[i] == 0 ? 0 : 1, nullptr, nullptr, 0, 0, waiting)) {}
     ChainRes r;
-    r.end_bit = L.rd.pos;
-    r.out_count = L.n;
-    r.status = L.status;
-    r.reason = L.reason;
+    count_chain(starts[i], stops[i], starts[i] == 0, in, t, gs, fx, r);
     res[i] = r;
 }
 
-// One lane per linked chain, in stream order.  Lanes claim chains through `ticket` in groups of
-// 64 (one wave), so every chain a lane may wait on already belongs to a running wave.
-extern "C" __global__ void __launch_bounds__(256)
+// One lane per linked chain, in stream order.  Each wave claims its 64 chains through `ticket`,
+// so every chain a lane may wait on already belongs to a running wave.
+extern "C" __global__ void __launch_bounds__(64)
 ndfl_inflate_emit_kernel(const uint32_t* w, uint64_t nwords, uint64_t nbits, const EmitChain* chains,
                          const uint64_t* chain_off, uint32_t nchains, uint32_t* done, uint32_t* ticket,
-                         uint8_t* out, ChainRes* res, inf::LaneTabs* tabs, const inf::LaneTabs* fixedTabs) {
+                         uint8_t* out, ChainRes* res, uint16_t* gsort, const inf::FixedTabs* fx) {
     using namespace inf;
+    extern __shared__ uint16_t lds_tab[];
     const int lane = threadIdx.x & 63;
+    const LT t{lds_tab + lane};
+    uint16_t* gs = gsort + (uint64_t)blockIdx.x * G_SORT * 64 + lane;
     uint32_t base = 0;
     if (lane == 0) base = atomicAdd(ticket, 64u);
     base = __shfl(base, 0, 64);
@@ -600,13 +919,14 @@ ndfl_inflate_emit_kernel(const uint32_t* w, uint64_t nwords, uint64_t nbits, con
     L.rd.init(in, ch.start_bit);
     L.n = 0; L.stop_bit = ch.end_bit; L.state = 0; L.stored_left = 0; L.last = false; L.fixed = false;
     L.empty_dist = false; L.status = 0; L.reason = 0; L.cp_len = 0; L.cp_dist = 0; L.lastb = 0;
+    L.wc = 0; L.wcn = 0;
     bool active = valid;
     int idle = 0;
     uint32_t waits = 0;
     while (__any(active)) {
         bool waiting = false;
         if (active) {
-            bool more = lane_step<1>(L, in, &tabs[i], fixedTabs, out, ch.out_off, chain_off, done, nchains, i, waiting);
+            bool more = emit_step(L, in, t, gs, fx, out, ch.out_off, chain_off, done, i, waiting);
             if (waiting && ++waits > (1u << 26)) {          // safety net: never hang the device
                 more = false; L.status = ST_ERROR; L.reason = R_INTERNAL;
             }
@@ -620,7 +940,6 @@ ndfl_inflate_emit_kernel(const uint32_t* w, uint64_t nwords, uint64_t nbits, con
                 res[i] = r;
             }
         }
-        // back off only when every active lane is waiting
         if (__all(!active || waiting)) { if (++idle > 2) __builtin_amdgcn_s_sleep(2); }
         else idle = 0;
     }
@@ -665,36 +984,32 @@ static hipError_t inf_ensure(void** p, size_t* cap, size_t n) {
 }
 
 // Host-side construction of the fixed-Huffman decode tables (D/decomp/Open.java:812-830).
-static void host_build_fixed(inf::LaneTabs* t) {
+static void host_build_fixed(inf::FixedTabs* t) {
     memset(t, 0, sizeof(*t));
-    auto build = [](const uint8_t* lens, int n, inf::Tab* tab) {
+    auto build = [](const uint8_t* lens, int n, uint16_t* prim, int pbits) {
         uint16_t cnt[16] = {0};
         for (int s = 0; s < n; s++) cnt[lens[s]]++;
         cnt[0] = 0;
-        uint16_t first[16] = {0}, offs[16] = {0};
-        uint32_t code = 0, off = 0;
-        for (int l = 1; l < 16; l++) {
-            code = (code + (l > 1 ? cnt[l - 1] : 0)) << 1;
-            first[l] = (uint16_t)code; offs[l] = (uint16_t)off; off += cnt[l];
-            tab->first[l] = first[l]; tab->count[l] = cnt[l]; tab->offs[l] = offs[l];
-        }
+        uint16_t first[16] = {0};
+        uint32_t code = 0;
+        for (int l = 1; l < 16; l++) { code = (code + (l > 1 ? cnt[l - 1] : 0)) << 1; first[l] = (uint16_t)code; }
         uint16_t nxt[16] = {0};
         for (int s = 0; s < n; s++) {
             uint32_t l = lens[s];
             if (!l) continue;
-            uint32_t rank = nxt[l]++;
-            tab->sorted[offs[l] + rank] = (uint16_t)s;
-            uint32_t c = first[l] + rank, r = 0;
+            uint32_t c = first[l] + nxt[l]++, r = 0;
             for (uint32_t b = 0; b < l; b++) r |= ((c >> b) & 1u) << (l - 1 - b);
-            for (uint32_t k = r; k < (1u << inf::PRIM); k += (1u << l)) tab->prim[k] = (uint16_t)(s | (l << 9));
+            for (uint32_t k = r; k < (1u << pbits); k += (1u << l)) prim[k] = (uint16_t)(s | (l << 9));
         }
     };
     uint8_t ll[288], dl[32];
     for (int i = 0; i < 288; i++) ll[i] = i < 144 ? 8 : i < 256 ? 9 : i < 280 ? 7 : 8;
     for (int i = 0; i < 32; i++) dl[i] = 5;
-    build(ll, 288, &t->lit);
-    build(dl, 32, &t->dist);
+    build(ll, 288, t->lit, 9);
+    build(dl, 32, t->dist, 5);
 }
+
+static constexpr uint32_t LDS_TAB_BYTES = inf::LDS_BYTES;
 
 #define INF_CHK(x) do { hipError_t _e = (x); if (_e != hipSuccess) return -4; } while (0)
 
@@ -718,10 +1033,14 @@ static int inflate_run(InflateScratch& S, hipStream_t s, const uint8_t* in, uint
         d_w = (const uint32_t*)S.d_in;
     }
     if (!S.d_fixed) {
-        INF_CHK(hipMalloc(&S.d_fixed, sizeof(LaneTabs)));
-        LaneTabs* h = (LaneTabs*)malloc(sizeof(LaneTabs));
+        INF_CHK(hipFuncSetAttribute((const void*)ndfl_inflate_count_kernel, hipFuncAttributeMaxDynamicSharedMemorySize,
+                                    (int)LDS_TAB_BYTES));
+        INF_CHK(hipFuncSetAttribute((const void*)ndfl_inflate_emit_kernel, hipFuncAttributeMaxDynamicSharedMemorySize,
+                                    (int)LDS_TAB_BYTES));
+        INF_CHK(hipMalloc(&S.d_fixed, sizeof(FixedTabs)));
+        FixedTabs* h = (FixedTabs*)malloc(sizeof(FixedTabs));
         host_build_fixed(h);
-        INF_CHK(hipMemcpy(S.d_fixed, h, sizeof(LaneTabs), hipMemcpyHostToDevice));
+        INF_CHK(hipMemcpy(S.d_fixed, h, sizeof(FixedTabs), hipMemcpyHostToDevice));
         free(h);
     }
     if (!S.ev[0]) for (auto& e : S.ev) INF_CHK(hipEventCreate(&e));
@@ -733,6 +1052,7 @@ static int inflate_run(InflateScratch& S, hipStream_t s, const uint8_t* in, uint
     INF_CHK(hipEventRecord(S.ev[0], s));
     {
         const uint64_t nthr = (nbits + 31) / 32;
+        INF_CHK(inf_ensure(&S.d_starts, &S.d_starts_cap, 64));
         if (nthr)
             hipLaunchKernelGGL(ndfl_inflate_find_kernel, dim3((uint32_t)((nthr + 255) / 256)), dim3(256), 0, s, d_w,
                                nwords, nbits, d_cnt, d_list);
@@ -740,22 +1060,25 @@ static int inflate_run(InflateScratch& S, hipStream_t s, const uint8_t* in, uint
     }
     INF_CHK(hipEventRecord(S.ev[1], s));
     std::vector<uint32_t> hcnt(nseg);
-    std::vector<uint64_t> hlist((uint64_t)nseg * SEG_CAP);
     INF_CHK(hipMemcpyAsync(hcnt.data(), d_cnt, nseg * 4ull, hipMemcpyDeviceToHost, s));
-    INF_CHK(hipMemcpyAsync(hlist.data(), d_list, (uint64_t)nseg * SEG_CAP * 8ull, hipMemcpyDeviceToHost, s));
     INF_CHK(hipStreamSynchronize(s));
-    std::vector<uint64_t> starts;
-    starts.reserve((size_t)nseg * 4);
-    starts.push_back(0);
-    for (uint32_t k = 0; k < nseg; k++) {
-        const uint32_t c = std::min(hcnt[k], SEG_CAP);
-        const size_t b0 = starts.size();
-        for (uint32_t j = 0; j < c; j++) {
-            const uint64_t v = hlist[(uint64_t)k * SEG_CAP + j];
-            if (v != NONE && v != 0) starts.push_back(v);
-        }
-        std::sort(starts.begin() + b0, starts.end());
-    }
+    std::vector<uint64_t> hoff(nseg + 1);
+    hoff[0] = 1;                                   // slot 0 is the stream start (bit 0)
+    for (uint32_t k = 0; k < nseg; k++) hoff[k + 1] = hoff[k] + std::min(hcnt[k], SEG_CAP);
+    const uint64_t ncand_all = hoff[nseg];
+    INF_CHK(inf_ensure(&S.d_starts, &S.d_starts_cap, (ncand_all + nseg + 2) * 8));
+    uint64_t* d_sorted = (uint64_t*)S.d_starts;
+    uint64_t* d_segoff = d_sorted + ncand_all;
+    INF_CHK(hipMemcpyAsync(d_segoff, hoff.data(), nseg * 8ull, hipMemcpyHostToDevice, s));
+    INF_CHK(hipMemsetAsync(d_sorted, 0, 8, s));
+    hipLaunchKernelGGL(ndfl_inflate_compact_kernel, dim3((nseg + 255) / 256), dim3(256), 0, s, (const uint32_t*)d_cnt,
+                       (const uint64_t*)d_list, (const uint64_t*)d_segoff, nseg, d_sorted);
+    INF_CHK(hipGetLastError());
+    std::vector<uint64_t> starts(ncand_all);
+    INF_CHK(hipMemcpyAsync(starts.data(), d_sorted, ncand_all * 8, hipMemcpyDeviceToHost, s));
+    INF_CHK(hipStreamSynchronize(s));
+    // drop a duplicate bit-0 entry (a header at bit 0 found by the finder)
+    starts.erase(std::unique(starts.begin(), starts.end()), starts.end());
     const std::vector<uint64_t> sorted_cand(starts);
 
     auto next_after = [&](uint64_t b) -> uint64_t {
@@ -770,13 +1093,13 @@ static int inflate_run(InflateScratch& S, hipStream_t s, const uint8_t* in, uint
         INF_CHK(inf_ensure(&S.d_starts, &S.d_starts_cap, n * 8));
         INF_CHK(inf_ensure(&S.d_stops, &S.d_stops_cap, n * 8));
         INF_CHK(inf_ensure(&S.d_res, &S.d_res_cap, n * sizeof(ChainRes)));
-        INF_CHK(inf_ensure(&S.d_tabs, &S.d_tabs_cap, n * sizeof(LaneTabs)));
+        INF_CHK(inf_ensure(&S.d_tabs, &S.d_tabs_cap, ((n + 63) / 64) * (uint64_t)G_SORT * 64 * 2));
         INF_CHK(hipMemcpyAsync(S.d_starts, st.data(), n * 8, hipMemcpyHostToDevice, s));
         INF_CHK(hipMemcpyAsync(S.d_stops, sp.data(), n * 8, hipMemcpyHostToDevice, s));
         if (S.count_first) INF_CHK(hipEventRecord(S.ev[2], s));
-        hipLaunchKernelGGL(ndfl_inflate_count_kernel, dim3((uint32_t)((n + 255) / 256)), dim3(256), 0, s, d_w, nwords,
-                           nbits, (const uint64_t*)S.d_starts, (const uint64_t*)S.d_stops, (uint32_t)n,
-                           (ChainRes*)S.d_res, (LaneTabs*)S.d_tabs, (const LaneTabs*)S.d_fixed);
+        hipLaunchKernelGGL(ndfl_inflate_count_kernel, dim3((uint32_t)((n + 63) / 64)), dim3(64), LDS_TAB_BYTES, s, d_w,
+                           nwords, nbits, (const uint64_t*)S.d_starts, (const uint64_t*)S.d_stops, (uint32_t)n,
+                           (ChainRes*)S.d_res, (uint16_t*)S.d_tabs, (const FixedTabs*)S.d_fixed);
         INF_CHK(hipGetLastError());
         if (S.count_first) { INF_CHK(hipEventRecord(S.ev[3], s)); S.count_first = false; }
         r.resize(n);
@@ -860,7 +1183,7 @@ static int inflate_run(InflateScratch& S, hipStream_t s, const uint8_t* in, uint
     INF_CHK(inf_ensure(&S.d_off, &S.d_off_cap, (nch + 1) * 8ull));
     INF_CHK(inf_ensure(&S.d_done, &S.d_done_cap, nch * 4ull));
     INF_CHK(inf_ensure(&S.d_res, &S.d_res_cap, nch * sizeof(ChainRes)));
-    INF_CHK(inf_ensure(&S.d_tabs, &S.d_tabs_cap, nch * sizeof(LaneTabs)));
+    INF_CHK(inf_ensure(&S.d_tabs, &S.d_tabs_cap, ((nch + 63) / 64) * (uint64_t)G_SORT * 64 * 2));
     if (!S.d_ticket) INF_CHK(hipMalloc(&S.d_ticket, 64));
     INF_CHK(hipMemcpyAsync(S.d_chains, chains.data(), nch * sizeof(EmitChain), hipMemcpyHostToDevice, s));
     offs.push_back(total);
@@ -874,10 +1197,10 @@ static int inflate_run(InflateScratch& S, hipStream_t s, const uint8_t* in, uint
     hipEvent_t e2 = S.ev[4], e3 = S.ev[5];
     INF_CHK(hipEventRecord(e2, s));
     const uint32_t waves = (nch + 63) / 64;
-    hipLaunchKernelGGL(ndfl_inflate_emit_kernel, dim3((waves + 3) / 4), dim3(256), 0, s, d_w, nwords, nbits,
+    hipLaunchKernelGGL(ndfl_inflate_emit_kernel, dim3(waves), dim3(64), LDS_TAB_BYTES, s, d_w, nwords, nbits,
                        (const EmitChain*)S.d_chains, (const uint64_t*)S.d_off, nch, (uint32_t*)S.d_done,
-                       (uint32_t*)S.d_ticket, d_out, (ChainRes*)S.d_res, (LaneTabs*)S.d_tabs,
-                       (const LaneTabs*)S.d_fixed);
+                       (uint32_t*)S.d_ticket, d_out, (ChainRes*)S.d_res, (uint16_t*)S.d_tabs,
+                       (const FixedTabs*)S.d_fixed);
     INF_CHK(hipGetLastError());
     INF_CHK(hipEventRecord(e3, s));
     std::vector<ChainRes> er(nch);
