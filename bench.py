@@ -38,6 +38,7 @@ def main():
     ap.add_argument("--cpu-sample", type=int, default=256 << 20, help="bytes for the CPU baseline leg")
     ap.add_argument("--no-cpu", action="store_true")
     ap.add_argument("--no-verify", action="store_true")
+    ap.add_argument("--backend", default="nccl", help="nccl (= RCCL over xGMI); gloo only to rehearse N>1 on one GPU")
     args = ap.parse_args()
 
     import torch
@@ -47,11 +48,15 @@ def main():
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
+    local = local % max(1, torch.cuda.device_count())
     torch.cuda.set_device(local)
     dist = None
     if world > 1:
         import torch.distributed as dist
-        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+        if args.backend == "nccl":
+            dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+        else:
+            dist.init_process_group(args.backend)
 
     n = args.size
     data = corpus.c4_mixed(n, seed=0xC4 + rank, device="cuda")
@@ -60,33 +65,36 @@ def main():
     L = ndfl._lib.load()
     cap = L.ndfl_deflate_bound(n, 65536) + 64
     comp = torch.empty(cap, dtype=torch.uint8, device="cuda")
-    dec = torch.empty(n + (32 << 10) + 64, dtype=torch.uint8, device="cuda")
     RLE_DYNAMIC = 3
     DEV = ndfl.IN_DEVICE | ndfl.OUT_DEVICE
-
-    prev_byte = None
+    state = {"dict_len": 0}
     if world > 1:
-        # the byte preceding this rank's shard (RLE history) -- exchanged once, it is input
-        lasts = torch.empty(world, dtype=torch.uint8, device="cuda")
-        dist.all_gather_into_tensor(lasts, data[-1:].contiguous())
-        if rank > 0:
-            prev_byte = lasts[rank - 1:rank].clone()
-
-    state = {}
+        from ndfl import parallel as P
+        codec = P.DeviceCodec(ctx, torch)
+        shifted = torch.empty(cap + 1, dtype=torch.uint8, device="cuda")
+        dec = torch.empty(P.WINDOW + n + 64, dtype=torch.uint8, device="cuda")
+    else:
+        dec = torch.empty(n + 64, dtype=torch.uint8, device="cuda")
 
     def step():
-        hist_addr = prev_byte.data_ptr() if prev_byte is not None else None
-        endbits, _ = ctx.deflate_chunks_raw(hist_addr, 1 if prev_byte is not None else 0, 32768, data.data_ptr(), n,
-                                            65536, RLE_DYNAMIC, rank == world - 1, 0, comp.data_ptr(), cap, DEV)
-        t_c = ctx.timings()["deflate"]
-        cbytes = (endbits + 7) // 8
         if world == 1:
+            endbits, _ = ctx.deflate_chunks_raw(None, 0, 32768, data.data_ptr(), n, 65536, RLE_DYNAMIC, True, 0,
+                                                comp.data_ptr(), cap, DEV)
+            t_c = ctx.timings()["deflate"]
+            cbytes = (endbits + 7) // 8
             r, olen, bits = ctx.inflate_raw(comp.data_ptr(), cbytes, dec.data_ptr(), dec.numel(), DEV)
             ndfl.check(r, "inflate")
-            if r != 0:
-                raise RuntimeError(f"decode error {r}")
         else:
-            r, olen, bits = distributed_roundtrip_decode(ctx, dist, torch, comp, endbits, dec, rank, world)
+            # one global stream: history halo + seam index + realignment, then range decode with the
+            # window chain (ndfl/parallel.py)
+            part = P.deflate_shard(codec, dist, torch, data, rank, world, work=comp, out=shifted)
+            t_c = ctx.timings()["deflate"]
+            endbits = part.nbits
+            cbytes = (endbits + 7) // 8
+            r, olen, dl = P.inflate_shard(codec, dist, torch, part, dec, rank, world)
+            state["dict_len"] = dl
+        if r != 0:
+            raise RuntimeError(f"decode error {r}")
         tm = ctx.timings()
         state.update(endbits=endbits, cbytes=cbytes, olen=olen, t_deflate=t_c, t_emit=tm["inflate_emit"],
                      t_find=tm["inflate_find"], t_count=tm["inflate_count"], t_inflate_span=tm["inflate_span"],
@@ -97,7 +105,8 @@ def main():
         step()
     if not args.no_verify:
         assert state["olen"] == n, (state["olen"], n)
-        assert torch.equal(dec[:n], data), "round trip mismatch"
+        dl = state["dict_len"]
+        assert torch.equal(dec[dl:dl + n], data), "round trip mismatch"
 
     def barrier():
         if dist is not None:
@@ -113,10 +122,11 @@ def main():
     per = (t1 - t0) / args.steps
     c_total = state["cbytes"]
     if dist is not None:
-        t = torch.tensor([per], dtype=torch.float64, device="cuda")
+        cdev = "cpu" if args.backend == "gloo" else "cuda"
+        t = torch.tensor([per], dtype=torch.float64, device=cdev)
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         per = float(t.item())
-        cb = torch.tensor([state["cbytes"]], dtype=torch.int64, device="cuda")
+        cb = torch.tensor([state["cbytes"]], dtype=torch.int64, device=cdev)
         dist.all_reduce(cb)
         c_total = int(cb.item())
 
@@ -167,10 +177,6 @@ def main():
         print(json.dumps(line), flush=True)
     if dist is not None:
         dist.destroy_process_group()
-
-
-def distributed_roundtrip_decode(ctx, dist, torch, comp, endbits, dec, rank, world):
-    raise NotImplementedError
 
 
 def cpu_baseline(data_dev, sample_bytes):

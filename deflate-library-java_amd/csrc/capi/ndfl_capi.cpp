@@ -297,8 +297,44 @@ int ndfl_inflate(ndfl_ctx* c, const uint8_t* in, uint64_t in_len, uint8_t* out, 
                  uint64_t* out_len, uint64_t* consumed_bits, uint32_t flags) {
     if (!c || !out_len || !consumed_bits || (!in && in_len)) return NDFL_E_ARG;
     HIPCHK(hipSetDevice(c->device));
-    return inflate_run(c->inf, c->stream, in, in_len, out, out_cap, out_len, consumed_bits, flags,
-                       c->ev0, c->ev1, &c->last_ms);
+    return inflate_run(c->inf, c->stream, in, in_len, 0, inf::NONE, out, 0, out_cap, out_len, consumed_bits,
+                       flags, false, &c->last_ms);
+}
+
+int ndfl_inflate_range(ndfl_ctx* c, const uint8_t* in, uint64_t in_len, uint64_t start_bit, uint64_t end_bit,
+                       uint8_t* out, uint64_t dict_len, uint64_t out_cap, uint64_t* out_len, uint64_t* consumed_bits,
+                       uint32_t flags) {
+    if (!c || !out_len || !consumed_bits || (!in && in_len) || (!out && (dict_len || out_cap))) return NDFL_E_ARG;
+    if (dict_len > 32768 || start_bit > in_len * 8 || end_bit <= start_bit) return NDFL_E_ARG;
+    const bool deferred = (flags & NDFL_DICT_DEFERRED) != 0;
+    if (deferred && !(flags & NDFL_OUT_DEVICE)) return NDFL_E_ARG;
+    HIPCHK(hipSetDevice(c->device));
+    return inflate_run(c->inf, c->stream, in, in_len, start_bit, end_bit, out, dict_len, out_cap, out_len,
+                       consumed_bits, flags, deferred, &c->last_ms);
+}
+
+int ndfl_inflate_resolve(ndfl_ctx* c, uint64_t* n_reemitted) {
+    if (!c || !n_reemitted) return NDFL_E_ARG;
+    HIPCHK(hipSetDevice(c->device));
+    return inflate_resolve(c->inf, c->stream, n_reemitted);
+}
+
+int ndfl_bits_shift(ndfl_ctx* c, const uint8_t* in, uint64_t nbits, uint32_t shift, uint8_t* out, uint64_t out_cap,
+                    uint32_t flags) {
+    if (!c || (!in && nbits) || !out || shift > 7) return NDFL_E_ARG;
+    if ((flags & (NDFL_IN_DEVICE | NDFL_OUT_DEVICE)) != (NDFL_IN_DEVICE | NDFL_OUT_DEVICE)) return NDFL_E_ARG;
+    const uint64_t nout = (nbits + shift + 7) / 8;
+    if (nout > out_cap) return NDFL_E_CAPACITY;
+    const uint64_t nin = (nbits + 7) / 8;
+    if (nout && in < out + nout && out < in + nin) return NDFL_E_ARG;     // no in-place shifting
+    if (nout == 0) return NDFL_OK;
+    HIPCHK(hipSetDevice(c->device));
+    const uint64_t nthr = (nout + 3) / 4;
+    hipLaunchKernelGGL(ndfl_bits_shift_kernel, dim3((uint32_t)((nthr + 255) / 256)), dim3(256), 0, c->stream, in,
+                       nbits, shift, out, nout);
+    HIPCHK(hipGetLastError());
+    HIPCHK(hipStreamSynchronize(c->stream));
+    return NDFL_OK;
 }
 
 }  // extern "C"

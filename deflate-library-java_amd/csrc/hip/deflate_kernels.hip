@@ -736,3 +736,39 @@ ndfl_crc_segments_kernel(const uint8_t* in, uint64_t n, const uint32_t* crc_tab,
         seg_raw[seg] = x;
     }
 }
+
+// Multi-GPU seam step: a shard's bit stream, compressed at bit 0, is moved to bit `shift` (0..7)
+// of its first byte, i.e. to its global bit offset mod 8.  One output word per
+// thread from input words t-1 and t; bits past `nbits` are cleared.
+__device__ __forceinline__ uint32_t seam_word(const uint8_t* in, uint64_t nin, bool aligned, int64_t t) {
+    if (t < 0) return 0u;
+    const uint64_t b = (uint64_t)t * 4;
+    if (aligned && b + 4 <= nin) return *(const uint32_t*)(in + b);
+    uint32_t v = 0;
+    for (uint32_t k = 0; k < 4; k++)
+        if (b + k < nin) v |= (uint32_t)in[b + k] << (8 * k);
+    return v;
+}
+
+extern "C" __global__ void __launch_bounds__(256)
+ndfl_bits_shift_kernel(const uint8_t* in, uint64_t nbits, uint32_t shift, uint8_t* out, uint64_t nout) {
+    const uint64_t t = (uint64_t)blockIdx.x * 256 + threadIdx.x;
+    const uint64_t b = t * 4;
+    if (b >= nout) return;
+    const uint64_t nin = (nbits + 7) / 8;
+    const bool aligned = (((uintptr_t)in) & 3) == 0;
+    uint32_t hi = seam_word(in, nin, aligned, (int64_t)t), lo = seam_word(in, nin, aligned, (int64_t)t - 1);
+    // clear bits at or past nbits (in either source word)
+    auto keep = [nbits](uint64_t wbit) -> uint32_t {
+        return wbit + 32 <= nbits ? 0xFFFFFFFFu : nbits > wbit ? (uint32_t)((1ull << (nbits - wbit)) - 1) : 0u;
+    };
+    hi &= keep(t * 32);
+    if (t > 0) lo &= keep(t * 32 - 32);
+    const uint32_t v = shift ? (hi << shift) | (lo >> (32 - shift)) : hi;
+    if (b + 4 <= nout && (((uintptr_t)out) & 3) == 0) {
+        *(uint32_t*)(out + b) = v;
+    } else {
+        for (uint32_t k = 0; k < 4; k++)
+            if (b + k < nout) out[b + k] = (uint8_t)(v >> (8 * k));
+    }
+}

@@ -661,7 +661,7 @@ __device__ __forceinline__ uint32_t dist_sym(bool fixed, Rp& rd, const In& in, L
 
 // Count pass for one chain: straight-line decode, no output.  Stops at the first block boundary at
 // or past `stop`, after a final block, or at the first error (reference check order).
-__device__ void count_chain(uint64_t start, uint64_t stop, bool abs0, const In& in, LT t, uint16_t* gs,
+__device__ void count_chain(uint64_t start, uint64_t stop, uint64_t lim, const In& in, LT t, uint16_t* gs,
                             const FixedTabs* fx, ChainRes& res) {
     Rp rd;
     rd.init(in, start);
@@ -710,8 +710,9 @@ __device__ void count_chain(uint64_t start, uint64_t stop, bool abs0, const In& 
             dist_base(dsym, base, ne);
             const uint32_t dist = base + rd.get(in, ne);
             if (rd.pos > in.nbits) CFAIL(R_UEOS);
-            // the dictionary bound needs the absolute position: decidable here only at stream start
-            if (abs0 && (uint64_t)dist > n) CFAIL(R_COPY_BEFORE);
+            // the dictionary bound needs the absolute position: decidable here only for the chain
+            // at the range start (lim = dictionary bytes before it; others pass lim = 2^62)
+            if ((uint64_t)dist > n + lim) CFAIL(R_COPY_BEFORE);
             n += run;
         }
         if (bf) { status = ST_FINAL; break; }
@@ -780,7 +781,8 @@ __device__ __forceinline__ void do_copy(Lane& L, uint8_t* out, uint64_t dst, uin
 template <bool DUMMY = true>
 __device__ bool emit_step(inf::Lane& L, const inf::In& in, inf::LT t, uint16_t* gs, const inf::FixedTabs* fx,
                           uint8_t* out, uint64_t out_off, const uint64_t* chain_off, const uint32_t* done,
-                          uint32_t my_chain, bool& waiting) {
+                          uint32_t my_chain, bool& waiting, uint64_t dict_len, const uint32_t* taint,
+                          bool& tainted) {
     using namespace inf;
     waiting = false;
 #define FAIL(r) do { flushb(L, out, out_off + L.n); L.status = ST_ERROR; L.reason = (r); L.state = 3; return false; } while (0)
@@ -860,15 +862,23 @@ __device__ bool emit_step(inf::Lane& L, const inf::In& in, inf::LT t, uint16_t* 
         const uint64_t dst = out_off + L.n;
         const uint64_t src = dst - L.cp_dist;
         if (src < out_off && !(L.cp_dist == 1 && L.n > 0)) {
-            // source precedes this chain: wait for the chains owning bytes [src, min(dst, src+len))
-            uint32_t lo = 0, hi = my_chain;
-            while (lo + 1 < hi) { const uint32_t mid = (lo + hi) >> 1; if (chain_off[mid] <= src) lo = mid; else hi = mid; }
+            // source precedes this chain.  Bytes below dict_len are the caller's window (in deferred
+            // mode its content arrives later: the chain is tainted and re-emitted by the resolve
+            // pass); bytes in [dict_len, out_off) wait for the chains owning them.
             const uint64_t src_end = min(dst, src + L.cp_len);
-            uint32_t need_hi = lo;
-            while (need_hi + 1 < my_chain && chain_off[need_hi + 1] < src_end) need_hi++;
-            for (uint32_t j = lo; j <= need_hi; j++)
-                if (__hip_atomic_load(&done[j], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == 0) { waiting = true; return true; }
-            __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+            if (src < dict_len) tainted = true;
+            if (src_end > dict_len) {
+                const uint64_t s0 = max(src, dict_len);
+                uint32_t lo = 0, hi = my_chain;
+                while (lo + 1 < hi) { const uint32_t mid = (lo + hi) >> 1; if (chain_off[mid] <= s0) lo = mid; else hi = mid; }
+                uint32_t need_hi = lo;
+                while (need_hi + 1 < my_chain && chain_off[need_hi + 1] < src_end) need_hi++;
+                for (uint32_t j = lo; j <= need_hi; j++)
+                    if (__hip_atomic_load(&done[j], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == 0) { waiting = true; return true; }
+                __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+                if (taint)
+                    for (uint32_t j = lo; j <= need_hi; j++) tainted |= taint[j] != 0;
+            }
         }
         do_copy(L, out, dst, src, L.cp_len, L.cp_dist, out_off);
         L.n += L.cp_len;
@@ -882,7 +892,7 @@ __device__ bool emit_step(inf::Lane& L, const inf::In& in, inf::LT t, uint16_t* 
 extern "C" __global__ void __launch_bounds__(64)
 ndfl_inflate_count_kernel(const uint32_t* w, uint64_t nwords, uint64_t nbits, const uint64_t* starts,
                           const uint64_t* stops, uint32_t nchains, ChainRes* res, uint16_t* gsort,
-                          const inf::FixedTabs* fx) {
+                          const inf::FixedTabs* fx, uint64_t base_bit, uint64_t dict_len) {
     using namespace inf;
     extern __shared__ uint16_t lds_tab[];
     const uint32_t i = blockIdx.x * 64 + threadIdx.x;
@@ -891,7 +901,7 @@ ndfl_inflate_count_kernel(const uint32_t* w, uint64_t nwords, uint64_t nbits, co
     if (i >= nchains) return;
     In in{w, nwords, nbits};
     ChainRes r;
-    count_chain(starts[i], stops[i], starts[i] == 0, in, t, gs, fx, r);
+    count_chain(starts[i], stops[i], starts[i] == base_bit ? dict_len : (1ull << 62), in, t, gs, fx, r);
     res[i] = r;
 }
 
@@ -899,8 +909,9 @@ ndfl_inflate_count_kernel(const uint32_t* w, uint64_t nwords, uint64_t nbits, co
 // so every chain a lane may wait on already belongs to a running wave.
 extern "C" __global__ void __launch_bounds__(64)
 ndfl_inflate_emit_kernel(const uint32_t* w, uint64_t nwords, uint64_t nbits, const EmitChain* chains,
-                         const uint64_t* chain_off, uint32_t nchains, uint32_t* done, uint32_t* ticket,
-                         uint8_t* out, ChainRes* res, uint16_t* gsort, const inf::FixedTabs* fx) {
+                         const uint64_t* chain_off, uint32_t nlist, uint32_t* done, uint32_t* ticket,
+                         uint8_t* out, ChainRes* res, uint16_t* gsort, const inf::FixedTabs* fx,
+                         uint64_t dict_len, uint32_t* taint, const uint32_t* sel) {
     using namespace inf;
     extern __shared__ uint16_t lds_tab[];
     const int lane = threadIdx.x & 63;
@@ -909,8 +920,10 @@ ndfl_inflate_emit_kernel(const uint32_t* w, uint64_t nwords, uint64_t nbits, con
     uint32_t base = 0;
     if (lane == 0) base = atomicAdd(ticket, 64u);
     base = __shfl(base, 0, 64);
-    const uint32_t i = base + (uint32_t)lane;
-    const bool valid = i < nchains;
+    // `sel` (resolve pass): the listed chains only, in stream order; the others are already done
+    const uint32_t k = base + (uint32_t)lane;
+    const bool valid = k < nlist;
+    const uint32_t i = valid ? (sel ? sel[k] : k) : 0;
     In in{w, nwords, nbits};
     Lane L;
     EmitChain ch;
@@ -921,17 +934,20 @@ ndfl_inflate_emit_kernel(const uint32_t* w, uint64_t nwords, uint64_t nbits, con
     L.empty_dist = false; L.status = 0; L.reason = 0; L.cp_len = 0; L.cp_dist = 0; L.lastb = 0;
     L.wc = 0; L.wcn = 0;
     bool active = valid;
+    bool tainted = false;
     int idle = 0;
     uint32_t waits = 0;
     while (__any(active)) {
         bool waiting = false;
         if (active) {
-            bool more = emit_step(L, in, t, gs, fx, out, ch.out_off, chain_off, done, i, waiting);
+            bool more = emit_step(L, in, t, gs, fx, out, ch.out_off, chain_off, done, i, waiting, dict_len,
+                                  taint, tainted);
             if (waiting && ++waits > (1u << 26)) {          // safety net: never hang the device
                 more = false; L.status = ST_ERROR; L.reason = R_INTERNAL;
             }
             if (!more) {
                 active = false;
+                if (taint) taint[i] = tainted ? 1u : 0u;
                 __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
                 asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
                 __hip_atomic_store(&done[i], 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
@@ -958,19 +974,28 @@ struct InflateScratch {
     void* d_chains = nullptr; size_t d_chains_cap = 0;
     void* d_off = nullptr; size_t d_off_cap = 0;
     void* d_done = nullptr; size_t d_done_cap = 0;
+    void* d_taint = nullptr; size_t d_taint_cap = 0;
+    void* d_sel = nullptr; size_t d_sel_cap = 0;
     void* d_ticket = nullptr;
     void* d_out = nullptr; size_t d_out_cap = 0;
     double last_ms_find = 0, last_ms_count = 0, last_ms_emit = 0, last_ms_wall = 0;
     hipEvent_t ev[6] = {nullptr, nullptr, nullptr, nullptr, nullptr, nullptr};
     uint64_t repairs = 0, chains = 0, candidates = 0;
     bool count_first = false;
+    // state kept for ndfl_inflate_resolve after a deferred-window range decode
+    bool pending = false;
+    const uint32_t* p_w = nullptr;
+    uint64_t p_nwords = 0, p_nbits = 0, p_dict_len = 0;
+    uint8_t* p_out = nullptr;
+    uint32_t p_nch = 0;
     void release() {
         void** ps[] = {&d_in, &d_cand, &d_starts, &d_stops, &d_res, &d_tabs, &d_fixed, &d_chains, &d_off,
-                       &d_done, &d_ticket, &d_out};
+                       &d_done, &d_taint, &d_sel, &d_ticket, &d_out};
         for (void** p : ps) { if (*p) hipFree(*p); *p = nullptr; }
         for (auto& e : ev) { if (e) hipEventDestroy(e); e = nullptr; }
         d_in_cap = d_cand_cap = d_starts_cap = d_stops_cap = d_res_cap = d_tabs_cap = d_chains_cap = 0;
-        d_off_cap = d_done_cap = d_out_cap = 0;
+        d_off_cap = d_done_cap = d_taint_cap = d_sel_cap = d_out_cap = 0;
+        pending = false;
     }
 };
 
@@ -1013,14 +1038,21 @@ static constexpr uint32_t LDS_TAB_BYTES = inf::LDS_BYTES;
 
 #define INF_CHK(x) do { hipError_t _e = (x); if (_e != hipSuccess) return -4; } while (0)
 
-static int inflate_run(InflateScratch& S, hipStream_t s, const uint8_t* in, uint64_t in_len, uint8_t* out,
-                       uint64_t out_cap, uint64_t* out_len, uint64_t* consumed_bits, uint32_t flags,
-                       hipEvent_t ev0, hipEvent_t ev1, double* last_ms) {
+// Decode one raw DEFLATE stream, or the block-aligned range [start_bit, end_bit) of one.
+//   out       the window start: out[0, dict_len) holds the dict_len bytes of output preceding the
+//             range (0 for a whole stream); decoded bytes go to out[dict_len, dict_len + n)
+//   deferred  the window content is not valid yet: chains that read it (directly or through other
+//             chains) are recorded and re-emitted by inflate_resolve once it is written
+static int inflate_run(InflateScratch& S, hipStream_t s, const uint8_t* in, uint64_t in_len, uint64_t start_bit,
+                       uint64_t end_bit, uint8_t* out, uint64_t dict_len, uint64_t out_cap, uint64_t* out_len,
+                       uint64_t* consumed_bits, uint32_t flags, bool deferred, double* last_ms) {
     using namespace inf;
     *out_len = 0;
     *consumed_bits = 0;
+    S.pending = false;
     const uint64_t nbits = in_len * 8;
     const uint64_t nwords = (in_len + 3) / 4;
+    if (start_bit > nbits) return -1;
     // input words (padded copy when the caller's buffer is host memory or unaligned)
     const uint32_t* d_w;
     if ((flags & 1u) && (((uintptr_t)in) & 3) == 0 && (in_len % 4 == 0)) {
@@ -1063,27 +1095,33 @@ static int inflate_run(InflateScratch& S, hipStream_t s, const uint8_t* in, uint
     INF_CHK(hipMemcpyAsync(hcnt.data(), d_cnt, nseg * 4ull, hipMemcpyDeviceToHost, s));
     INF_CHK(hipStreamSynchronize(s));
     std::vector<uint64_t> hoff(nseg + 1);
-    hoff[0] = 1;                                   // slot 0 is the stream start (bit 0)
+    hoff[0] = 1;                                   // slot 0 is the range start
     for (uint32_t k = 0; k < nseg; k++) hoff[k + 1] = hoff[k] + std::min(hcnt[k], SEG_CAP);
     const uint64_t ncand_all = hoff[nseg];
     INF_CHK(inf_ensure(&S.d_starts, &S.d_starts_cap, (ncand_all + nseg + 2) * 8));
     uint64_t* d_sorted = (uint64_t*)S.d_starts;
     uint64_t* d_segoff = d_sorted + ncand_all;
     INF_CHK(hipMemcpyAsync(d_segoff, hoff.data(), nseg * 8ull, hipMemcpyHostToDevice, s));
-    INF_CHK(hipMemsetAsync(d_sorted, 0, 8, s));
     hipLaunchKernelGGL(ndfl_inflate_compact_kernel, dim3((nseg + 255) / 256), dim3(256), 0, s, (const uint32_t*)d_cnt,
                        (const uint64_t*)d_list, (const uint64_t*)d_segoff, nseg, d_sorted);
     INF_CHK(hipGetLastError());
     std::vector<uint64_t> starts(ncand_all);
-    INF_CHK(hipMemcpyAsync(starts.data(), d_sorted, ncand_all * 8, hipMemcpyDeviceToHost, s));
+    INF_CHK(hipMemcpyAsync(starts.data() + 1, d_sorted + 1, (ncand_all - 1) * 8, hipMemcpyDeviceToHost, s));
     INF_CHK(hipStreamSynchronize(s));
-    // drop a duplicate bit-0 entry (a header at bit 0 found by the finder)
-    starts.erase(std::unique(starts.begin(), starts.end()), starts.end());
+    starts[0] = start_bit;
+    // keep candidates inside the range; drop a duplicate of the start (a header found there)
+    {
+        size_t m = 1;
+        for (size_t k = 1; k < starts.size(); k++)
+            if (starts[k] > start_bit && starts[k] < end_bit) starts[m++] = starts[k];
+        starts.resize(m);
+    }
     const std::vector<uint64_t> sorted_cand(starts);
 
     auto next_after = [&](uint64_t b) -> uint64_t {
         auto ub = std::upper_bound(sorted_cand.begin(), sorted_cand.end(), b);
-        return ub != sorted_cand.end() ? *ub : NONE;
+        const uint64_t nx = ub != sorted_cand.end() ? *ub : NONE;
+        return std::min(nx, end_bit);
     };
     std::vector<ChainRes> res;
     auto run_count = [&](const std::vector<uint64_t>& st, std::vector<ChainRes>& r) -> int {
@@ -1099,7 +1137,7 @@ static int inflate_run(InflateScratch& S, hipStream_t s, const uint8_t* in, uint
         if (S.count_first) INF_CHK(hipEventRecord(S.ev[2], s));
         hipLaunchKernelGGL(ndfl_inflate_count_kernel, dim3((uint32_t)((n + 63) / 64)), dim3(64), LDS_TAB_BYTES, s, d_w,
                            nwords, nbits, (const uint64_t*)S.d_starts, (const uint64_t*)S.d_stops, (uint32_t)n,
-                           (ChainRes*)S.d_res, (uint16_t*)S.d_tabs, (const FixedTabs*)S.d_fixed);
+                           (ChainRes*)S.d_res, (uint16_t*)S.d_tabs, (const FixedTabs*)S.d_fixed, start_bit, dict_len);
         INF_CHK(hipGetLastError());
         if (S.count_first) { INF_CHK(hipEventRecord(S.ev[3], s)); S.count_first = false; }
         r.resize(n);
@@ -1118,16 +1156,16 @@ static int inflate_run(InflateScratch& S, hipStream_t s, const uint8_t* in, uint
         S.last_ms_find = a; S.last_ms_count = b;
     }
 
-    // link from bit 0.  A boundary that is no candidate (fixed-Huffman block, header rejected by
-    // the finder) is repaired: every such boundary of every chain is decoded on in parallel
-    // rounds; a final serial fallback guarantees progress.
+    // link from the range start.  A boundary that is no candidate (fixed-Huffman block, header
+    // rejected by the finder) is repaired: every such boundary of every chain is decoded on in
+    // parallel rounds; a final serial fallback guarantees progress.
     std::unordered_map<uint64_t, size_t> at;
     at.reserve(starts.size() * 2);
     for (size_t k = 0; k < starts.size(); k++) at[starts[k]] = k;
     for (int round = 0; round < 8; round++) {
         std::vector<uint64_t> todo;
         for (size_t k = 0; k < res.size(); k++)
-            if (res[k].status == ST_BOUNDARY && !at.count(res[k].end_bit)) {
+            if (res[k].status == ST_BOUNDARY && res[k].end_bit < end_bit && !at.count(res[k].end_bit)) {
                 at[res[k].end_bit] = NONE;          // placeholder, filled below
                 todo.push_back(res[k].end_bit);
             }
@@ -1144,9 +1182,9 @@ static int inflate_run(InflateScratch& S, hipStream_t s, const uint8_t* in, uint
     }
     std::vector<EmitChain> chains;
     std::vector<uint64_t> offs;
-    uint64_t off = 0;
+    uint64_t off = dict_len;
     size_t cur = 0;
-    uint64_t end_bit = 0;
+    uint64_t stop_bit = 0;
     for (;;) {
         const ChainRes& r = res[cur];
         EmitChain ec;
@@ -1157,8 +1195,10 @@ static int inflate_run(InflateScratch& S, hipStream_t s, const uint8_t* in, uint
         chains.push_back(ec);
         offs.push_back(off);
         off += r.out_count;
-        if (r.status == ST_FINAL) { end_bit = r.end_bit; break; }
+        if (r.status == ST_FINAL) { stop_bit = r.end_bit; break; }
         if (r.status == ST_ERROR) break;
+        if (r.end_bit == end_bit) { stop_bit = end_bit; break; }
+        if (r.end_bit > end_bit) return -1;          // the range end is no block boundary
         auto it = at.find(r.end_bit);
         if (it != at.end() && it->second != (size_t)NONE) { cur = it->second; continue; }
         // serial fallback (beyond the parallel rounds)
@@ -1174,7 +1214,7 @@ static int inflate_run(InflateScratch& S, hipStream_t s, const uint8_t* in, uint
     }
     S.chains = chains.size();
     S.candidates = sorted_cand.size();
-    const uint64_t total = off;
+    const uint64_t total = off - dict_len;
     if (total > out_cap) { *out_len = total; return -3; }
 
     // emit pass
@@ -1184,23 +1224,29 @@ static int inflate_run(InflateScratch& S, hipStream_t s, const uint8_t* in, uint
     INF_CHK(inf_ensure(&S.d_done, &S.d_done_cap, nch * 4ull));
     INF_CHK(inf_ensure(&S.d_res, &S.d_res_cap, nch * sizeof(ChainRes)));
     INF_CHK(inf_ensure(&S.d_tabs, &S.d_tabs_cap, ((nch + 63) / 64) * (uint64_t)G_SORT * 64 * 2));
+    if (deferred) INF_CHK(inf_ensure(&S.d_taint, &S.d_taint_cap, nch * 4ull));
     if (!S.d_ticket) INF_CHK(hipMalloc(&S.d_ticket, 64));
     INF_CHK(hipMemcpyAsync(S.d_chains, chains.data(), nch * sizeof(EmitChain), hipMemcpyHostToDevice, s));
-    offs.push_back(total);
+    offs.push_back(off);
     INF_CHK(hipMemcpyAsync(S.d_off, offs.data(), (nch + 1) * 8ull, hipMemcpyHostToDevice, s));
     INF_CHK(hipMemsetAsync(S.d_done, 0, nch * 4ull, s));
     INF_CHK(hipMemsetAsync(S.d_ticket, 0, 64, s));
     uint8_t* d_out;
-    bool direct = (flags & 2u) != 0;
+    const bool direct = (flags & 2u) != 0;
     if (direct) d_out = out;
-    else { INF_CHK(inf_ensure(&S.d_out, &S.d_out_cap, total + 64)); d_out = (uint8_t*)S.d_out; }
+    else {
+        INF_CHK(inf_ensure(&S.d_out, &S.d_out_cap, dict_len + total + 64));
+        d_out = (uint8_t*)S.d_out;
+        if (dict_len) INF_CHK(hipMemcpyAsync(d_out, out, dict_len, hipMemcpyHostToDevice, s));
+    }
     hipEvent_t e2 = S.ev[4], e3 = S.ev[5];
     INF_CHK(hipEventRecord(e2, s));
     const uint32_t waves = (nch + 63) / 64;
     hipLaunchKernelGGL(ndfl_inflate_emit_kernel, dim3(waves), dim3(64), LDS_TAB_BYTES, s, d_w, nwords, nbits,
                        (const EmitChain*)S.d_chains, (const uint64_t*)S.d_off, nch, (uint32_t*)S.d_done,
                        (uint32_t*)S.d_ticket, d_out, (ChainRes*)S.d_res, (uint16_t*)S.d_tabs,
-                       (const FixedTabs*)S.d_fixed);
+                       (const FixedTabs*)S.d_fixed, dict_len, deferred ? (uint32_t*)S.d_taint : (uint32_t*)nullptr,
+                       (const uint32_t*)nullptr);
     INF_CHK(hipGetLastError());
     INF_CHK(hipEventRecord(e3, s));
     std::vector<ChainRes> er(nch);
@@ -1213,20 +1259,54 @@ static int inflate_run(InflateScratch& S, hipStream_t s, const uint8_t* in, uint
     hipEventElapsedTime(&ms2, S.ev[0], e3);
     S.last_ms_wall = ms2;
     *last_ms = ms;
-    (void)ev0; (void)ev1;
+    if (deferred) {
+        S.pending = true;
+        S.p_w = d_w; S.p_nwords = nwords; S.p_nbits = nbits; S.p_dict_len = dict_len; S.p_out = d_out; S.p_nch = nch;
+    }
     // first error in stream order (the emit pass also checks the dictionary bound exactly)
-    uint64_t produced = 0;
     for (uint32_t k = 0; k < nch; k++) {
         if (er[k].status == ST_ERROR) {
-            produced = chains[k].out_off + er[k].out_count;
-            if (!direct && produced) INF_CHK(hipMemcpy(out, d_out, produced, hipMemcpyDeviceToHost));
+            const uint64_t produced = chains[k].out_off - dict_len + er[k].out_count;
+            if (!direct && produced) INF_CHK(hipMemcpy(out + dict_len, d_out + dict_len, produced, hipMemcpyDeviceToHost));
             *out_len = produced;
             *consumed_bits = er[k].end_bit;
             return (int)er[k].reason;
         }
     }
-    if (!direct && total) INF_CHK(hipMemcpy(out, d_out, total, hipMemcpyDeviceToHost));
+    if (!direct && total) INF_CHK(hipMemcpy(out + dict_len, d_out + dict_len, total, hipMemcpyDeviceToHost));
     *out_len = total;
-    *consumed_bits = end_bit;
+    *consumed_bits = stop_bit;
+    return 0;
+}
+
+// Second half of a deferred-window range decode: the caller has written the window
+// (out[0, dict_len)); re-emit, in stream order, exactly the chains that read it.
+static int inflate_resolve(InflateScratch& S, hipStream_t s, uint64_t* n_reemitted) {
+    using namespace inf;
+    *n_reemitted = 0;
+    if (!S.pending) return -5;
+    S.pending = false;
+    const uint32_t nch = S.p_nch;
+    std::vector<uint32_t> taint(nch);
+    INF_CHK(hipMemcpyAsync(taint.data(), S.d_taint, nch * 4ull, hipMemcpyDeviceToHost, s));
+    INF_CHK(hipStreamSynchronize(s));
+    std::vector<uint32_t> sel, done(nch);
+    for (uint32_t k = 0; k < nch; k++) {
+        done[k] = taint[k] ? 0u : 1u;
+        if (taint[k]) sel.push_back(k);
+    }
+    *n_reemitted = sel.size();
+    if (sel.empty()) return 0;
+    const uint32_t nsel = (uint32_t)sel.size();
+    INF_CHK(inf_ensure(&S.d_sel, &S.d_sel_cap, nsel * 4ull));
+    INF_CHK(hipMemcpyAsync(S.d_sel, sel.data(), nsel * 4ull, hipMemcpyHostToDevice, s));
+    INF_CHK(hipMemcpyAsync(S.d_done, done.data(), nch * 4ull, hipMemcpyHostToDevice, s));
+    INF_CHK(hipMemsetAsync(S.d_ticket, 0, 64, s));
+    hipLaunchKernelGGL(ndfl_inflate_emit_kernel, dim3((nsel + 63) / 64), dim3(64), LDS_TAB_BYTES, s, S.p_w, S.p_nwords,
+                       S.p_nbits, (const EmitChain*)S.d_chains, (const uint64_t*)S.d_off, nsel, (uint32_t*)S.d_done,
+                       (uint32_t*)S.d_ticket, S.p_out, (ChainRes*)S.d_res, (uint16_t*)S.d_tabs,
+                       (const FixedTabs*)S.d_fixed, S.p_dict_len, (uint32_t*)nullptr, (const uint32_t*)S.d_sel);
+    INF_CHK(hipGetLastError());
+    INF_CHK(hipStreamSynchronize(s));
     return 0;
 }

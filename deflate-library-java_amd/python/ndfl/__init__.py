@@ -17,7 +17,7 @@ import enum
 import io
 
 from . import _lib
-from ._lib import IN_DEVICE, OUT_DEVICE, STRATEGIES, NdflError, check, load, reason_name
+from ._lib import IN_DEVICE, OUT_DEVICE, DICT_DEFERRED, NO_END, STRATEGIES, NdflError, check, load, reason_name
 
 __all__ = ["Context", "Reason", "DataFormatException", "DeflaterOutputStream", "InflaterInputStream",
            "GzipMetadata", "GzipOutputStream", "GzipInputStream", "ZlibMetadata", "ZlibOutputStream",
@@ -164,6 +164,27 @@ class Context:
             check(r, "ndfl_inflate")
             reason = None if r == 0 else Reason(r - 1)
             return reason, out.raw[:olen], bits
+
+    def inflate_range_raw(self, in_addr, in_len, start_bit, end_bit, out_addr, dict_len, out_cap, flags):
+        """ndfl_inflate_range: decode bits [start_bit, end_bit) into out_addr + dict_len, with the
+        dict_len bytes at out_addr as the window.  Returns (code, out_len, consumed_bits)."""
+        L = load()
+        olen = ctypes.c_uint64(0)
+        bits = ctypes.c_uint64(0)
+        r = L.ndfl_inflate_range(self._h, in_addr, in_len, start_bit, NO_END if end_bit is None else end_bit,
+                                 out_addr, dict_len, out_cap, ctypes.byref(olen), ctypes.byref(bits), flags)
+        return r, olen.value, bits.value
+
+    def inflate_resolve(self):
+        """Finish a DICT_DEFERRED range decode once the window is written; returns re-emitted chains."""
+        n = ctypes.c_uint64(0)
+        check(load().ndfl_inflate_resolve(self._h, ctypes.byref(n)), "ndfl_inflate_resolve")
+        return n.value
+
+    def bits_shift_raw(self, in_addr, nbits, shift, out_addr, out_cap):
+        """ndfl_bits_shift on device buffers: in's first nbits bits placed at bit `shift` of out."""
+        check(load().ndfl_bits_shift(self._h, in_addr, nbits, shift, out_addr, out_cap, IN_DEVICE | OUT_DEVICE),
+              "ndfl_bits_shift")
 
     def crc32(self, data, crc=0, flags=0):
         addr, keep = _ptr(data)

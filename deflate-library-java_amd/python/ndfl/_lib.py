@@ -9,6 +9,8 @@ LIB_PATH = os.path.join(PKG_ROOT, "lib", "libndfl.so")
 
 IN_DEVICE = 1
 OUT_DEVICE = 2
+DICT_DEFERRED = 4
+NO_END = (1 << 64) - 1
 
 STRATEGIES = {"LITERAL_STATIC": 0, "LITERAL_DYNAMIC": 1, "RLE_STATIC": 2, "RLE_DYNAMIC": 3,
               "FULL_STATIC": 4, "FULL_DYNAMIC": 5, "UNCOMPRESSED": 6}
@@ -28,7 +30,8 @@ E_ARG, E_UNSUPPORTED, E_CAPACITY, E_DEVICE, E_STATE, E_INTERNAL = -1, -2, -3, -4
 # Every symbol include/ndfl.h declares (checked by tests/test_capi_symbols.py).
 EXPORTS = ["ndfl_abi_version", "ndfl_error_string", "ndfl_ctx_create", "ndfl_ctx_destroy",
            "ndfl_ctx_set_stream", "ndfl_ctx_last_kernel_ms", "ndfl_ctx_timings", "ndfl_deflate_chunks", "ndfl_deflate_bound",
-           "ndfl_inflate", "ndfl_crc32", "ndfl_crc32_combine"]
+           "ndfl_inflate", "ndfl_inflate_range", "ndfl_inflate_resolve", "ndfl_bits_shift", "ndfl_crc32",
+           "ndfl_crc32_combine"]
 
 _lib = None
 
@@ -55,6 +58,10 @@ def load():
     L.ndfl_deflate_bound.restype = u64
     L.ndfl_deflate_bound.argtypes = [u64, u32]
     L.ndfl_inflate.argtypes = [vp, vp, u64, vp, u64, ctypes.POINTER(u64), ctypes.POINTER(u64), u32]
+    L.ndfl_inflate_range.argtypes = [vp, vp, u64, u64, u64, vp, u64, u64, ctypes.POINTER(u64), ctypes.POINTER(u64),
+                                     u32]
+    L.ndfl_inflate_resolve.argtypes = [vp, ctypes.POINTER(u64)]
+    L.ndfl_bits_shift.argtypes = [vp, vp, u64, u32, vp, u64, u32]
     L.ndfl_crc32.argtypes = [vp, ctypes.POINTER(u32), vp, u64, u32]
     L.ndfl_crc32_combine.restype = u32
     L.ndfl_crc32_combine.argtypes = [u32, u32, u64]

@@ -1,0 +1,202 @@
+"""Multi-GPU DEFLATE of ONE stream: one process per GPU, shard by 64 KiB chunk.
+
+The reference is single-threaded; its stream is a sequence of chunk blocks whose bits depend only
+on raw input (D/DeflaterOutputStream.java:119-137).  So rank r compresses chunks
+[r*K, (r+1)*K) by itself.  The exchange steps are the only places where ranks talk to each other:
+
+  compress    (1) the raw bytes preceding the shard (the encoder's history, <= 32 KiB) go from
+                  rank r-1 to rank r, point to point;
+              (2) all_gather of every shard's bit count and byte count: the seam index;
+              (3) each rank moves its bits to its global bit offset mod 8 (ndfl_bits_shift), so
+                  the global stream is the concatenation of the shards with the shared boundary
+                  bytes ORed (BitOut's packing, D/DeflaterOutputStream.java:147-156).
+  decompress  each rank decodes its seam-delimited bit range with a deferred window
+              (ndfl_inflate_range + NDFL_DICT_DEFERRED), all ranks in parallel; then the last
+              32 KiB of output pass from rank to rank (the reference's dictionary ring,
+              D/decomp/Open.java:592-603) and each rank re-emits only the blocks that read them
+              (ndfl_inflate_resolve).
+
+The protocol is codec-agnostic: `DeviceCodec` runs it on the GPU through the C ABI; the CPU tests
+drive the same functions with a checker codec over gloo.
+"""
+from dataclasses import dataclass, field
+
+WINDOW = 32768
+
+
+@dataclass
+class Part:
+    """One rank's piece of the global stream."""
+    buf: object                 # uint8 tensor: the shard's bits start at bit `shift` of buf[0]
+    nbits: int                  # bits of this shard
+    shift: int                  # global bit offset mod 8
+    bit_offsets: list = field(default_factory=list)    # seam index: global bit offset per rank (+ total)
+    byte_offsets: list = field(default_factory=list)   # uncompressed byte offset per rank (+ total)
+
+    @property
+    def nbytes(self):
+        return (self.shift + self.nbits + 7) // 8
+
+
+class DeviceCodec:
+    """The GPU codec (libndfl.so through ndfl.Context) on torch device tensors."""
+
+    def __init__(self, ctx, torch):
+        self.ctx = ctx
+        self.torch = torch
+        self.device = torch.device("cuda", ctx.device)
+        ctx.set_stream(torch.cuda.current_stream(self.device).cuda_stream)
+
+    def empty(self, n):
+        return self.torch.empty(max(1, n), dtype=self.torch.uint8, device=self.device)
+
+    def bound(self, n, chunk_len):
+        from . import _lib
+        return _lib.load().ndfl_deflate_bound(n, chunk_len) + 64
+
+    def deflate_chunks(self, hist, data, final, out, strategy, chunk_len, hist_limit):
+        from . import IN_DEVICE, OUT_DEVICE, _strategy_id
+        hl = 0 if hist is None else hist.numel()
+        endbits, _ = self.ctx.deflate_chunks_raw(hist.data_ptr() if hl else None, hl, hist_limit, data.data_ptr(),
+                                                 data.numel(), chunk_len, _strategy_id(strategy), final, 0,
+                                                 out.data_ptr(), out.numel(), IN_DEVICE | OUT_DEVICE)
+        return endbits
+
+    def bits_shift(self, src, nbits, shift, dst):
+        self.ctx.bits_shift_raw(src.data_ptr(), nbits, shift, dst.data_ptr(), dst.numel())
+
+    def inflate_range(self, src, in_len, start_bit, end_bit, out, dict_len, deferred):
+        from . import IN_DEVICE, OUT_DEVICE, DICT_DEFERRED
+        flags = IN_DEVICE | OUT_DEVICE | (DICT_DEFERRED if deferred else 0)
+        return self.ctx.inflate_range_raw(src.data_ptr(), in_len, start_bit, end_bit, out.data_ptr(), dict_len,
+                                          out.numel() - dict_len, flags)
+
+    def resolve(self):
+        return self.ctx.inflate_resolve()
+
+
+def _staged(dist, t):
+    """gloo moves host tensors only: stage device tensors through the host (tests / rehearsals on a
+    single GPU); RCCL moves device tensors directly over xGMI."""
+    return t.is_cuda and dist.get_backend() == "gloo"
+
+
+def _send(dist, t, dst):
+    dist.send(t.cpu() if _staged(dist, t) else t, dst)
+
+
+def _recv(dist, t, src):
+    if _staged(dist, t):
+        tmp = t.cpu()
+        dist.recv(tmp, src)
+        t.copy_(tmp)
+    else:
+        dist.recv(t, src)
+
+
+def _gather_ints(dist, torch, value, world, device):
+    """all_gather of one int64 per rank."""
+    dev = "cpu" if dist.get_backend() == "gloo" else device
+    t = torch.tensor([int(value)], dtype=torch.int64, device=dev)
+    lst = [torch.zeros(1, dtype=torch.int64, device=dev) for _ in range(world)]
+    dist.all_gather(lst, t)
+    return [int(x.item()) for x in lst]
+
+
+def _exchange_prev(dist, torch, send_t, recv_t, rank, world):
+    """send_t -> rank+1, recv_t <- rank-1 (point to point, all pairs at once)."""
+    if _staged(dist, send_t) or _staged(dist, recv_t):
+        # host staging: even ranks send first, odd ranks receive first (no deadlock on blocking p2p)
+        for phase in (0, 1):
+            if (rank + phase) % 2 == 0:
+                if rank + 1 < world:
+                    _send(dist, send_t, rank + 1)
+            elif rank > 0:
+                _recv(dist, recv_t, rank - 1)
+        return
+    ops = []
+    if rank + 1 < world:
+        ops.append(dist.P2POp(dist.isend, send_t, rank + 1))
+    if rank > 0:
+        ops.append(dist.P2POp(dist.irecv, recv_t, rank - 1))
+    if ops:
+        for req in dist.batch_isend_irecv(ops):
+            req.wait()
+
+
+def deflate_shard(codec, dist, torch, shard, rank, world, *, strategy="RLE_DYNAMIC", chunk_len=65536,
+                  hist_limit=WINDOW, work=None, out=None):
+    """Compress this rank's shard as chunks [r*K, (r+1)*K) of one stream.  Every shard but the
+    last must hold whole chunks.  `work`/`out`: optional preallocated buffers (bound bytes)."""
+    n = shard.numel()
+    if rank + 1 < world and (n == 0 or n % chunk_len):
+        raise ValueError("every shard but the last must be a positive multiple of chunk_len")
+    # (1) history: the last min(hist_limit, n) raw bytes of the previous shard
+    hlen = min(hist_limit, n)
+    sizes = _gather_ints(dist, torch, n, world, codec.device)
+    prev_h = min(hist_limit, sizes[rank - 1]) if rank > 0 else 0
+    hist = codec.empty(prev_h)[:prev_h]
+    _exchange_prev(dist, torch, shard[n - hlen:].contiguous() if hlen else codec.empty(0)[:0], hist, rank, world)
+    if prev_h < min(hist_limit, sum(sizes[:rank])):
+        raise ValueError("a shard shorter than the history window precedes this one")
+    # local compress at bit 0
+    cap = codec.bound(n, chunk_len)
+    work = work if work is not None else codec.empty(cap)
+    nbits = codec.deflate_chunks(hist if prev_h else None, shard, rank == world - 1, work, strategy, chunk_len,
+                                 hist_limit)
+    # (2) seam index
+    nb = _gather_ints(dist, torch, nbits, world, codec.device)
+    bit_offsets = [0]
+    for v in nb:
+        bit_offsets.append(bit_offsets[-1] + v)
+    byte_offsets = [0]
+    for v in sizes:
+        byte_offsets.append(byte_offsets[-1] + v)
+    # (3) realign to the global bit offset
+    shift = bit_offsets[rank] % 8
+    out = out if out is not None else codec.empty(cap + 1)
+    codec.bits_shift(work, nbits, shift, out)
+    return Part(out, nbits, shift, bit_offsets, byte_offsets)
+
+
+def inflate_shard(codec, dist, torch, part, out, rank, world):
+    """Decode this rank's range of the stream into out[dict_len:], out[:dict_len] = the window.
+    Returns (code, out_len, dict_len): code 0 or the Reason+1 of the FIRST error in stream order
+    over all ranks (every rank returns the same code)."""
+    dict_len = min(WINDOW, part.byte_offsets[rank])
+    deferred = rank > 0 and dict_len > 0
+    code, olen, _ = codec.inflate_range(part.buf, part.nbytes, part.shift, part.shift + part.nbits, out, dict_len,
+                                        deferred)
+    if code < 0:
+        raise RuntimeError(f"inflate_range failed: {code}")
+    # window chain: rank r-1's last 32 KiB of output -> rank r
+    if rank > 0 and dict_len:
+        _recv(dist, out[:dict_len], rank - 1)
+        if code == 0:
+            codec.resolve()
+    if rank + 1 < world:
+        nxt = min(WINDOW, part.byte_offsets[rank + 1])
+        end = dict_len + olen
+        if code == 0 and end >= nxt:
+            _send(dist, out[end - nxt:end].contiguous(), rank + 1)
+        else:                                    # an error ends the stream here: keep the chain moving
+            _send(dist, torch.zeros(nxt, dtype=torch.uint8, device=codec.device), rank + 1)
+    # first error in stream order
+    codes = _gather_ints(dist, torch, code, world, codec.device)
+    first = next((c for c in codes if c != 0), 0)
+    return first, olen, dict_len
+
+
+def assemble(parts):
+    """Join the parts (host bytes objects with their shift/nbits) into the global stream, ORing the
+    byte each pair of neighbours shares.  Used by the tests and by a writer that gathers to one rank."""
+    out = bytearray()
+    for buf, shift, nbits in parts:
+        nbytes = (shift + nbits + 7) // 8
+        b = bytes(buf[:nbytes])
+        if shift and out:
+            out[-1] |= b[0]
+            out += b[1:]
+        else:
+            out += b
+    return bytes(out)

@@ -50,6 +50,7 @@ enum ndfl_strategy {
 /* memory flags */
 #define NDFL_IN_DEVICE   1u    /* input pointers (data, hist) are device memory */
 #define NDFL_OUT_DEVICE  2u    /* output pointer is device memory */
+#define NDFL_DICT_DEFERRED 4u  /* ndfl_inflate_range: window bytes are written later (see resolve) */
 
 typedef struct ndfl_ctx ndfl_ctx;
 
@@ -106,6 +107,39 @@ uint64_t ndfl_deflate_bound(uint64_t len, uint32_t chunk_len);
  */
 int ndfl_inflate(ndfl_ctx* ctx, const uint8_t* in, uint64_t in_len, uint8_t* out, uint64_t out_cap,
                  uint64_t* out_len, uint64_t* consumed_bits, uint32_t flags);
+
+/*
+ * Decompress the block-aligned bit range [start_bit, end_bit) of one raw DEFLATE stream: one GPU's
+ * shard of a stream decoded across GPUs.  Same decoder as ndfl_inflate, i.e.
+ * Open.read (D/decomp/Open.java:83-124), started at a block boundary with the reference's
+ * dictionary state (the 32 KiB ring, :592-603) given by the caller instead of built up.
+ *   out         window start: out[0, dict_len) holds the dict_len (<= 32768) output bytes preceding
+ *               the range; decoded bytes are written to out[dict_len, dict_len + *out_len)
+ *   end_bit     stop at the block boundary == end_bit (UINT64_MAX: run to the final block);
+ *               NDFL_E_ARG if a block straddles it
+ *   flags       NDFL_DICT_DEFERRED (requires NDFL_OUT_DEVICE): the window is not written yet.  The
+ *               call decodes everything, records which chains of blocks read the window (directly
+ *               or through other chains), and ndfl_inflate_resolve re-emits exactly those after the
+ *               caller has written it; so all GPUs decode in parallel and only the window (32 KiB)
+ *               is passed along.  `in` and `out` must stay valid until the resolve call.
+ * Returns as ndfl_inflate (COPY_FROM_BEFORE_DICTIONARY_START counts the window as dictionary).
+ */
+int ndfl_inflate_range(ndfl_ctx* ctx, const uint8_t* in, uint64_t in_len, uint64_t start_bit, uint64_t end_bit,
+                       uint8_t* out, uint64_t dict_len, uint64_t out_cap, uint64_t* out_len,
+                       uint64_t* consumed_bits, uint32_t flags);
+/* Finish the last NDFL_DICT_DEFERRED range decode on this context (NDFL_E_STATE if none). */
+int ndfl_inflate_resolve(ndfl_ctx* ctx, uint64_t* n_reemitted);
+
+/*
+ * Multi-GPU seam step for compression: place the first `nbits` bits of `in` at bit
+ * `shift` (0..7) of out[0] (lower bits 0, bits past the end 0).  A shard compressed at bit 0 by
+ * ndfl_deflate_chunks is thereby moved to its global bit offset mod 8; the byte shared with the
+ * previous shard is ORed when the stream is assembled -- BitOut's byte packing
+ * (D/DeflaterOutputStream.java:147-156) across GPUs.  Device pointers only (NDFL_IN_DEVICE |
+ * NDFL_OUT_DEVICE), not in place.
+ */
+int ndfl_bits_shift(ndfl_ctx* ctx, const uint8_t* in, uint64_t nbits, uint32_t shift, uint8_t* out,
+                    uint64_t out_cap, uint32_t flags);
 
 /* java.util.zip.CRC32.update over a buffer, on the GPU (flags: NDFL_IN_DEVICE). */
 int ndfl_crc32(ndfl_ctx* ctx, uint32_t* crc_inout, const uint8_t* data, uint64_t len, uint32_t flags);

@@ -440,6 +440,36 @@ int64_t or_deflate(const uint8_t* data, uint64_t len, uint32_t chunk_len, uint32
     return (int64_t)w.n;
 }
 
+int64_t or_deflate_chunks(const uint8_t* hist, uint64_t hist_len, const uint8_t* data, uint64_t len,
+                          uint32_t chunk_len, uint32_t hist_limit, int strategy, int final_flag,
+                          uint8_t* out, uint64_t out_cap, uint64_t* out_bits) {
+    if (strategy < 0 || strategy > 6 || chunk_len < 1 || hist_limit > 32768) return OR_ERR_ARG;
+    if (!final_flag && (len == 0 || len % chunk_len != 0)) return OR_ERR_ARG;
+    if (hist_len > hist_limit) { hist += hist_len - hist_limit; hist_len = hist_limit; }
+    uint8_t* buf = (uint8_t*)malloc((size_t)(hist_len + len + 1));
+    if (!buf) return OR_ERR_ARG;
+    if (hist_len) memcpy(buf, hist, (size_t)hist_len);
+    if (len) memcpy(buf + hist_len, data, (size_t)len);
+    bw_t w = {out, out_cap, 0, 0, 0, 0};
+    uint64_t pos = hist_len, end = hist_len + len;               /* positions in buf */
+    for (;;) {                                                   /* writeBuffer per chunk */
+        uint64_t dlen = end - pos; int fin = final_flag;
+        if (dlen > chunk_len) { dlen = chunk_len; fin = 0; }
+        else if (final_flag && dlen == chunk_len && pos + dlen < end) fin = 0;
+        uint64_t hlen = pos < hist_limit ? pos : hist_limit;
+        sink_t sk = { &w, 0 };
+        if (strategy == OR_UNCOMPRESSED) unc_compress(buf + (pos - hlen), 0, (int64_t)hlen, (int64_t)dlen, fin, &sk);
+        else lz_compress(buf + (pos - hlen), 0, (int64_t)hlen, (int64_t)dlen, &PRESETS[strategy], fin, &sk, 0);
+        pos += dlen;
+        if (fin || pos >= end) break;
+    }
+    free(buf);
+    *out_bits = w.n * 8 + (uint64_t)w.len;
+    for (; w.len > 0; w.len -= 8, w.buf >>= 8) bw_put(&w, (uint8_t)w.buf);   /* pending bits, zero-padded */
+    if (w.overflow) return OR_ERR_CAPACITY;
+    return (int64_t)w.n;
+}
+
 int64_t or_deflate_mixed(const uint8_t* data, uint64_t len, uint32_t chunk_len, uint32_t hist_limit,
                          const int8_t* strat, uint32_t nstrat, uint8_t* out, uint64_t out_cap) {
     /* Fixture generator: chunk i is encoded with strategy strat[i % nstrat] (a mix of stored,
@@ -562,10 +592,16 @@ static const int8_t  DIST_EXTRA[30] = {0,0,0,0,1,1,2,2,3,3,4,4,5,5,6,6,7,7,8,8,9
 
 typedef struct { uint8_t* out; uint64_t cap, n; } ob_t;
 
-int or_inflate(const uint8_t* in, uint64_t in_len, uint8_t* out, uint64_t out_cap,
-               uint64_t* out_len, uint64_t* consumed_bits) {
-    br_t r = {in, in_len * 8, 0};
+/* One raw DEFLATE stream (or a block-aligned range of one): Open.read (:83-124) run to the end.
+ * Range form (multi-GPU shards): decoding starts at bit `start_bit` with `dict_len` bytes of
+ * preceding output available to copies (the reference's 32 KiB ring, :592-603), and stops at the
+ * first block boundary == `end_bit` (UINT64_MAX: after the final block). */
+int or_inflate_range(const uint8_t* in, uint64_t in_len, uint64_t start_bit, uint64_t end_bit,
+                     const uint8_t* dict, uint64_t dict_len, uint8_t* out, uint64_t out_cap,
+                     uint64_t* out_len, uint64_t* consumed_bits) {
+    br_t r = {in, in_len * 8, start_bit};
     uint64_t n = 0;
+    if (dict_len > 32768) { dict += dict_len - 32768; dict_len = 32768; }
     int err = 0, last = 0;
     int16_t litTree[2 * 288], distTree[2 * 32], clTree[2 * 19];
     int16_t fixLit[2 * 288], fixDist[2 * 32];
@@ -579,6 +615,7 @@ int or_inflate(const uint8_t* in, uint64_t in_len, uint8_t* out, uint64_t out_ca
 #define CHK(x) do { err = (x); if (err) goto fail; } while (0)
     while (!last) {                                          /* Open.read :83-110 */
         uint32_t bf, bt;
+        if (r.pos == end_bit) break;
         CHK(br_bits(&r, 1, &bf));
         last = (int)bf;
         CHK(br_bits(&r, 2, &bt));
@@ -662,10 +699,11 @@ int or_inflate(const uint8_t* in, uint64_t in_len, uint8_t* out, uint64_t out_ca
             if (dsym > 29) CHK(OR_RESERVED_DISTANCE_SYMBOL);
             CHK(br_bits(&r, DIST_EXTRA[dsym], &e));
             uint64_t dist = (uint64_t)DIST_BASE[dsym] + e;
-            uint64_t dictLen = n < 32768 ? n : 32768;
+            uint64_t dictLen = n + dict_len < 32768 ? n + dict_len : 32768;
             if (dist > dictLen) CHK(OR_COPY_FROM_BEFORE_DICTIONARY_START);   /* :592-593 */
             if (n + (uint64_t)run > out_cap) { err = OR_ERR_CAPACITY; goto fail; }
-            for (int i = 0; i < run; i++, n++) out[n] = out[n - dist];      /* byte-serial copy */
+            for (int i = 0; i < run; i++, n++)                               /* byte-serial copy */
+                out[n] = n >= dist ? out[n - dist] : dict[dict_len - (dist - n)];
         }
     }
     *out_len = n;
@@ -676,6 +714,11 @@ fail:
     *consumed_bits = r.pos;
     return err;
 #undef CHK
+}
+
+int or_inflate(const uint8_t* in, uint64_t in_len, uint8_t* out, uint64_t out_cap,
+               uint64_t* out_len, uint64_t* consumed_bits) {
+    return or_inflate_range(in, in_len, 0, UINT64_MAX, NULL, 0, out, out_cap, out_len, consumed_bits);
 }
 
 /* ------------------------------------------------------------------------------------------ */

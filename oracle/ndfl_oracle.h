@@ -70,6 +70,19 @@ int64_t or_deflate_mixed(const uint8_t* data, uint64_t len, uint32_t chunk_len, 
  * final block (meaningful on success).  OR_ERR_CAPACITY if out_cap is too small. */
 int or_inflate(const uint8_t* in, uint64_t in_len, uint8_t* out, uint64_t out_cap,
                uint64_t* out_len, uint64_t* consumed_bits);
+/* Range form: start at start_bit with dict_len bytes of preceding output, stop at the block
+ * boundary == end_bit (UINT64_MAX: after the final block). */
+int or_inflate_range(const uint8_t* in, uint64_t in_len, uint64_t start_bit, uint64_t end_bit,
+                     const uint8_t* dict, uint64_t dict_len, uint8_t* out, uint64_t out_cap,
+                     uint64_t* out_len, uint64_t* consumed_bits);
+
+/* K iterations of DeflaterOutputStream.writeBuffer (D/DeflaterOutputStream.java:119-137) on
+ * `data` with the raw bytes `hist` before it (only its last min(hist_limit, .) bytes are used),
+ * starting at bit 0: the semantics of ndfl_deflate_chunks.  final_flag = 0 requires whole chunks.
+ * Writes ceil(bits/8) bytes (last byte zero-padded, no finish()); *out_bits = bits. */
+int64_t or_deflate_chunks(const uint8_t* hist, uint64_t hist_len, const uint8_t* data, uint64_t len,
+                          uint32_t chunk_len, uint32_t hist_limit, int strategy, int final_flag,
+                          uint8_t* out, uint64_t out_cap, uint64_t* out_bits);
 
 /* Checksums (JDK java.util.zip.CRC32 / Adler32 semantics: CRC-32/ISO-HDLC, Adler-32). */
 uint32_t or_crc32(uint32_t crc, const uint8_t* p, uint64_t n);

@@ -120,3 +120,22 @@ def c4_mixed(n, seed=0xC4, device="cpu"):
 def c3_text(n, seed=0xC3, device="cpu"):
     g = torch.Generator(device=device).manual_seed(seed)
     return _text(g, n, device, nwords=65536)
+
+
+def mixed_bytes(n_total, seed):
+    """Small host-side mix (random spans, byte runs, 7-letter text) for the multi-rank and range
+    tests: bytes, seeded numpy generator."""
+    import numpy as np
+    rng = np.random.default_rng(seed)
+    parts, size = [], 0
+    while size < n_total:
+        kind = rng.integers(0, 3)
+        ln = int(rng.integers(1000, 60000))
+        if kind == 0:
+            parts.append(rng.integers(0, 256, ln, dtype=np.uint8).tobytes())
+        elif kind == 1:
+            parts.append(bytes([int(rng.integers(0, 256))]) * ln)
+        else:
+            parts.append(bytes(rng.choice(list(b"abcde \n"), ln).astype(np.uint8)))
+        size += ln
+    return b"".join(parts)[:n_total]

@@ -65,6 +65,13 @@ def lib():
         L.or_inflate.restype = ctypes.c_int
         L.or_inflate.argtypes = [u8p, ctypes.c_uint64, u8p, ctypes.c_uint64,
                                  ctypes.POINTER(ctypes.c_uint64), ctypes.POINTER(ctypes.c_uint64)]
+        L.or_deflate_chunks.restype = ctypes.c_int64
+        L.or_deflate_chunks.argtypes = [u8p, ctypes.c_uint64, u8p, ctypes.c_uint64, ctypes.c_uint32, ctypes.c_uint32,
+                                        ctypes.c_int, ctypes.c_int, u8p, ctypes.c_uint64, ctypes.POINTER(ctypes.c_uint64)]
+        L.or_inflate_range.restype = ctypes.c_int
+        L.or_inflate_range.argtypes = [u8p, ctypes.c_uint64, ctypes.c_uint64, ctypes.c_uint64, u8p, ctypes.c_uint64,
+                                       u8p, ctypes.c_uint64, ctypes.POINTER(ctypes.c_uint64),
+                                       ctypes.POINTER(ctypes.c_uint64)]
         L.or_crc32.restype = ctypes.c_uint32
         L.or_crc32.argtypes = [ctypes.c_uint32, u8p, ctypes.c_uint64]
         L.or_adler32.restype = ctypes.c_uint32
@@ -124,6 +131,20 @@ def deflate_mixed(data, strategies, chunk_len=65535, hist_limit=32768):
     return out.raw[:r]
 
 
+def deflate_chunks(hist, data, final, strategy="RLE_DYNAMIC", chunk_len=65536, hist_limit=32768):
+    """ndfl_deflate_chunks semantics on the CPU: returns (bytes, nbits), stream starting at bit 0."""
+    h, hn = _buf(hist)
+    src, n = _buf(data)
+    cap = deflate_bound(n, chunk_len)
+    out = ctypes.create_string_buffer(cap)
+    bits = ctypes.c_uint64(0)
+    r = lib().or_deflate_chunks(h, hn, src, n, chunk_len, hist_limit, STRATEGIES.index(strategy), int(final), out, cap,
+                                ctypes.byref(bits))
+    if r < 0:
+        raise ValueError(f"or_deflate_chunks failed: {r}")
+    return out.raw[:r], bits.value
+
+
 def block_bits(data, strategy="RLE_DYNAMIC", chunk_len=65536, hist_limit=32768):
     src, n = _buf(data)
     nchunks = max(1, -(-n // chunk_len))
@@ -147,6 +168,26 @@ def inflate(data, out_cap=None):
             continue
         if r < 0:
             raise ValueError(f"or_inflate error {r}")
+        return reason_name(r), out.raw[:olen.value], bits.value
+
+
+def inflate_range(data, start_bit=0, end_bit=None, dictionary=b"", out_cap=None):
+    """Range decode (multi-GPU shard): start at start_bit with `dictionary` as preceding output, stop
+    at the block boundary == end_bit (None: after the final block).  Returns like inflate()."""
+    src, n = _buf(data)
+    d, dn = _buf(dictionary)
+    cap = out_cap if out_cap is not None else 4 * n + 65536
+    while True:
+        out = ctypes.create_string_buffer(max(1, cap))
+        olen = ctypes.c_uint64(0)
+        bits = ctypes.c_uint64(0)
+        r = lib().or_inflate_range(src, n, start_bit, (1 << 64) - 1 if end_bit is None else end_bit, d, dn, out,
+                                   cap, ctypes.byref(olen), ctypes.byref(bits))
+        if r == -1 and out_cap is None and cap < 1100 * n + 65536:
+            cap *= 8
+            continue
+        if r < 0:
+            raise ValueError(f"or_inflate_range error {r}")
         return reason_name(r), out.raw[:olen.value], bits.value
 
 

@@ -1,0 +1,118 @@
+"""One rank of the multi-process sharded-stream check (launched by tests/test_parallel_cpu.py
+through torch.distributed.run, gloo backend, CPU).  Drives ndfl.parallel's protocol with the
+oracle as the codec, so the exchange steps (history halo, seam index, bit realignment, window
+chain, first-error reduction) are checked without a GPU: the assembled stream must equal the
+oracle's single-stream encoding bit for bit, and each rank must get its shard back."""
+import json
+import os
+import sys
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, HERE)
+sys.path.insert(0, os.path.join(os.path.dirname(HERE), "deflate-library-java_amd", "python"))
+
+import torch  # noqa: E402
+import torch.distributed as dist  # noqa: E402
+
+import oracle_lib as O  # noqa: E402
+from corpus import mixed_bytes  # noqa: E402
+from ndfl import parallel as P  # noqa: E402
+
+
+class OracleCodec:
+    """Checker codec: the oracle behind the DeviceCodec interface, on CPU tensors."""
+    device = torch.device("cpu")
+
+    def __init__(self):
+        self.pending = None
+        self.resolved = 0
+
+    def empty(self, n):
+        return torch.zeros(max(1, n), dtype=torch.uint8)
+
+    def bound(self, n, chunk_len):
+        return O.deflate_bound(n, chunk_len) + 64
+
+    def deflate_chunks(self, hist, data, final, out, strategy, chunk_len, hist_limit):
+        h = b"" if hist is None else bytes(hist.numpy())
+        b, nbits = O.deflate_chunks(h, bytes(data.numpy()), final, strategy, chunk_len, hist_limit)
+        out[:len(b)] = torch.frombuffer(bytearray(b), dtype=torch.uint8)
+        return nbits
+
+    def bits_shift(self, src, nbits, shift, dst):
+        nin = (nbits + 7) // 8
+        v = int.from_bytes(bytes(src[:nin].numpy()), "little") & ((1 << nbits) - 1)
+        nout = (nbits + shift + 7) // 8
+        dst[:nout] = torch.frombuffer(bytearray((v << shift).to_bytes(nout, "little")), dtype=torch.uint8)
+
+    def _decode(self, data, start, end, out, dict_len, window):
+        r, dec, bits = O.inflate_range(data, start, end, window)
+        if dec:
+            out[dict_len:dict_len + len(dec)] = torch.frombuffer(bytearray(dec), dtype=torch.uint8)
+        code = 0 if r is None else O.REASONS.index(r) + 1
+        return code, len(dec), bits
+
+    def inflate_range(self, src, in_len, start, end, out, dict_len, deferred):
+        data = bytes(src[:in_len].numpy())
+        window = bytes(dict_len) if deferred else bytes(out[:dict_len].numpy())
+        self.pending = (data, start, end, out, dict_len) if deferred else None
+        return self._decode(data, start, end, out, dict_len, window)
+
+    def resolve(self):
+        data, start, end, out, dict_len = self.pending
+        self.pending = None
+        self._decode(data, start, end, out, dict_len, bytes(out[:dict_len].numpy()))
+        self.resolved += 1
+        return 1
+
+
+def main():
+    dist.init_process_group("gloo")
+    rank, world = dist.get_rank(), dist.get_world_size()
+    cfg = json.loads(os.environ["NDFL_PAR_CFG"])
+    chunk = cfg["chunk_len"]
+    sizes = [cfg["chunks_per_rank"] * chunk] * (world - 1) + [cfg["last_bytes"]]
+    data = mixed_bytes(sum(sizes), cfg["seed"])
+    if cfg.get("seam_run"):
+        # a byte run across every seam: the next rank's first block copies from the window
+        b = bytearray(data)
+        off = 0
+        for s in sizes[:-1]:
+            off += s
+            hi = min(off + 5000, len(b))
+            b[off - 5000:hi] = b"\x07" * (hi - off + 5000)
+        data = bytes(b)
+    off = sum(sizes[:rank])
+    shard = torch.frombuffer(bytearray(data[off:off + sizes[rank]]), dtype=torch.uint8)
+    if cfg.get("codec") == "device":
+        # the GPU codec through the C ABI; every rank on cuda:0, gloo stages the exchanges via host
+        import ndfl
+        codec = P.DeviceCodec(ndfl.Context(0), torch)
+        shard = shard.to(codec.device)
+    else:
+        codec = OracleCodec()
+    part = P.deflate_shard(codec, dist, torch, shard, rank, world, strategy=cfg["strategy"], chunk_len=chunk)
+    mine = (bytes(part.buf[:part.nbytes].cpu().numpy()), part.shift, part.nbits)
+    allp = [None] * world
+    dist.all_gather_object(allp, mine)
+    ok = {}
+    if rank == 0:
+        stream = P.assemble(allp)
+        ref = O.deflate(data, cfg["strategy"], chunk)
+        ok["stream_equal"] = stream == ref
+        ok["total_bits"] = part.bit_offsets[-1]
+    out = torch.zeros(P.WINDOW + sizes[rank] + 64, dtype=torch.uint8, device=codec.device)
+    code, olen, dict_len = P.inflate_shard(codec, dist, torch, part, out, rank, world)
+    ok["code"] = code
+    ok["decoded_equal"] = olen == sizes[rank] and \
+        bytes(out[dict_len:dict_len + olen].cpu().numpy()) == bytes(shard.cpu().numpy())
+    ok["resolved"] = getattr(codec, "resolved", None)
+    res = [None] * world
+    dist.all_gather_object(res, ok)
+    if rank == 0:
+        print("RESULT " + json.dumps(res), flush=True)
+    dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

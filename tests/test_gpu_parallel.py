@@ -1,0 +1,147 @@
+"""GPU checks of the multi-GPU building blocks through the C ABI: bit realignment
+(ndfl_bits_shift), range decode with a window (ndfl_inflate_range), deferred windows
+(NDFL_DICT_DEFERRED + ndfl_inflate_resolve), and the whole sharded protocol with 2 ranks sharing
+cuda:0 over gloo (host-staged exchanges)."""
+import os
+import random
+
+import pytest
+
+import oracle_lib as O
+from corpus import mixed_bytes
+
+pytestmark = pytest.mark.gpu
+
+
+@pytest.fixture(scope="module")
+def env():
+    import torch
+    import ndfl
+    return torch, ndfl, ndfl.Context(0)
+
+
+def test_bits_shift_matches_integer_shift(env):
+    torch, ndfl, ctx = env
+    rng = random.Random(5)
+    for nbits in [1, 7, 8, 9, 31, 32, 33, 1000, 8 * 4096 + 3, 1 << 20]:
+        nin = (nbits + 7) // 8
+        src_b = bytes(rng.getrandbits(8) for _ in range(nin))
+        v = int.from_bytes(src_b, "little") & ((1 << nbits) - 1)
+        for off in (0, 1):                       # aligned and unaligned source
+            src = torch.frombuffer(bytearray(b"\xAA" * off + src_b + b"\xFF" * 8), dtype=torch.uint8).cuda()
+            for shift in range(8):
+                nout = (nbits + shift + 7) // 8
+                dst = torch.full((nout + 8,), 0x55, dtype=torch.uint8, device="cuda")
+                ctx.bits_shift_raw(src.data_ptr() + off, nbits, shift, dst.data_ptr(), nout)
+                got = bytes(dst[:nout].cpu().numpy())
+                assert got == (v << shift).to_bytes(nout, "little"), (nbits, off, shift)
+                assert bytes(dst[nout:].cpu().numpy()) == b"\x55" * 8
+
+
+def _stream_and_seams(data, strategy="RLE_DYNAMIC", chunk=65536):
+    comp = O.deflate(data, strategy, chunk)
+    bits = O.block_bits(data, strategy, chunk)
+    seams = [0]
+    for b in bits:
+        seams.append(seams[-1] + b)
+    return comp, seams
+
+
+@pytest.mark.parametrize("strategy", ["RLE_DYNAMIC", "FULL_DYNAMIC", "RLE_STATIC"])
+def test_inflate_range_with_window_matches_oracle(env, strategy):
+    torch, ndfl, ctx = env
+    data = mixed_bytes(12 * 65536 + 999, seed=11)
+    comp, seams = _stream_and_seams(data, strategy)
+    dev_in = torch.frombuffer(bytearray(comp), dtype=torch.uint8).cuda()
+    for a, b in [(0, 3), (3, 7), (5, 13), (12, 13), (1, 2)]:
+        s_bit, e_bit = seams[a], seams[b] if b < len(seams) - 1 else None
+        out_pre = a * 65536
+        dict_len = min(32768, out_pre)
+        window = data[out_pre - dict_len:out_pre]
+        r0, ref, rbits = O.inflate_range(comp, s_bit, e_bit, window)
+        assert r0 is None
+        n = len(ref)
+        out = torch.zeros(dict_len + n + 64, dtype=torch.uint8, device="cuda")
+        if dict_len:
+            out[:dict_len] = torch.frombuffer(bytearray(window), dtype=torch.uint8).cuda()
+        r, olen, bits = ctx.inflate_range_raw(dev_in.data_ptr(), len(comp), s_bit, e_bit, out.data_ptr(), dict_len,
+                                              n + 64, ndfl.IN_DEVICE | ndfl.OUT_DEVICE)
+        assert (r, olen, bits) == (0, n, rbits), (a, b)
+        assert bytes(out[dict_len:dict_len + n].cpu().numpy()) == ref
+        # host-memory variant (window staged by the library)
+        hbuf = bytearray(window + bytes(n + 64))
+        import ctypes
+        cbuf = (ctypes.c_uint8 * len(hbuf)).from_buffer(hbuf)
+        cin = ctypes.create_string_buffer(comp, len(comp))
+        r, olen, bits = ctx.inflate_range_raw(ctypes.addressof(cin), len(comp), s_bit, e_bit, ctypes.addressof(cbuf),
+                                              dict_len, n + 64, 0)
+        assert (r, olen) == (0, n) and bytes(hbuf[dict_len:dict_len + n]) == ref
+
+
+def test_inflate_range_dictionary_bound(env):
+    torch, ndfl, ctx = env
+    # a range whose first block copies from 1 byte back needs >= 1 byte of window
+    data = b"\x07" * 200000
+    comp, seams = _stream_and_seams(data)
+    dev_in = torch.frombuffer(bytearray(comp), dtype=torch.uint8).cuda()
+    out = torch.zeros(32768 + 200000, dtype=torch.uint8, device="cuda")
+    r, olen, bits = ctx.inflate_range_raw(dev_in.data_ptr(), len(comp), seams[1], None, out.data_ptr(), 0, 200000,
+                                          ndfl.IN_DEVICE | ndfl.OUT_DEVICE)
+    r0, _, _ = O.inflate_range(comp, seams[1], None, b"")
+    assert r0 == "COPY_FROM_BEFORE_DICTIONARY_START"
+    assert r == O.REASONS.index(r0) + 1
+    out[:1] = 7
+    r, olen, bits = ctx.inflate_range_raw(dev_in.data_ptr(), len(comp), seams[1], None, out.data_ptr(), 1, 200000,
+                                          ndfl.IN_DEVICE | ndfl.OUT_DEVICE)
+    assert (r, olen) == (0, 200000 - 65536)
+
+
+def test_range_end_must_be_block_boundary(env):
+    torch, ndfl, ctx = env
+    data = mixed_bytes(4 * 65536, seed=3)
+    comp, seams = _stream_and_seams(data)
+    dev_in = torch.frombuffer(bytearray(comp), dtype=torch.uint8).cuda()
+    out = torch.zeros(4 * 65536 + 64, dtype=torch.uint8, device="cuda")
+    r, _, _ = ctx.inflate_range_raw(dev_in.data_ptr(), len(comp), 0, seams[2] - 5, out.data_ptr(), 0, out.numel(),
+                                    ndfl.IN_DEVICE | ndfl.OUT_DEVICE)
+    assert r == ndfl._lib.E_ARG
+
+
+@pytest.mark.parametrize("seed", [1, 2])
+def test_deferred_window_then_resolve(env, seed):
+    torch, ndfl, ctx = env
+    rng = random.Random(seed)
+    # runs across every chunk seam + LZ77 (FULL) so chains read the window transitively
+    parts = []
+    for k in range(10):
+        parts.append(mixed_bytes(50000, seed=seed * 100 + k))
+        parts.append(bytes([rng.getrandbits(8)]) * rng.randint(20000, 90000))
+    data = bytearray(b"".join(parts))
+    data[4 * 65536 - 1000:4 * 65536 + 1000] = b"\x5a" * 2000    # the range starts inside a run
+    data = bytes(data)
+    for strategy in ("RLE_DYNAMIC", "FULL_DYNAMIC"):
+        comp, seams = _stream_and_seams(data, strategy)
+        dev_in = torch.frombuffer(bytearray(comp), dtype=torch.uint8).cuda()
+        a = 4
+        pre = a * 65536
+        window = data[pre - 32768:pre]
+        r0, ref, _ = O.inflate_range(comp, seams[a], None, window)
+        assert r0 is None
+        out = torch.full((32768 + len(ref) + 64,), 0xEE, dtype=torch.uint8, device="cuda")
+        r, olen, bits = ctx.inflate_range_raw(dev_in.data_ptr(), len(comp), seams[a], None, out.data_ptr(), 32768,
+                                              len(ref) + 64, ndfl.IN_DEVICE | ndfl.OUT_DEVICE | ndfl.DICT_DEFERRED)
+        assert (r, olen) == (0, len(ref))
+        out[:32768] = torch.frombuffer(bytearray(window), dtype=torch.uint8).cuda()
+        n_re = ctx.inflate_resolve()
+        assert n_re >= 1
+        assert bytes(out[32768:32768 + olen].cpu().numpy()) == ref
+        with pytest.raises(ndfl.NdflError):
+            ctx.inflate_resolve()                       # nothing pending any more
+
+
+def test_sharded_protocol_two_ranks_one_gpu():
+    from test_parallel_cpu import run_workers
+    res = run_workers(2, dict(chunk_len=65536, chunks_per_rank=6, last_bytes=300001, seed=9,
+                              strategy="RLE_DYNAMIC", seam_run=True, codec="device"))
+    assert res[0]["stream_equal"]
+    assert all(r["code"] == 0 and r["decoded_equal"] for r in res)
