@@ -1,0 +1,796 @@
+// inflate_wave.hpp -- wave-per-chain decode passes (count + emit) of the MI355X DEFLATE decoder.
+//
+// One wave64 per chain of blocks (a chain starts at a header candidate).  Per block:
+//   * lane 0 parses the header (D/decomp/Open.java:232-431, the reference's check order) into
+//     code lengths in LDS; the wave builds ONE set of decode tables in LDS for the block
+//     (canonical codes by ballot ranks, D/decomp/Open.java:705-789): a 10-bit literal/length and an
+//     8-bit distance primary whose entries carry the run/distance base and extra-bit count, with a
+//     canonical slow path for longer codes;
+//   * the block's data bits are split into 64 segments, one per lane.  Lane j decodes from its
+//     segment start s_j (usually inside a codeword: speculative), recording its first token
+//     starts, up to the first token boundary >= s_{j+1}.  Then every lane re-decodes from the TRUE
+//     start (the previous lane's exit) until it reaches one of its own recorded token starts --
+//     from there its speculative decode is exact (Huffman decoding self-synchronises, usually
+//     within a few tokens) -- or decodes its whole segment if it never meets one.  A fix-up loop
+//     re-runs lanes whose predecessor's exit moved.  The first lane that sees the end-of-block
+//     symbol or an error ends the block; when no lane does (the segment end was a false header
+//     candidate), the next round continues from lane 63's exit.
+//   * count pass: output bytes, end bit, status per chain (the host links chains);
+//     emit pass: a third decode per segment writes the output at its offset.  A copy whose source
+//     lies in an earlier lane's segment waits (per-step progress counters in LDS); a source in an
+//     earlier chain waits on that chain's done flag, as before.
+// Many waves per CU (small LDS footprint) hide the per-token latency chain.
+#pragma once
+
+namespace wv {
+using namespace inf;
+
+constexpr uint32_t LB = 10;                 // literal/length primary bits
+constexpr uint32_t DB = 8;                  // distance primary bits
+constexpr int BUDGET = 16;                  // tokens per emit step
+// table entry: [4:0] code length (0: longer than the primary), [8:5] extra bits, [10:9] kind,
+// [31:16] literal byte / run base / distance base
+enum : uint32_t { K_LIT = 0, K_LEN = 1, K_EOB = 2, K_BAD = 3 };
+enum : uint32_t { T_EXIT = 0, T_EOB = 1, T_ERR = 2 };
+
+struct Tabs {
+    uint32_t lit[1u << LB];
+    uint32_t dst[1u << DB];
+    uint16_t lfirst[16], lcnt[16], loff[16];
+    uint16_t dfirst[16], dcnt[16], doff[16];
+    uint16_t lsorted[288];
+    uint16_t dsorted[32];
+};
+
+struct Shared {
+    Tabs t;
+    uint8_t lens[320];                       // literal/length 0..287, distance at 288..319
+    uint16_t cl_tab[128];                    // code-length code, full 7-bit table: sym | len << 9
+    uint32_t ph_cp[7][64];                   // fallback phases 1..7: checkpoint offset,
+    uint32_t ph_cpc[7][64];                  //   bytes before it,
+    uint32_t ph_end[7][64];                  //   end offset,
+    uint32_t ph_cnt[7][64];                  //   bytes,
+    uint32_t ph_kr[7][64];                   //   kind << 16 | reason
+    uint64_t exit_[64];
+    uint32_t kind_[64];
+    uint64_t off_[64];                       // emit: absolute output offset per lane
+    uint64_t cnt_[64];                       // emit: output bytes per lane
+    uint32_t prog[64];                       // emit: bytes durably written per lane
+    // header broadcast (lane 0 -> wave)
+    uint64_t h_pos, h_d0;
+    uint32_t h_err, h_bfinal, h_btype, h_len, h_numlit, h_numdist;
+};
+
+__device__ __forceinline__ uint32_t lit_entry(uint32_t sym, uint32_t len) {
+    if (sym < 256) return len | (K_LIT << 9) | (sym << 16);
+    if (sym == 256) return len | (K_EOB << 9);
+    if (sym <= 285) {
+        uint32_t base, ne;
+        run_base(sym - 257, base, ne);
+        return len | (ne << 5) | (K_LEN << 9) | (base << 16);
+    }
+    return len | (K_BAD << 9);
+}
+__device__ __forceinline__ uint32_t dist_entry(uint32_t sym, uint32_t len) {
+    if (sym <= 29) {
+        uint32_t base, ne;
+        dist_base(sym, base, ne);
+        return len | (ne << 5) | (base << 16);
+    }
+    return len | (K_BAD << 9);
+}
+
+__device__ __noinline__ uint32_t slow_lit(uint32_t p15, const Tabs& t) {
+    const uint32_t r15 = rev_bits(p15, 15);
+    for (uint32_t l = LB + 1; l < 16; l++) {
+        const uint32_t idx = (r15 >> (15 - l)) - t.lfirst[l];
+        if (idx < t.lcnt[l]) return lit_entry(t.lsorted[t.loff[l] + idx], l);
+    }
+    return 15u | (K_BAD << 9);              // unreachable: codes are complete
+}
+__device__ __noinline__ uint32_t slow_dist(uint32_t p15, const Tabs& t) {
+    const uint32_t r15 = rev_bits(p15, 15);
+    for (uint32_t l = DB + 1; l < 16; l++) {
+        const uint32_t idx = (r15 >> (15 - l)) - t.dfirst[l];
+        if (idx < t.dcnt[l]) return dist_entry(t.dsorted[t.doff[l] + idx], l);
+    }
+    return 15u | (K_BAD << 9);
+}
+
+struct Tok {
+    uint32_t kind;      // K_LIT (val = byte), K_LEN (val = run, dist), K_EOB, K_BAD (val = reason)
+    uint32_t val, dist;
+};
+
+// One token of a Huffman block, with the reference's check order (D/decomp/Open.java:446-618).
+__device__ __forceinline__ void next_tok(Rp& rd, const In& in, const Tabs& t, bool empty_dist, Tok& tk) {
+    rd.fill(in);
+    uint32_t e = t.lit[rd.peek(LB)];
+    if (!(e & 31)) e = slow_lit(rd.peek(15), t);
+    rd.skip(e & 31);
+    if (rd.pos > in.nbits) { tk.kind = K_BAD; tk.val = R_UEOS; return; }
+    const uint32_t k = (e >> 9) & 3;
+    if (k == K_LIT) { tk.kind = K_LIT; tk.val = e >> 16; return; }
+    if (k == K_EOB) { tk.kind = K_EOB; return; }
+    if (k == K_BAD) { tk.kind = K_BAD; tk.val = R_RESERVED_LEN; return; }
+    const uint32_t run = (e >> 16) + rd.get(in, (e >> 5) & 15);
+    if (rd.pos > in.nbits) { tk.kind = K_BAD; tk.val = R_UEOS; return; }
+    if (empty_dist) { tk.kind = K_BAD; tk.val = R_EMPTY_DIST; return; }
+    rd.fill(in);
+    uint32_t d = t.dst[rd.peek(DB)];
+    if (!(d & 31)) d = slow_dist(rd.peek(15), t);
+    rd.skip(d & 31);
+    if (rd.pos > in.nbits) { tk.kind = K_BAD; tk.val = R_UEOS; return; }
+    if (((d >> 9) & 3) == K_BAD) { tk.kind = K_BAD; tk.val = R_RESERVED_DIST; return; }
+    const uint32_t dist = (d >> 16) + rd.get(in, (d >> 5) & 15);
+    if (rd.pos > in.nbits) { tk.kind = K_BAD; tk.val = R_UEOS; return; }
+    tk.kind = K_LEN; tk.val = run; tk.dist = dist;
+}
+
+// ---- block header (lane 0) ----------------------------------------------------------------------
+// Parses the header at p into S.h_* and (dynamic) S.lens; validation in the reference's order up to
+// END_OF_BLOCK_CODE_ZERO_LENGTH; the tree checks of the two codes follow in build_code.
+__device__ void parse_hdr(const In& in, uint64_t p, Shared& S) {
+    Rd rd;
+    rd.init(in, p);
+    S.h_err = 0; S.h_len = 0; S.h_numlit = 0; S.h_numdist = 0;
+    const uint32_t bf = rd.get(in, 1), bt = rd.get(in, 2);
+    S.h_bfinal = bf; S.h_btype = bt;
+#define HFAIL(r) do { S.h_err = (r); S.h_pos = rd.pos; return; } while (0)
+    if (rd.pos > in.nbits) HFAIL(R_UEOS);
+    if (bt == 3) HFAIL(R_RESERVED_BLOCK_TYPE);
+    if (bt == 0) {
+        rd.get(in, (uint32_t)((8 - (rd.pos & 7)) & 7));
+        const uint32_t ln = rd.get(in, 16), nln = rd.get(in, 16);
+        if (rd.pos > in.nbits) HFAIL(R_UEOS);
+        if (ln != (nln ^ 0xFFFFu)) HFAIL(R_LEN_MISMATCH);
+        S.h_len = ln; S.h_d0 = rd.pos; S.h_pos = rd.pos;
+        return;
+    }
+    if (bt == 1) { S.h_d0 = rd.pos; S.h_pos = rd.pos; return; }
+    const uint32_t hlit = rd.get(in, 5), hdist = rd.get(in, 5), hclen = rd.get(in, 4);
+    if (rd.pos > in.nbits) HFAIL(R_UEOS);
+    const uint32_t numLit = hlit + 257, numDist = hdist + 1, numCl = hclen + 4;
+    uint32_t cl[19];
+#pragma unroll
+    for (int i = 0; i < 19; i++) cl[i] = 0;
+#pragma unroll
+    for (int i = 0; i < 19; i++)
+        if ((uint32_t)i < numCl) cl[CLO[i]] = rd.get(in, 3);
+    if (rd.pos > in.nbits) HFAIL(R_UEOS);
+    uint32_t cc[16];
+#pragma unroll
+    for (int l = 0; l < 16; l++) cc[l] = 0;
+#pragma unroll
+    for (int s = 0; s < 19; s++) cc[cl[s]] += 1;
+    cc[0] = 0;
+    int e = tree_check(cc);
+    if (e) HFAIL(e);
+    {
+        uint32_t first[8], nx[8];
+        uint32_t code = 0;
+        first[0] = 0;
+        for (int l = 1; l < 8; l++) { code = (code + (l > 1 ? cc[l - 1] : 0)) << 1; first[l] = code; nx[l] = 0; }
+        for (int s = 0; s < 19; s++) {
+            const uint32_t l = cl[s];
+            if (!l) continue;
+            const uint32_t r = rev_bits(first[l] + nx[l]++, l);
+            for (uint32_t k = r; k < 128; k += (1u << l)) S.cl_tab[k] = (uint16_t)(s | (l << 9));
+        }
+    }
+    const uint32_t total = numLit + numDist;
+    uint32_t i = 0;
+    int runVal = -1;
+    while (i < total) {
+        rd.fill(in);
+        const uint32_t ent = S.cl_tab[rd.peek(7)];
+        rd.skip(ent >> 9);
+        const uint32_t sym = ent & 0x1FF;
+        if (rd.pos > in.nbits) HFAIL(R_UEOS);
+        uint32_t run = 1, v;
+        if (sym < 16) { v = sym; runVal = (int)sym; }
+        else if (sym == 16) {
+            if (runVal == -1) HFAIL(R_NO_PREV);
+            run = rd.get(in, 2) + 3; v = (uint32_t)runVal;
+        } else if (sym == 17) { runVal = 0; run = rd.get(in, 3) + 3; v = 0; }
+        else { runVal = 0; run = rd.get(in, 7) + 11; v = 0; }
+        if (rd.pos > in.nbits) HFAIL(R_UEOS);
+        if (i + run > total) HFAIL(R_CL_OVER_FULL);
+        for (uint32_t k = 0; k < run; k++, i++) S.lens[i < numLit ? i : 288 + (i - numLit)] = (uint8_t)v;
+    }
+    if (S.lens[256] == 0) HFAIL(R_EOB_ZERO);
+    S.h_numlit = numLit; S.h_numdist = numDist;
+    S.h_d0 = rd.pos; S.h_pos = rd.pos;
+#undef HFAIL
+}
+
+// Canonical code from S.lens[base .. base+n) into a primary table + slow-path arrays (wave).
+// Returns the tree check result of codeLengthsToCodeTree (D/decomp/Open.java:705-756) (uniform).
+__device__ int build_code(Shared& S, uint32_t base, uint32_t n, uint32_t* prim, uint32_t pbits, uint16_t* first,
+                          uint16_t* cntv, uint16_t* offv, uint16_t* sorted, bool is_lit, int lane) {
+    for (uint32_t k = (uint32_t)lane; k < (1u << pbits); k += 64) prim[k] = 0;
+    uint32_t c[16];
+#pragma unroll
+    for (int l = 0; l < 16; l++) c[l] = 0;
+    uint32_t mylen[5], rank[5];
+    const uint64_t lt = (1ull << lane) - 1;
+#pragma unroll
+    for (int q = 0; q < 5; q++) {
+        const uint32_t s = (uint32_t)q * 64 + (uint32_t)lane;
+        const uint32_t l = (s < n) ? S.lens[base + s] : 0u;
+        mylen[q] = l;
+        rank[q] = 0;
+        if ((uint32_t)q * 64 < n) {
+#pragma unroll
+            for (int L = 1; L < 16; L++) {
+                const uint64_t m = __ballot(l == (uint32_t)L);
+                if (l == (uint32_t)L) rank[q] = c[L] + (uint32_t)__popcll(m & lt);
+                c[L] += (uint32_t)__popcll(m);
+            }
+        }
+    }
+    const int err = tree_check(c);
+    if (err) return err;
+    uint32_t fst[16], off[16];
+    {
+        uint32_t code = 0, o = 0;
+        fst[0] = 0; off[0] = 0;
+#pragma unroll
+        for (int l = 1; l < 16; l++) {
+            code = (code + (l > 1 ? c[l - 1] : 0)) << 1;
+            fst[l] = code; off[l] = o; o += c[l];
+        }
+    }
+    if (lane < 16) { first[lane] = (uint16_t)fst[lane]; cntv[lane] = (uint16_t)c[lane]; offv[lane] = (uint16_t)off[lane]; }
+    __syncthreads();
+#pragma unroll
+    for (int q = 0; q < 5; q++) {
+        const uint32_t l = mylen[q];
+        if (!l) continue;
+        const uint32_t s = (uint32_t)q * 64 + (uint32_t)lane;
+        uint32_t f = 0, o = 0;
+#pragma unroll
+        for (int L = 1; L < 16; L++) if (l == (uint32_t)L) { f = fst[L]; o = off[L]; }
+        sorted[o + rank[q]] = (uint16_t)s;
+        if (l <= pbits) {
+            const uint32_t ent = is_lit ? lit_entry(s, l) : dist_entry(s, l);
+            for (uint32_t k = rev_bits(f + rank[q], l); k < (1u << pbits); k += (1u << l)) prim[k] = ent;
+        }
+    }
+    __syncthreads();
+    return 0;
+}
+
+// Fixed code lengths (D/decomp/Open.java:812-830) into S.lens.
+__device__ void fixed_lens(Shared& S, int lane) {
+    for (uint32_t s = (uint32_t)lane; s < 320; s += 64) {
+        uint32_t l;
+        if (s < 288) l = s < 144 ? 8 : s < 256 ? 9 : s < 280 ? 7 : 8;
+        else l = 5;
+        S.lens[s] = (uint8_t)l;
+    }
+}
+
+// Tables for the block whose header S.h_* describes.  Returns a Reason (uniform) or 0.
+__device__ int build_tables(Shared& S, int lane, bool& empty_dist) {
+    empty_dist = false;
+    if (S.h_btype == 1) {
+        fixed_lens(S, lane);
+        __syncthreads();
+        build_code(S, 0, 288, S.t.lit, LB, S.t.lfirst, S.t.lcnt, S.t.loff, S.t.lsorted, true, lane);
+        build_code(S, 288, 32, S.t.dst, DB, S.t.dfirst, S.t.dcnt, S.t.doff, S.t.dsorted, false, lane);
+        return 0;
+    }
+    const uint32_t numDist = S.h_numdist;
+    int e = build_code(S, 0, 288, S.t.lit, LB, S.t.lfirst, S.t.lcnt, S.t.loff, S.t.lsorted, true, lane);
+    if (e) return e;
+    // distance code: empty (one zero length) or one used code padded at index 31 (:398-425)
+    const uint32_t dl = (lane < 32) ? S.lens[288 + lane] : 0u;
+    empty_dist = numDist == 1 && S.lens[288] == 0;
+    if (empty_dist) return 0;
+    const uint32_t ones = (uint32_t)__popcll(__ballot(dl == 1)), other = (uint32_t)__popcll(__ballot(dl > 1));
+    __syncthreads();
+    if (ones == 1 && other == 0 && lane == 0) S.lens[288 + 31] = 1;
+    __syncthreads();
+    return build_code(S, 288, 32, S.t.dst, DB, S.t.dfirst, S.t.dcnt, S.t.doff, S.t.dsorted, false, lane);
+}
+
+// ---- segmented speculative decode of one round ------------------------------------------------
+// Lane j owns [s_j, e_j) and a checkpoint C_j = s_j + min(XCP, e_j - s_j).  A speculative run from
+// a start records (cp, cpc): its first token boundary >= C_j (offset from s_j) and the output bytes
+// before it, plus its end state.  Two decodes that stand on the same boundary at the checkpoint
+// agree from there on, so a verify run from the TRUE start only decodes up to C_j and, on a match,
+// takes the speculative end state.  Codes whose lengths are all multiples of 8 never resynchronise
+// from a wrong bit phase; for them the fallback adds runs from s_j+1 .. s_j+7 (one per phase).
+constexpr uint32_t XCP = 128;
+constexpr uint32_t NPH = 8;
+constexpr uint32_t NOCP = 0xFFFFFFFFu;
+
+struct Seg {
+    uint64_t start, end, cnt;
+    uint32_t kind, reason;
+};
+struct Spec {
+    uint64_t end, cnt;
+    uint32_t kind, reason, cp, cpc;
+};
+
+__device__ void spec_run(const In& in, const Tabs& t, bool ed, uint64_t st, uint64_t s, uint64_t C, uint64_t e,
+                         Spec& o) {
+    Rp rd;
+    rd.init(in, st);
+    uint64_t cnt = 0;
+    uint32_t kind = T_EXIT, reason = 0, cp = NOCP, cpc = 0;
+    Tok tk;
+    for (;;) {
+        if (cp == NOCP && rd.pos >= C) { cp = (uint32_t)(rd.pos - s); cpc = (uint32_t)min(cnt, (uint64_t)NOCP); }
+        if (rd.pos >= e) break;
+        next_tok(rd, in, t, ed, tk);
+        if (tk.kind == K_LIT) { cnt++; continue; }
+        if (tk.kind == K_LEN) { cnt += tk.val; continue; }
+        kind = tk.kind == K_EOB ? T_EOB : T_ERR;
+        reason = tk.kind == K_EOB ? 0u : tk.val;
+        break;
+    }
+    if (cnt >= NOCP) cp = NOCP;                 // counts kept in 32 bits: no sync through this run
+    o.end = rd.pos; o.cnt = cnt; o.kind = kind; o.reason = reason; o.cp = cp; o.cpc = cpc;
+}
+
+// Decode from the true start t0 to the checkpoint; on a match with phase 0 (registers) or, when
+// `nph` > 1, phases 1..nph-1 (LDS), take that run's end state; otherwise decode the rest of the
+// segment (authoritative).  Returns true when it synchronised.
+__device__ bool verify_run(const In& in, const Tabs& t, bool ed, uint64_t t0, uint64_t s, uint64_t C, uint64_t e,
+                           const Spec& p0, const Shared& S, int lane, uint32_t nph, Seg& r) {
+    Rp rd;
+    rd.init(in, t0);
+    uint64_t c = 0;
+    Tok tk;
+    r.start = t0;
+    bool at_cp = false;
+    for (;;) {
+        const uint64_t q = rd.pos;
+        if (!at_cp && q >= C) {
+            at_cp = true;
+            const uint32_t off = (uint32_t)(q - s);
+            if (p0.cp == off) {
+                r.end = p0.end; r.cnt = c + (p0.cnt - p0.cpc); r.kind = p0.kind; r.reason = p0.reason;
+                return true;
+            }
+            for (uint32_t f = 1; f < nph; f++) {
+                if (S.ph_cp[f - 1][lane] == off) {
+                    r.end = s + S.ph_end[f - 1][lane];
+                    r.cnt = c + (S.ph_cnt[f - 1][lane] - S.ph_cpc[f - 1][lane]);
+                    const uint32_t kr = S.ph_kr[f - 1][lane];
+                    r.kind = kr >> 16; r.reason = kr & 0xFFFF;
+                    return true;
+                }
+            }
+        }
+        if (q >= e) { r.end = q; r.cnt = c; r.kind = T_EXIT; r.reason = 0; return false; }
+        next_tok(rd, in, t, ed, tk);
+        if (tk.kind == K_LIT) { c++; continue; }
+        if (tk.kind == K_LEN) { c += tk.val; continue; }
+        r.end = rd.pos; r.cnt = c;
+        r.kind = tk.kind == K_EOB ? T_EOB : T_ERR;
+        r.reason = tk.kind == K_EOB ? 0u : tk.val;
+        return false;
+    }
+}
+
+// One round over [rs, E): exact per-lane segments; first_term = first lane ending the block (64:
+// none).  All lanes call.
+__device__ void round_decode(const In& in, const Tabs& t, bool ed, uint64_t rs, uint64_t E, Shared& S, int lane,
+                             Seg& r, uint32_t& first_term, uint32_t& nslow, uint32_t& nfix) {
+    const uint64_t span = E - rs;
+    const uint64_t per = (span + 63) / 64;
+    const uint64_t s = min(rs + (uint64_t)lane * per, E);
+    const uint64_t e = (lane == 63) ? E : min(rs + (uint64_t)(lane + 1) * per, E);
+    const uint64_t C = s + min((uint64_t)XCP, e - s);
+    Spec p0;
+    spec_run(in, t, ed, s, s, C, e, p0);
+    S.exit_[lane] = p0.end;
+    __syncthreads();
+    bool fin;                                   // r is this lane's exact result
+    if (lane == 0) {
+        r.start = s; r.end = p0.end; r.cnt = p0.cnt; r.kind = p0.kind; r.reason = p0.reason;
+        fin = true;
+    } else {
+        fin = verify_run(in, t, ed, S.exit_[lane - 1], s, C, e, p0, S, lane, 1, r);
+    }
+    // exact prefix: lanes before the first unsynchronised lane
+    const uint64_t um = __ballot(!fin);
+    const uint32_t j0 = um ? (uint32_t)__builtin_ctzll(um) : 64u;
+    const uint64_t tm = __ballot(fin && r.kind != T_EXIT);
+    const uint32_t t0 = tm ? (uint32_t)__builtin_ctzll(tm) : 64u;
+    if (j0 >= t0) { first_term = t0; return; }
+    // lane j0 started right (its predecessor is exact) but did not meet its own speculation: its
+    // verify run already decoded the segment.  Lanes after it resolve in order.
+    nslow += (uint32_t)__popcll(um);
+    const uint32_t nph = __popcll(um) > 2 ? NPH : 1u;
+    if (nph > 1 && (uint32_t)lane > j0) {
+        for (uint32_t f = 1; f < NPH; f++) {
+            Spec q;
+            spec_run(in, t, ed, min(s + f, e), s, C, e, q);
+            S.ph_cp[f - 1][lane] = q.cp; S.ph_cpc[f - 1][lane] = q.cpc;
+            S.ph_end[f - 1][lane] = (uint32_t)(q.end - s);
+            S.ph_cnt[f - 1][lane] = (uint32_t)min(q.cnt, (uint64_t)NOCP);
+            S.ph_kr[f - 1][lane] = (q.kind << 16) | q.reason;
+            if (q.end - s >= NOCP || q.cnt >= NOCP) S.ph_cp[f - 1][lane] = NOCP;
+        }
+    }
+    S.exit_[lane] = r.end;
+    S.kind_[lane] = r.kind;
+    __syncthreads();
+    first_term = (r.kind != T_EXIT && (uint32_t)lane == j0) ? j0 : 64u;
+    first_term = __shfl(first_term, (int)j0, 64);
+    for (uint32_t j = j0 + 1; j < 64 && first_term == 64; j++) {
+        nfix++;
+        if ((uint32_t)lane == j) {
+            const uint64_t st = S.exit_[j - 1];
+            if (!(fin && st == r.start)) {
+                verify_run(in, t, ed, st, s, C, e, p0, S, lane, nph, r);
+                S.exit_[lane] = r.end;
+                S.kind_[lane] = r.kind;
+            }
+        }
+        __syncthreads();
+        if (S.kind_[j] != T_EXIT) first_term = j;
+    }
+}
+
+__device__ __forceinline__ uint64_t wave_sum_u64(uint64_t x) {
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) x += __shfl_xor((unsigned long long)x, o, 64);
+    return x;
+}
+__device__ __forceinline__ uint64_t wave_excl_u64(uint64_t v, int lane) {
+    uint64_t x = v;
+#pragma unroll
+    for (int o = 1; o < 64; o <<= 1) {
+        const uint64_t y = __shfl_up((unsigned long long)x, o, 64);
+        if (lane >= o) x += y;
+    }
+    return x - v;
+}
+
+// Next header candidate strictly after b (sorted list), capped at `limit`.
+__device__ __forceinline__ uint64_t next_cand(const uint64_t* cands, uint32_t ncand, uint64_t b, uint64_t limit) {
+    uint32_t lo = 0, hi = ncand;
+    while (lo < hi) { const uint32_t mid = (lo + hi) >> 1; if (cands[mid] <= b) lo = mid + 1; else hi = mid; }
+    const uint64_t nx = lo < ncand ? cands[lo] : NONE;
+    return min(nx, limit);
+}
+
+// ---- emit: write pass of one lane ---------------------------------------------------------------
+struct WLane {
+    Rp rd;
+    uint64_t dst0, n, cnt, end;
+    uint32_t cp_len, cp_dist, lastb, wc, wcn;
+    uint32_t kind, reason;      // final state (T_ERR also for COPY_BEFORE found here)
+    bool active, tainted;
+};
+
+__device__ __forceinline__ void wputb(WLane& L, uint8_t* out, uint64_t P, uint32_t b) {
+    if (L.wcn == 0 && (P & 3)) { out[P] = (uint8_t)b; return; }
+    L.wc |= b << (8 * (uint32_t)(P & 3));
+    L.wcn++;
+    if ((P & 3) == 3) { *(uint32_t*)(out + P - 3) = L.wc; L.wc = 0; L.wcn = 0; }
+}
+__device__ __forceinline__ void wflush(WLane& L, uint8_t* out, uint64_t Pnext) {
+    for (uint32_t k = 0; k < L.wcn; k++) out[Pnext - L.wcn + k] = (uint8_t)(L.wc >> (8 * k));
+    L.wc = 0; L.wcn = 0;
+}
+__device__ __forceinline__ void wcopy(WLane& L, uint8_t* out, uint64_t dst, uint64_t src, uint32_t len, uint32_t dist) {
+    if (dist == 1) {
+        const uint32_t v = (L.n > 0) ? L.lastb : (uint32_t)out[src];
+        uint32_t k = 0;
+        for (; k < len && (L.wcn > 0 || ((dst + k) & 3)); k++) wputb(L, out, dst + k, v);
+        const uint32_t v4 = v * 0x01010101u;
+        for (; k + 4 <= len; k += 4) *(uint32_t*)(out + dst + k) = v4;
+        for (; k < len; k++) wputb(L, out, dst + k, v);
+        L.lastb = v;
+        return;
+    }
+    uint32_t b = L.lastb;
+    if (dist < 4) {
+        wflush(L, out, dst);
+        for (uint32_t k = 0; k < len; k++) { b = out[src + k]; out[dst + k] = (uint8_t)b; }
+    } else {
+        for (uint32_t k = 0; k < len; k++) { b = out[src + k]; wputb(L, out, dst + k, b); }
+    }
+    L.lastb = b;
+}
+
+}  // namespace wv
+
+// Count pass: one wave per candidate chain.
+extern "C" __global__ void __launch_bounds__(64)
+ndfl_inflate_count_wave_kernel(const uint32_t* w, uint64_t nwords, uint64_t nbits, const uint64_t* starts,
+                               const uint64_t* stops, uint32_t nchains, const uint64_t* cands, uint32_t ncand,
+                               uint64_t limit, ChainRes* res, uint32_t* stats, uint64_t slot_base, uint64_t nslot,
+                               uint64_t* seg_start, uint32_t* seg_cnt, SegMeta* seg_meta) {
+    using namespace wv;
+    __shared__ Shared S;
+    const int lane = threadIdx.x;
+    const uint32_t c = blockIdx.x;
+    if (c >= nchains) return;
+    const In in{w, nwords, nbits};
+    const uint64_t start = starts[c], stop = stops[c];
+    uint64_t cur = start, total = 0, endpos = start;
+    uint32_t status = ST_BOUNDARY, reason = 0, nslow = 0, nfix = 0, nround = 0;
+    for (int blk = 0;; blk++) {
+        if (blk > 0 && cur >= stop) { status = ST_BOUNDARY; endpos = cur; break; }
+        for (uint32_t s = (uint32_t)lane; s < 320; s += 64) S.lens[s] = 0;
+        __syncthreads();
+        if (lane == 0) parse_hdr(in, cur, S);
+        __syncthreads();
+        if (S.h_err) { status = ST_ERROR; reason = S.h_err; endpos = S.h_pos; break; }
+        const uint64_t d0 = S.h_d0;
+        const bool bfinal = S.h_bfinal != 0;
+        if (S.h_btype == 0) {
+            const uint64_t avail = (nbits - d0) / 8, ln = S.h_len;
+            if (avail < ln) { total += avail; status = ST_ERROR; reason = R_UEOS; endpos = d0 + 8 * avail; break; }
+            total += ln;
+            cur = d0 + 8 * ln;
+            if (bfinal) { status = ST_FINAL; endpos = cur; break; }
+            continue;
+        }
+        bool ed;
+        const int te = build_tables(S, lane, ed);
+        if (te) { status = ST_ERROR; reason = (uint32_t)te; endpos = d0; break; }
+        uint64_t rs = d0;
+        bool block_done = false, chain_done = false;
+        while (!block_done) {
+            uint64_t E = next_cand(cands, ncand, rs, limit);
+            if (E <= rs) E = rs + 1;
+            Seg r;
+            uint32_t ft;
+            round_decode(in, S.t, ed, rs, E, S, lane, r, ft, nslow, nfix);
+            if (blk == 0 && nround == 0 && slot_base + c < nslot) {
+                // record the exact segments for the emit pass
+                const bool live = (uint32_t)lane <= ft;
+                if (__all(!live || r.cnt < 0xFFFFFFFFull)) {
+                    const uint64_t slot = slot_base + c;
+                    seg_start[slot * 64 + lane] = r.start;
+                    seg_cnt[slot * 64 + lane] = (uint32_t)r.cnt;
+                    const int src = ft < 64 ? (int)ft : 63;
+                    const uint64_t fe = __shfl((unsigned long long)r.end, src, 64);
+                    const uint32_t fk = __shfl(r.kind, src, 64), fr = __shfl(r.reason, src, 64);
+                    if (lane == 0) {
+                        SegMeta m;
+                        m.valid = 1; m.ft = ft; m.kind_ft = fk; m.reason_ft = fr;
+                        m.end_ft = fe; m.exit63 = fe;
+                        seg_meta[slot] = m;
+                    }
+                }
+            }
+            nround++;
+            total += wave_sum_u64((uint32_t)lane <= ft ? r.cnt : 0ull);
+            if (ft < 64) {
+                const uint64_t fe = __shfl((unsigned long long)r.end, (int)ft, 64);
+                const uint32_t fk = __shfl(r.kind, (int)ft, 64), fr = __shfl(r.reason, (int)ft, 64);
+                block_done = true;
+                if (fk == T_ERR) { status = ST_ERROR; reason = fr; endpos = fe; chain_done = true; }
+                else {
+                    cur = fe;
+                    if (bfinal) { status = ST_FINAL; endpos = cur; chain_done = true; }
+                }
+            } else {
+                rs = __shfl((unsigned long long)r.end, 63, 64);
+            }
+        }
+        if (chain_done) break;
+    }
+    if (lane == 0) {
+        ChainRes o;
+        o.end_bit = endpos; o.out_count = total; o.status = status; o.reason = reason;
+        res[c] = o;
+        if (stats) { atomicAdd(&stats[0], nslow); atomicAdd(&stats[1], nfix); atomicAdd(&stats[2], nround); }
+    }
+}
+
+// Emit pass: one wave per linked chain, claimed in stream order through `ticket`.
+extern "C" __global__ void __launch_bounds__(64)
+ndfl_inflate_emit_wave_kernel(const uint32_t* w, uint64_t nwords, uint64_t nbits, const EmitChain* chains,
+                              const uint64_t* chain_off, uint32_t nlist, uint32_t* done, uint32_t* ticket,
+                              uint8_t* out, ChainRes* res, const uint64_t* cands, uint32_t ncand, uint64_t dict_len,
+                              uint32_t* taint, const uint32_t* sel, uint64_t nslot, const uint64_t* seg_start,
+                              const uint32_t* seg_cnt, const SegMeta* seg_meta) {
+    using namespace wv;
+    __shared__ Shared S;
+    __shared__ uint32_t s_ticket;
+    const int lane = threadIdx.x;
+    if (lane == 0) s_ticket = atomicAdd(ticket, 1u);
+    __syncthreads();
+    const uint32_t k = s_ticket;
+    if (k >= nlist) return;
+    const uint32_t ci = sel ? sel[k] : k;
+    const In in{w, nwords, nbits};
+    const EmitChain ch = chains[ci];
+    uint64_t cur = ch.start_bit, base = ch.out_off;
+    uint32_t status = ST_BOUNDARY, reason = 0;
+    uint64_t endpos = ch.start_bit;
+    bool tainted = false;
+    uint32_t nslow = 0, nfix = 0;
+    for (int blk = 0;; blk++) {
+        if (blk > 0 && cur == ch.end_bit) { status = ST_BOUNDARY; endpos = cur; break; }
+        for (uint32_t s = (uint32_t)lane; s < 320; s += 64) S.lens[s] = 0;
+        __syncthreads();
+        if (lane == 0) parse_hdr(in, cur, S);
+        __syncthreads();
+        if (S.h_err) { status = ST_ERROR; reason = S.h_err; endpos = S.h_pos; break; }
+        const uint64_t d0 = S.h_d0;
+        const bool bfinal = S.h_bfinal != 0;
+        if (S.h_btype == 0) {
+            const uint64_t avail = (nbits - d0) / 8, ln = S.h_len;
+            const uint64_t take = min(avail, ln);
+            const uint64_t ib = d0 >> 3;
+            for (uint64_t i = (uint64_t)lane; i < take; i += 64) {
+                const uint64_t b = ib + i;
+                out[base + i] = (uint8_t)(in.ld(b >> 2) >> (8 * (uint32_t)(b & 3)));
+            }
+            base += take;
+            __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
+            __syncthreads();
+            __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup");
+            if (take < ln) { status = ST_ERROR; reason = R_UEOS; endpos = d0 + 8 * avail; break; }
+            cur = d0 + 8 * ln;
+            if (bfinal) { status = ST_FINAL; endpos = cur; break; }
+            continue;
+        }
+        bool ed;
+        const int te = build_tables(S, lane, ed);
+        if (te) { status = ST_ERROR; reason = (uint32_t)te; endpos = d0; break; }
+        uint64_t rs = d0;
+        bool block_done = false, chain_done = false;
+        bool first_round = blk == 0;
+        while (!block_done) {
+            Seg r;
+            uint32_t ft;
+            if (first_round && ch.slot < nslot && seg_meta[ch.slot].valid) {
+                // exact segments from the count pass
+                const SegMeta m = seg_meta[ch.slot];
+                ft = m.ft;
+                r.start = seg_start[ch.slot * 64 + lane];
+                r.cnt = seg_cnt[ch.slot * 64 + lane];
+                const uint64_t nx = __shfl_down((unsigned long long)r.start, 1, 64);
+                r.end = lane < 63 ? nx : m.exit63;
+                r.kind = T_EXIT; r.reason = 0;
+                if ((uint32_t)lane == ft) { r.end = m.end_ft; r.kind = m.kind_ft; r.reason = m.reason_ft; }
+            } else {
+                uint64_t E = next_cand(cands, ncand, rs, ch.end_bit);
+                if (E <= rs) E = rs + 1;
+                round_decode(in, S.t, ed, rs, E, S, lane, r, ft, nslow, nfix);
+            }
+            first_round = false;
+            // offsets of this round's lanes
+            const bool live = (uint32_t)lane <= ft;
+            const uint64_t mycnt = live ? r.cnt : 0ull;
+            const uint64_t pre = wave_excl_u64(mycnt, lane);
+            const uint64_t rsum = wave_sum_u64(mycnt);
+            S.off_[lane] = base + pre;
+            S.cnt_[lane] = mycnt;
+            S.prog[lane] = 0;
+            __syncthreads();
+            // write pass (budgeted steps; a lane waiting on another lane or chain skips its turn)
+            WLane L;
+            L.rd.init(in, r.start);
+            L.dst0 = base + pre; L.n = 0; L.cnt = mycnt; L.end = r.end;
+            L.cp_len = 0; L.cp_dist = 0; L.lastb = 0; L.wc = 0; L.wcn = 0;
+            L.kind = r.kind; L.reason = r.reason;
+            L.active = live; L.tainted = false;
+            uint32_t waits = 0;
+            int idle = 0;
+            while (__any(L.active)) {
+                bool waiting = false;
+                if (L.active) {
+                    for (int b = 0; b < BUDGET; b++) {
+                        if (L.cp_len == 0) {
+                            if (L.rd.pos >= L.end && L.kind == T_EXIT) { L.active = false; break; }
+                            Tok tk;
+                            next_tok(L.rd, in, S.t, ed, tk);
+                            if (tk.kind == K_LIT) {
+                                wputb(L, out, L.dst0 + L.n, tk.val);
+                                L.lastb = tk.val;
+                                L.n++;
+                                continue;
+                            }
+                            if (tk.kind != K_LEN) { L.active = false; break; }     // EOB or error (as verified)
+                            if ((uint64_t)tk.dist > L.dst0 + L.n) {
+                                L.kind = T_ERR; L.reason = R_COPY_BEFORE; L.end = L.rd.pos; L.active = false; break;
+                            }
+                            L.cp_len = tk.val; L.cp_dist = tk.dist;
+                        }
+                        const uint64_t dst = L.dst0 + L.n;
+                        const uint64_t src = dst - L.cp_dist;
+                        if (src < L.dst0 && !(L.cp_dist == 1 && L.n > 0)) {
+                            const uint64_t src_end = min(dst, src + L.cp_len);
+                            if (src < dict_len) L.tainted = true;
+                            bool ok = true;
+                            // bytes of earlier lanes of this round
+                            if (src_end > S.off_[0]) {
+                                for (int j = lane - 1; j >= 0; j--) {
+                                    const uint64_t o = S.off_[j];
+                                    if (o + S.cnt_[j] <= src) break;
+                                    const uint64_t need = min(o + S.cnt_[j], src_end) - max(o, src);
+                                    const uint64_t have = S.prog[j];
+                                    if (max(o, src) + need > o + have) { ok = false; break; }
+                                    if (o <= src) break;
+                                }
+                            }
+                            // bytes of earlier chains
+                            if (ok && src < ch.out_off && src_end > dict_len) {
+                                const uint64_t s0 = max(src, dict_len);
+                                const uint64_t se = min(src_end, ch.out_off);
+                                uint32_t lo = 0, hi = ci;
+                                while (lo + 1 < hi) {
+                                    const uint32_t mid = (lo + hi) >> 1;
+                                    if (chain_off[mid] <= s0) lo = mid; else hi = mid;
+                                }
+                                uint32_t need_hi = lo;
+                                while (need_hi + 1 < ci && chain_off[need_hi + 1] < se) need_hi++;
+                                for (uint32_t j = lo; j <= need_hi && ok; j++)
+                                    if (__hip_atomic_load(&done[j], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == 0) ok = false;
+                                if (ok && taint)
+                                    for (uint32_t j = lo; j <= need_hi; j++) L.tainted |= taint[j] != 0;
+                            }
+                            if (!ok) { waiting = true; break; }
+                            __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+                        }
+                        wcopy(L, out, dst, src, L.cp_len, L.cp_dist);
+                        L.n += L.cp_len;
+                        L.cp_len = 0;
+                    }
+                    if (!L.active) wflush(L, out, L.dst0 + L.n);
+                    if (waiting && ++waits > (1u << 24)) {          // safety net: never hang the device
+                        L.active = false; L.kind = T_ERR; L.reason = R_INTERNAL;
+                    }
+                }
+                __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
+                // a lane that stopped on an error releases its waiters: what follows an error is
+                // never reported, so they may read anything
+                S.prog[lane] = (!L.active && L.kind == T_ERR) ? 0xFFFFFFFFu
+                                                              : (uint32_t)min(L.n - L.wcn, (uint64_t)0xFFFFFFFFu);
+                __syncthreads();
+                if (__all(!L.active || waiting)) { if (++idle > 2) __builtin_amdgcn_s_sleep(2); }
+                else idle = 0;
+            }
+            __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
+            __syncthreads();
+            __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup");
+            tainted |= __any(L.tainted);
+            // the first lane (in stream order) that ended with an error decides
+            const uint64_t em = __ballot(live && L.kind == T_ERR);
+            if (em) {
+                const int fl = (int)__builtin_ctzll(em);
+                status = ST_ERROR;
+                reason = __shfl(L.reason, fl, 64);
+                endpos = __shfl((unsigned long long)L.end, fl, 64);
+                base = __shfl((unsigned long long)(L.dst0 + L.n), fl, 64);
+                chain_done = true;
+                break;
+            }
+            base += rsum;
+            if (ft < 64) {
+                block_done = true;
+                cur = __shfl((unsigned long long)r.end, (int)ft, 64);
+                if (bfinal) { status = ST_FINAL; endpos = cur; chain_done = true; }
+            } else {
+                rs = __shfl((unsigned long long)r.end, 63, 64);
+            }
+        }
+        if (chain_done) break;
+    }
+    // publish: output complete -> done flag (release, agent scope)
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __syncthreads();
+    if (lane == 0) {
+        if (taint) taint[ci] = tainted ? 1u : 0u;
+        ChainRes o;
+        o.end_bit = endpos; o.out_count = base - ch.out_off; o.status = status; o.reason = reason;
+        res[ci] = o;
+        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
+        __hip_atomic_store(&done[ci], 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    }
+}
