@@ -299,16 +299,24 @@ __device__ bool strict_stored(const In& in, uint64_t p) {
 
 }  // namespace inf
 
-// Header finder over every bit position.  Each thread tests 32 consecutive positions: btype masks
-// for all 32 come from two shifts of a 64-bit window; the per-position tests read a 128-bit
-// funnel-shifted window with compile-time offsets only (no private arrays).  Survivors are
-// gathered per workgroup in LDS and strictly validated one per lane, then appended to their
-// 64 KiB segment's list.
+// Header finder over every bit position, stage 1 (quick filter).  Each thread tests 32 consecutive
+// positions: btype masks for all 32 come from two shifts of a 64-bit window.  Dynamic headers need
+// a complete code-length code (Kraft sum exactly 1 over the HCLEN+4 3-bit lengths, >= 2 codes):
+// the 19 lengths are read as six 9-bit groups + one, each group's Kraft sum and nonzero count
+// from a 512-entry LDS table.  Stored headers need zero padding and LEN == ~NLEN.  Survivors
+// (about 1 in 1000 positions) go to a global list for the strict stage.
 extern "C" __global__ void __launch_bounds__(256)
-ndfl_inflate_find_kernel(const uint32_t* w, uint64_t nwords, uint64_t nbits, uint32_t* seg_cnt, uint64_t* seg_list) {
+ndfl_inflate_find_kernel(const uint32_t* w, uint64_t nwords, uint64_t nbits, uint64_t* qlist, uint32_t* qcount,
+                         uint32_t qcap) {
     using namespace inf;
+    __shared__ uint32_t lut[512];            // kraft (x128) | nonzero count << 16 for 3 lengths
     __shared__ uint64_t cand[1024];
-    __shared__ uint32_t ncand;
+    __shared__ uint32_t ncand, gbase;
+    for (uint32_t v = threadIdx.x; v < 512; v += 256) {
+        uint32_t k = 0, nz = 0;
+        for (int f = 0; f < 3; f++) { const uint32_t l = (v >> (3 * f)) & 7u; if (l) { k += 128u >> l; nz++; } }
+        lut[v] = k | (nz << 16);
+    }
     if (threadIdx.x == 0) ncand = 0;
     __syncthreads();
     const uint64_t t = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
@@ -323,28 +331,26 @@ ndfl_inflate_find_kernel(const uint32_t* w, uint64_t nwords, uint64_t nbits, uin
         uint32_t m2 = ~b1 & b2 & valid;
         uint32_t m0 = ~b1 & ~b2 & valid;
         const uint64_t lo = W, hi = (uint64_t)w2 | ((uint64_t)w3 << 32);
+        const uint64_t hw = (uint64_t)w3 | ((uint64_t)w4 << 32);
         while (m2) {
             const uint32_t o = __builtin_ctz(m2);
             m2 &= m2 - 1;
             // 96 bits starting at position o: x0 = bits [o, o+64), x1 = bits [o+64, o+96)
             const uint64_t x0 = o ? (lo >> o) | (hi << (64 - o)) : lo;
-            const uint64_t hw = (uint64_t)w3 | ((uint64_t)w4 << 32);
             const uint32_t x1 = (uint32_t)((o ? (hi >> o) | (hw << (64 - o)) : hi));
-            const uint32_t ncl = (uint32_t)(x0 >> 13) & 15u;
-            // 19 x 3-bit lengths at offsets 17..73 (relative to o)
-            uint32_t kr = 0, nz = 0;
+            const uint32_t nf3 = 3 * (((uint32_t)(x0 >> 13) & 15u) + 4);      // bits of lengths present
+            uint32_t acc = 0;
 #pragma unroll
-            for (int i = 0; i < 19; i++) {
-                const int off = 17 + 3 * i;
-                uint32_t l;
-                if (off + 3 <= 64) l = (uint32_t)(x0 >> off) & 7u;
-                else if (off >= 64) l = (x1 >> (off - 64)) & 7u;
-                else l = (uint32_t)((x0 >> off) | ((uint64_t)x1 << (64 - off))) & 7u;
-                const bool in_range = (uint32_t)i < ncl + 4;
-                kr += (in_range && l) ? (128u >> l) : 0u;
-                nz += in_range && l;
+            for (int k = 0; k < 6; k++) {
+                const int off = 17 + 9 * k;
+                const uint32_t g = (off + 9 <= 64) ? (uint32_t)(x0 >> off) & 0x1FFu
+                                                   : ((uint32_t)(x0 >> off) | (x1 << (64 - off))) & 0x1FFu;
+                const int vb = (int)nf3 - 9 * k;
+                const uint32_t mask = vb >= 9 ? 0x1FFu : vb <= 0 ? 0u : (1u << vb) - 1u;
+                acc += lut[g & mask];
             }
-            if (kr == 128 && nz >= 2 && p0 + o + 17 + 3 * (ncl + 4) <= nbits) {
+            if (nf3 == 57) acc += lut[(x1 >> 7) & 7u];
+            if ((acc & 0xFFFFu) == 128u && (acc >> 16) >= 2u && p0 + o + 17 + nf3 <= nbits) {
                 uint32_t k = atomicAdd(&ncand, 1u);
                 if (k < 1024) cand[k] = (p0 + o) | (1ull << 63);
             }
@@ -365,8 +371,22 @@ ndfl_inflate_find_kernel(const uint32_t* w, uint64_t nwords, uint64_t nbits, uin
     }
     __syncthreads();
     const uint32_t nc = min(ncand, 1024u);
-    for (uint32_t k = threadIdx.x; k < nc; k += blockDim.x) {
-        const uint64_t e = cand[k];
+    if (threadIdx.x == 0) gbase = nc ? atomicAdd(qcount, nc) : 0u;
+    __syncthreads();
+    for (uint32_t k = threadIdx.x; k < nc; k += blockDim.x)
+        if (gbase + k < qcap) qlist[gbase + k] = cand[k];
+}
+
+// Stage 2: the reference's own header checks on every survivor, one lane each (grid-stride);
+// accepted headers go to their 64 KiB segment's list.
+extern "C" __global__ void __launch_bounds__(256)
+ndfl_inflate_strict_kernel(const uint32_t* w, uint64_t nwords, uint64_t nbits, const uint64_t* qlist,
+                           const uint32_t* qcount, uint32_t qcap, uint32_t* seg_cnt, uint64_t* seg_list) {
+    using namespace inf;
+    const uint32_t n = min(*qcount, qcap);
+    In in{w, nwords, nbits};
+    for (uint32_t k = blockIdx.x * blockDim.x + threadIdx.x; k < n; k += gridDim.x * blockDim.x) {
+        const uint64_t e = qlist[k];
         const uint64_t p = e & ~(1ull << 63);
         const bool ok = (e >> 63) ? strict_dynamic(in, p) : strict_stored(in, p);
         if (ok) {
@@ -429,6 +449,7 @@ struct InflateScratch {
     void* d_res = nullptr; size_t d_res_cap = 0;
     void* d_cands = nullptr; size_t d_cands_cap = 0;
     void* d_stats = nullptr;
+    void* d_q = nullptr; size_t d_q_cap = 0;           // finder survivors (stage 1 -> stage 2)
     void* d_seg = nullptr; size_t d_seg_cap = 0;      // [slots][64] u64 starts, [slots][64] u32 counts, [slots] SegMeta
     uint64_t seg_slots = 0;
     void* d_chains = nullptr; size_t d_chains_cap = 0;
@@ -449,11 +470,11 @@ struct InflateScratch {
     uint8_t* p_out = nullptr;
     uint32_t p_nch = 0, p_ncand = 0;
     void release() {
-        void** ps[] = {&d_in, &d_cand, &d_starts, &d_stops, &d_res, &d_cands, &d_stats, &d_seg, &d_chains, &d_off,
+        void** ps[] = {&d_in, &d_cand, &d_starts, &d_stops, &d_res, &d_cands, &d_stats, &d_q, &d_seg, &d_chains, &d_off,
                        &d_done, &d_taint, &d_sel, &d_ticket, &d_out};
         for (void** p : ps) { if (*p) hipFree(*p); *p = nullptr; }
         for (auto& e : ev) { if (e) hipEventDestroy(e); e = nullptr; }
-        d_in_cap = d_cand_cap = d_starts_cap = d_stops_cap = d_res_cap = d_cands_cap = d_seg_cap = d_chains_cap = 0;
+        d_in_cap = d_cand_cap = d_starts_cap = d_stops_cap = d_res_cap = d_cands_cap = d_seg_cap = d_q_cap = d_chains_cap = 0;
         d_off_cap = d_done_cap = d_taint_cap = d_sel_cap = d_out_cap = 0;
         pending = false;
     }
@@ -493,6 +514,7 @@ static int inflate_run(InflateScratch& S, hipStream_t s, const uint8_t* in, uint
     INF_CHK(hipMemsetAsync((char*)S.d_in + in_len, 0, nwords * 4 + IN_PAD - in_len, s));
     const uint32_t* d_w = (const uint32_t*)S.d_in;
     if (!S.d_stats) INF_CHK(hipMalloc(&S.d_stats, 64));
+    INF_CHK(hipMemsetAsync(S.d_stats, 0, 64, s));
     if (!S.ev[0]) for (auto& e : S.ev) INF_CHK(hipEventCreate(&e));
     const uint32_t nseg = (uint32_t)std::max<uint64_t>(1, (in_len + SEG_BYTES - 1) / SEG_BYTES);
     INF_CHK(inf_ensure(&S.d_cand, &S.d_cand_cap, (uint64_t)nseg * SEG_CAP * 8ull + (uint64_t)nseg * 4 + 64));
@@ -502,11 +524,18 @@ static int inflate_run(InflateScratch& S, hipStream_t s, const uint8_t* in, uint
     INF_CHK(hipEventRecord(S.ev[0], s));
     {
         const uint64_t nthr = (nbits + 31) / 32;
-        INF_CHK(inf_ensure(&S.d_starts, &S.d_starts_cap, 64));
-        if (nthr)
+        const uint32_t qcap = (uint32_t)std::min<uint64_t>(0x7FFFFFFFull, nbits / 256 + 65536);
+        INF_CHK(inf_ensure(&S.d_q, &S.d_q_cap, (uint64_t)qcap * 8 + 64));
+        uint32_t* d_qcount = (uint32_t*)S.d_stats + 8;
+        uint64_t* d_qlist = (uint64_t*)((char*)S.d_q + 64);
+        if (nthr) {
             hipLaunchKernelGGL(ndfl_inflate_find_kernel, dim3((uint32_t)((nthr + 255) / 256)), dim3(256), 0, s, d_w,
-                               nwords, nbits, d_cnt, d_list);
-        INF_CHK(hipGetLastError());
+                               nwords, nbits, d_qlist, d_qcount, qcap);
+            INF_CHK(hipGetLastError());
+            hipLaunchKernelGGL(ndfl_inflate_strict_kernel, dim3(2048), dim3(256), 0, s, d_w, nwords, nbits,
+                               (const uint64_t*)d_qlist, (const uint32_t*)d_qcount, qcap, d_cnt, d_list);
+            INF_CHK(hipGetLastError());
+        }
     }
     INF_CHK(hipEventRecord(S.ev[1], s));
     std::vector<uint32_t> hcnt(nseg);
@@ -539,7 +568,6 @@ static int inflate_run(InflateScratch& S, hipStream_t s, const uint8_t* in, uint
     const uint32_t ncand = (uint32_t)sorted_cand.size();
     INF_CHK(inf_ensure(&S.d_cands, &S.d_cands_cap, (ncand + 1) * 8ull));
     INF_CHK(hipMemcpyAsync(S.d_cands, sorted_cand.data(), ncand * 8ull, hipMemcpyHostToDevice, s));
-    INF_CHK(hipMemsetAsync(S.d_stats, 0, 64, s));
     const uint64_t limit = std::min(end_bit, nbits);
     // segment records: one slot per counted chain start (index in `starts`), with room for repairs
     const uint64_t nslot = starts.size() + std::max<uint64_t>(4096, starts.size() / 2);
@@ -650,10 +678,12 @@ static int inflate_run(InflateScratch& S, hipStream_t s, const uint8_t* in, uint
     S.chains = chains.size();
     S.candidates = sorted_cand.size();
     if (getenv("NDFL_STATS")) {
-        uint32_t st[4] = {0, 0, 0, 0};
-        INF_CHK(hipMemcpy(st, S.d_stats, 16, hipMemcpyDeviceToHost));
-        fprintf(stderr, "[ndfl] count pass: chains %zu candidates %zu repairs %llu slow-verify lanes %u fixups %u rounds %u\n",
-                chains.size(), sorted_cand.size(), (unsigned long long)S.repairs, st[0], st[1], st[2]);
+        uint32_t st[16] = {0};
+        INF_CHK(hipMemcpy(st, S.d_stats, 64, hipMemcpyDeviceToHost));
+        st[4] = st[8];
+        fprintf(stderr, "[ndfl] finder quick survivors %u; count pass: chains %zu candidates %zu repairs %llu "
+                "slow-verify lanes %u fixups %u rounds %u\n", st[4], chains.size(), sorted_cand.size(),
+                (unsigned long long)S.repairs, st[0], st[1], st[2]);
     }
     const uint64_t total = off - dict_len;
     if (total > out_cap) { *out_len = total; return -3; }

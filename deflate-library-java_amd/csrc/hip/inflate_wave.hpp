@@ -80,7 +80,7 @@ __device__ __forceinline__ uint32_t dist_entry(uint32_t sym, uint32_t len) {
     return len | (K_BAD << 9);
 }
 
-__device__ __noinline__ uint32_t slow_lit(uint32_t p15, const Tabs& t) {
+__device__ __forceinline__ uint32_t slow_lit(uint32_t p15, const Tabs& t) {
     const uint32_t r15 = rev_bits(p15, 15);
     for (uint32_t l = LB + 1; l < 16; l++) {
         const uint32_t idx = (r15 >> (15 - l)) - t.lfirst[l];
@@ -88,7 +88,7 @@ __device__ __noinline__ uint32_t slow_lit(uint32_t p15, const Tabs& t) {
     }
     return 15u | (K_BAD << 9);              // unreachable: codes are complete
 }
-__device__ __noinline__ uint32_t slow_dist(uint32_t p15, const Tabs& t) {
+__device__ __forceinline__ uint32_t slow_dist(uint32_t p15, const Tabs& t) {
     const uint32_t r15 = rev_bits(p15, 15);
     for (uint32_t l = DB + 1; l < 16; l++) {
         const uint32_t idx = (r15 >> (15 - l)) - t.dfirst[l];
@@ -102,28 +102,81 @@ struct Tok {
     uint32_t val, dist;
 };
 
+// Round-relative bit reader: positions are 32-bit offsets from a 128-bit-aligned round base, so
+// the per-token arithmetic is 32-bit.  64-bit active buffer refilled 32 bits at a time; the next two
+// 16-byte groups are always in flight (unconditional loads from the zero-padded input).
+struct RB {
+    const u32x4* gp;      // group 0 = round base
+    uint32_t gmax;        // last readable group (relative; clamped into the padding)
+    uint32_t nb;          // input bits relative to the base (saturated)
+    uint64_t base;        // absolute bit of the base
+};
+__device__ __forceinline__ RB make_rb(const In& in, uint64_t rs) {
+    RB b;
+    b.base = rs & ~127ull;
+    b.gp = (const u32x4*)in.w + (b.base >> 7);
+    b.gmax = (uint32_t)((in.nwords + 3) / 4 + 1 - (b.base >> 7));
+    b.nb = (uint32_t)min(in.nbits - min(in.nbits, b.base), (uint64_t)0xFFFFFFFFu);
+    return b;
+}
+struct Rq {
+    uint64_t bb;
+    uint32_t bn, ci, qw, pos;
+    u32x4 cur, nxt, nx2;
+    __device__ __forceinline__ static uint32_t pick(const u32x4& v, uint32_t i) {
+        uint32_t a = (i & 1) ? v.y : v.x, b = (i & 1) ? v.w : v.z;
+        return (i & 2) ? b : a;
+    }
+    __device__ __forceinline__ void adv(const RB& b) {
+        if (++ci == 4) { cur = nxt; nxt = nx2; qw++; nx2 = b.gp[min(qw + 2, b.gmax)]; ci = 0; }
+    }
+    __device__ __forceinline__ void init(const RB& b, uint32_t p) {
+        pos = p;
+        qw = p >> 7;
+        cur = b.gp[min(qw, b.gmax)];
+        nxt = b.gp[min(qw + 1, b.gmax)];
+        nx2 = b.gp[min(qw + 2, b.gmax)];
+        ci = (p >> 5) & 3;
+        bb = (uint64_t)(pick(cur, ci) >> (p & 31));
+        bn = 32 - (p & 31);
+        adv(b);
+        fill(b);
+    }
+    __device__ __forceinline__ void fill(const RB& b) {
+        if (bn <= 32) { bb |= (uint64_t)pick(cur, ci) << bn; bn += 32; adv(b); }
+    }
+    __device__ __forceinline__ uint32_t peek(uint32_t n) const { return (uint32_t)bb & ((1u << n) - 1u); }
+    __device__ __forceinline__ void skip(uint32_t n) { bb >>= n; bn -= n; pos += n; }
+    __device__ __forceinline__ uint32_t get(const RB& b, uint32_t n) {
+        fill(b);
+        const uint32_t v = peek(n);
+        skip(n);
+        return v;
+    }
+};
+
 // One token of a Huffman block, with the reference's check order (D/decomp/Open.java:446-618).
-__device__ __forceinline__ void next_tok(Rp& rd, const In& in, const Tabs& t, bool empty_dist, Tok& tk) {
-    rd.fill(in);
+__device__ __forceinline__ void next_tok(Rq& rd, const RB& b, const Tabs& t, bool empty_dist, Tok& tk) {
+    rd.fill(b);
     uint32_t e = t.lit[rd.peek(LB)];
     if (!(e & 31)) e = slow_lit(rd.peek(15), t);
     rd.skip(e & 31);
-    if (rd.pos > in.nbits) { tk.kind = K_BAD; tk.val = R_UEOS; return; }
+    if (rd.pos > b.nb) { tk.kind = K_BAD; tk.val = R_UEOS; return; }
     const uint32_t k = (e >> 9) & 3;
     if (k == K_LIT) { tk.kind = K_LIT; tk.val = e >> 16; return; }
     if (k == K_EOB) { tk.kind = K_EOB; return; }
     if (k == K_BAD) { tk.kind = K_BAD; tk.val = R_RESERVED_LEN; return; }
-    const uint32_t run = (e >> 16) + rd.get(in, (e >> 5) & 15);
-    if (rd.pos > in.nbits) { tk.kind = K_BAD; tk.val = R_UEOS; return; }
+    const uint32_t run = (e >> 16) + rd.get(b, (e >> 5) & 15);
+    if (rd.pos > b.nb) { tk.kind = K_BAD; tk.val = R_UEOS; return; }
     if (empty_dist) { tk.kind = K_BAD; tk.val = R_EMPTY_DIST; return; }
-    rd.fill(in);
+    rd.fill(b);
     uint32_t d = t.dst[rd.peek(DB)];
     if (!(d & 31)) d = slow_dist(rd.peek(15), t);
     rd.skip(d & 31);
-    if (rd.pos > in.nbits) { tk.kind = K_BAD; tk.val = R_UEOS; return; }
+    if (rd.pos > b.nb) { tk.kind = K_BAD; tk.val = R_UEOS; return; }
     if (((d >> 9) & 3) == K_BAD) { tk.kind = K_BAD; tk.val = R_RESERVED_DIST; return; }
-    const uint32_t dist = (d >> 16) + rd.get(in, (d >> 5) & 15);
-    if (rd.pos > in.nbits) { tk.kind = K_BAD; tk.val = R_UEOS; return; }
+    const uint32_t dist = (d >> 16) + rd.get(b, (d >> 5) & 15);
+    if (rd.pos > b.nb) { tk.kind = K_BAD; tk.val = R_UEOS; return; }
     tk.kind = K_LEN; tk.val = run; tk.dist = dist;
 }
 
@@ -296,64 +349,71 @@ __device__ int build_tables(Shared& S, int lane, bool& empty_dist) {
 }
 
 // ---- segmented speculative decode of one round ------------------------------------------------
-// Lane j owns [s_j, e_j) and a checkpoint C_j = s_j + min(XCP, e_j - s_j).  A speculative run from
-// a start records (cp, cpc): its first token boundary >= C_j (offset from s_j) and the output bytes
-// before it, plus its end state.  Two decodes that stand on the same boundary at the checkpoint
-// agree from there on, so a verify run from the TRUE start only decodes up to C_j and, on a match,
-// takes the speculative end state.  Codes whose lengths are all multiples of 8 never resynchronise
-// from a wrong bit phase; for them the fallback adds runs from s_j+1 .. s_j+7 (one per phase).
-constexpr uint32_t XCP = 128;
+// Lane j owns [s_j, e_j) (round-relative bits) and checkpoints C1_j = s_j + min(128, len) and
+// C2_j = s_j + min(1024, len).  A speculative run from a start records, per checkpoint, its first
+// token boundary at or past it (offset from s_j) and the output bytes before it, plus its end
+// state.  Two decodes that stand on the same boundary at a checkpoint agree from there on, so a
+// verify run from the TRUE start only decodes up to the first checkpoint where it meets its own
+// speculation and then takes the speculative end state.  Codes whose lengths are (nearly) all
+// multiples of 8 resynchronise slowly or never from a wrong bit phase; when several lanes fail the
+// fallback adds runs from s_j+1 .. s_j+7 (one per phase) compared at C1.
+constexpr uint32_t XCP1 = 128, XCP2 = 1024;
 constexpr uint32_t NPH = 8;
 constexpr uint32_t NOCP = 0xFFFFFFFFu;
+constexpr uint64_t MAX_SPAN = 1ull << 29;    // round span cap: 32-bit positions and counts
 
 struct Seg {
-    uint64_t start, end, cnt;
+    uint64_t start, end, cnt;                // absolute bits
     uint32_t kind, reason;
 };
+struct SegR {
+    uint32_t start, end, cnt, kind, reason;  // round-relative
+};
 struct Spec {
-    uint64_t end, cnt;
-    uint32_t kind, reason, cp, cpc;
+    uint32_t end, cnt, kind, reason;
+    uint32_t cp1, cpc1, cp2, cpc2;
 };
 
-__device__ void spec_run(const In& in, const Tabs& t, bool ed, uint64_t st, uint64_t s, uint64_t C, uint64_t e,
-                         Spec& o) {
-    Rp rd;
-    rd.init(in, st);
-    uint64_t cnt = 0;
-    uint32_t kind = T_EXIT, reason = 0, cp = NOCP, cpc = 0;
+__device__ void spec_run(const RB& b, const Tabs& t, bool ed, uint32_t st, uint32_t s, uint32_t C1, uint32_t C2,
+                         uint32_t e, Spec& o) {
+    Rq rd;
+    rd.init(b, st);
+    uint32_t cnt = 0, kind = T_EXIT, reason = 0;
+    o.cp1 = NOCP; o.cp2 = NOCP; o.cpc1 = 0; o.cpc2 = 0;
     Tok tk;
     for (;;) {
-        if (cp == NOCP && rd.pos >= C) { cp = (uint32_t)(rd.pos - s); cpc = (uint32_t)min(cnt, (uint64_t)NOCP); }
+        if (o.cp2 == NOCP && rd.pos >= C1) {
+            if (o.cp1 == NOCP) { o.cp1 = rd.pos - s; o.cpc1 = cnt; }
+            if (rd.pos >= C2) { o.cp2 = rd.pos - s; o.cpc2 = cnt; }
+        }
         if (rd.pos >= e) break;
-        next_tok(rd, in, t, ed, tk);
+        next_tok(rd, b, t, ed, tk);
         if (tk.kind == K_LIT) { cnt++; continue; }
         if (tk.kind == K_LEN) { cnt += tk.val; continue; }
         kind = tk.kind == K_EOB ? T_EOB : T_ERR;
         reason = tk.kind == K_EOB ? 0u : tk.val;
         break;
     }
-    if (cnt >= NOCP) cp = NOCP;                 // counts kept in 32 bits: no sync through this run
-    o.end = rd.pos; o.cnt = cnt; o.kind = kind; o.reason = reason; o.cp = cp; o.cpc = cpc;
+    o.end = rd.pos; o.cnt = cnt; o.kind = kind; o.reason = reason;
 }
 
-// Decode from the true start t0 to the checkpoint; on a match with phase 0 (registers) or, when
-// `nph` > 1, phases 1..nph-1 (LDS), take that run's end state; otherwise decode the rest of the
-// segment (authoritative).  Returns true when it synchronised.
-__device__ bool verify_run(const In& in, const Tabs& t, bool ed, uint64_t t0, uint64_t s, uint64_t C, uint64_t e,
-                           const Spec& p0, const Shared& S, int lane, uint32_t nph, Seg& r) {
-    Rp rd;
-    rd.init(in, t0);
-    uint64_t c = 0;
+// Decode from the true start t0; at C1 compare with phase 0 (registers) and, when nph > 1, phases
+// 1..nph-1 (LDS); at C2 with phase 0 again; on a match take that run's end state, otherwise
+// decode the rest of the segment (authoritative).  Returns true when it synchronised.
+__device__ bool verify_run(const RB& b, const Tabs& t, bool ed, uint32_t t0, uint32_t s, uint32_t C1, uint32_t C2,
+                           uint32_t e, const Spec& p0, const Shared& S, int lane, uint32_t nph, SegR& r) {
+    Rq rd;
+    rd.init(b, t0);
+    uint32_t c = 0, stage = 0;
     Tok tk;
     r.start = t0;
-    bool at_cp = false;
     for (;;) {
-        const uint64_t q = rd.pos;
-        if (!at_cp && q >= C) {
-            at_cp = true;
-            const uint32_t off = (uint32_t)(q - s);
-            if (p0.cp == off) {
-                r.end = p0.end; r.cnt = c + (p0.cnt - p0.cpc); r.kind = p0.kind; r.reason = p0.reason;
+        const uint32_t q = rd.pos;
+        if (stage == 0 && q >= C1) {
+            stage = 1;
+            const uint32_t off = q - s;
+            if (p0.cp1 == off) {
+                r.end = p0.end; r.cnt = c + (p0.cnt - p0.cpc1); r.kind = p0.kind; r.reason = p0.reason;
                 return true;
             }
             for (uint32_t f = 1; f < nph; f++) {
@@ -366,8 +426,15 @@ __device__ bool verify_run(const In& in, const Tabs& t, bool ed, uint64_t t0, ui
                 }
             }
         }
+        if (stage == 1 && q >= C2) {
+            stage = 2;
+            if (p0.cp2 == q - s) {
+                r.end = p0.end; r.cnt = c + (p0.cnt - p0.cpc2); r.kind = p0.kind; r.reason = p0.reason;
+                return true;
+            }
+        }
         if (q >= e) { r.end = q; r.cnt = c; r.kind = T_EXIT; r.reason = 0; return false; }
-        next_tok(rd, in, t, ed, tk);
+        next_tok(rd, b, t, ed, tk);
         if (tk.kind == K_LIT) { c++; continue; }
         if (tk.kind == K_LEN) { c += tk.val; continue; }
         r.end = rd.pos; r.cnt = c;
@@ -377,65 +444,72 @@ __device__ bool verify_run(const In& in, const Tabs& t, bool ed, uint64_t t0, ui
     }
 }
 
-// One round over [rs, E): exact per-lane segments; first_term = first lane ending the block (64:
-// none).  All lanes call.
+// One round over [rs, E) (E - rs <= MAX_SPAN): exact per-lane segments; first_term = first lane
+// ending the block (64: none).  All lanes call.
 __device__ void round_decode(const In& in, const Tabs& t, bool ed, uint64_t rs, uint64_t E, Shared& S, int lane,
-                             Seg& r, uint32_t& first_term, uint32_t& nslow, uint32_t& nfix) {
-    const uint64_t span = E - rs;
-    const uint64_t per = (span + 63) / 64;
-    const uint64_t s = min(rs + (uint64_t)lane * per, E);
-    const uint64_t e = (lane == 63) ? E : min(rs + (uint64_t)(lane + 1) * per, E);
-    const uint64_t C = s + min((uint64_t)XCP, e - s);
+                             Seg& out, uint32_t& first_term, uint32_t& nslow, uint32_t& nfix) {
+    const RB b = make_rb(in, rs);
+    const uint32_t r0 = (uint32_t)(rs - b.base), re = (uint32_t)(E - b.base);
+    const uint32_t span = re - r0;
+    const uint32_t per = (span + 63) / 64;
+    const uint32_t s = min(r0 + (uint32_t)lane * per, re);
+    const uint32_t e = (lane == 63) ? re : min(r0 + (uint32_t)(lane + 1) * per, re);
+    const uint32_t C1 = s + min(XCP1, e - s), C2 = s + min(XCP2, e - s);
     Spec p0;
-    spec_run(in, t, ed, s, s, C, e, p0);
+    spec_run(b, t, ed, s, s, C1, C2, e, p0);
     S.exit_[lane] = p0.end;
     __syncthreads();
+    SegR r;
     bool fin;                                   // r is this lane's exact result
     if (lane == 0) {
         r.start = s; r.end = p0.end; r.cnt = p0.cnt; r.kind = p0.kind; r.reason = p0.reason;
         fin = true;
     } else {
-        fin = verify_run(in, t, ed, S.exit_[lane - 1], s, C, e, p0, S, lane, 1, r);
+        fin = verify_run(b, t, ed, (uint32_t)S.exit_[lane - 1], s, C1, C2, e, p0, S, lane, 1, r);
     }
     // exact prefix: lanes before the first unsynchronised lane
     const uint64_t um = __ballot(!fin);
     const uint32_t j0 = um ? (uint32_t)__builtin_ctzll(um) : 64u;
     const uint64_t tm = __ballot(fin && r.kind != T_EXIT);
     const uint32_t t0 = tm ? (uint32_t)__builtin_ctzll(tm) : 64u;
-    if (j0 >= t0) { first_term = t0; return; }
-    // lane j0 started right (its predecessor is exact) but did not meet its own speculation: its
-    // verify run already decoded the segment.  Lanes after it resolve in order.
-    nslow += (uint32_t)__popcll(um);
-    const uint32_t nph = __popcll(um) > 2 ? NPH : 1u;
-    if (nph > 1 && (uint32_t)lane > j0) {
-        for (uint32_t f = 1; f < NPH; f++) {
-            Spec q;
-            spec_run(in, t, ed, min(s + f, e), s, C, e, q);
-            S.ph_cp[f - 1][lane] = q.cp; S.ph_cpc[f - 1][lane] = q.cpc;
-            S.ph_end[f - 1][lane] = (uint32_t)(q.end - s);
-            S.ph_cnt[f - 1][lane] = (uint32_t)min(q.cnt, (uint64_t)NOCP);
-            S.ph_kr[f - 1][lane] = (q.kind << 16) | q.reason;
-            if (q.end - s >= NOCP || q.cnt >= NOCP) S.ph_cp[f - 1][lane] = NOCP;
-        }
-    }
-    S.exit_[lane] = r.end;
-    S.kind_[lane] = r.kind;
-    __syncthreads();
-    first_term = (r.kind != T_EXIT && (uint32_t)lane == j0) ? j0 : 64u;
-    first_term = __shfl(first_term, (int)j0, 64);
-    for (uint32_t j = j0 + 1; j < 64 && first_term == 64; j++) {
-        nfix++;
-        if ((uint32_t)lane == j) {
-            const uint64_t st = S.exit_[j - 1];
-            if (!(fin && st == r.start)) {
-                verify_run(in, t, ed, st, s, C, e, p0, S, lane, nph, r);
-                S.exit_[lane] = r.end;
-                S.kind_[lane] = r.kind;
+    if (j0 >= t0) {
+        first_term = t0;
+    } else {
+        // lane j0 started right (its predecessor is exact) but did not meet its own speculation:
+        // its verify run already decoded the segment.  Lanes after it resolve in order.
+        nslow += (uint32_t)__popcll(um);
+        const uint32_t nph = __popcll(um) > 2 ? NPH : 1u;
+        if (nph > 1 && (uint32_t)lane > j0) {
+            for (uint32_t f = 1; f < NPH; f++) {
+                Spec q;
+                spec_run(b, t, ed, min(s + f, e), s, C1, C1, e, q);
+                S.ph_cp[f - 1][lane] = q.cp1; S.ph_cpc[f - 1][lane] = q.cpc1;
+                S.ph_end[f - 1][lane] = q.end - s;
+                S.ph_cnt[f - 1][lane] = q.cnt;
+                S.ph_kr[f - 1][lane] = (q.kind << 16) | q.reason;
             }
         }
+        S.exit_[lane] = r.end;
+        S.kind_[lane] = r.kind;
         __syncthreads();
-        if (S.kind_[j] != T_EXIT) first_term = j;
+        first_term = (r.kind != T_EXIT && (uint32_t)lane == j0) ? j0 : 64u;
+        first_term = __shfl(first_term, (int)j0, 64);
+        for (uint32_t j = j0 + 1; j < 64 && first_term == 64; j++) {
+            nfix++;
+            if ((uint32_t)lane == j) {
+                const uint32_t st = (uint32_t)S.exit_[j - 1];
+                if (!(fin && st == r.start)) {
+                    verify_run(b, t, ed, st, s, C1, C2, e, p0, S, lane, nph, r);
+                    S.exit_[lane] = r.end;
+                    S.kind_[lane] = r.kind;
+                }
+            }
+            __syncthreads();
+            if (S.kind_[j] != T_EXIT) first_term = j;
+        }
     }
+    out.start = b.base + r.start; out.end = b.base + r.end; out.cnt = r.cnt;
+    out.kind = r.kind; out.reason = r.reason;
 }
 
 __device__ __forceinline__ uint64_t wave_sum_u64(uint64_t x) {
@@ -463,8 +537,9 @@ __device__ __forceinline__ uint64_t next_cand(const uint64_t* cands, uint32_t nc
 
 // ---- emit: write pass of one lane ---------------------------------------------------------------
 struct WLane {
-    Rp rd;
-    uint64_t dst0, n, cnt, end;
+    Rq rd;
+    uint32_t end;               // round-relative stop bit (segment exit)
+    uint64_t dst0, n, cnt;
     uint32_t cp_len, cp_dist, lastb, wc, wcn;
     uint32_t kind, reason;      // final state (T_ERR also for COPY_BEFORE found here)
     bool active, tainted;
@@ -541,7 +616,7 @@ ndfl_inflate_count_wave_kernel(const uint32_t* w, uint64_t nwords, uint64_t nbit
         uint64_t rs = d0;
         bool block_done = false, chain_done = false;
         while (!block_done) {
-            uint64_t E = next_cand(cands, ncand, rs, limit);
+            uint64_t E = min(next_cand(cands, ncand, rs, limit), rs + MAX_SPAN);
             if (E <= rs) E = rs + 1;
             Seg r;
             uint32_t ft;
@@ -658,7 +733,7 @@ ndfl_inflate_emit_wave_kernel(const uint32_t* w, uint64_t nwords, uint64_t nbits
                 r.kind = T_EXIT; r.reason = 0;
                 if ((uint32_t)lane == ft) { r.end = m.end_ft; r.kind = m.kind_ft; r.reason = m.reason_ft; }
             } else {
-                uint64_t E = next_cand(cands, ncand, rs, ch.end_bit);
+                uint64_t E = min(next_cand(cands, ncand, rs, ch.end_bit), rs + MAX_SPAN);
                 if (E <= rs) E = rs + 1;
                 round_decode(in, S.t, ed, rs, E, S, lane, r, ft, nslow, nfix);
             }
@@ -674,8 +749,9 @@ ndfl_inflate_emit_wave_kernel(const uint32_t* w, uint64_t nwords, uint64_t nbits
             __syncthreads();
             // write pass (budgeted steps; a lane waiting on another lane or chain skips its turn)
             WLane L;
-            L.rd.init(in, r.start);
-            L.dst0 = base + pre; L.n = 0; L.cnt = mycnt; L.end = r.end;
+            const RB rb = make_rb(in, rs);
+            L.rd.init(rb, (uint32_t)(r.start - rb.base));
+            L.dst0 = base + pre; L.n = 0; L.cnt = mycnt; L.end = (uint32_t)(r.end - rb.base);
             L.cp_len = 0; L.cp_dist = 0; L.lastb = 0; L.wc = 0; L.wcn = 0;
             L.kind = r.kind; L.reason = r.reason;
             L.active = live; L.tainted = false;
@@ -688,7 +764,7 @@ ndfl_inflate_emit_wave_kernel(const uint32_t* w, uint64_t nwords, uint64_t nbits
                         if (L.cp_len == 0) {
                             if (L.rd.pos >= L.end && L.kind == T_EXIT) { L.active = false; break; }
                             Tok tk;
-                            next_tok(L.rd, in, S.t, ed, tk);
+                            next_tok(L.rd, rb, S.t, ed, tk);
                             if (tk.kind == K_LIT) {
                                 wputb(L, out, L.dst0 + L.n, tk.val);
                                 L.lastb = tk.val;
@@ -765,7 +841,7 @@ ndfl_inflate_emit_wave_kernel(const uint32_t* w, uint64_t nwords, uint64_t nbits
                 const int fl = (int)__builtin_ctzll(em);
                 status = ST_ERROR;
                 reason = __shfl(L.reason, fl, 64);
-                endpos = __shfl((unsigned long long)L.end, fl, 64);
+                endpos = rb.base + __shfl(L.end, fl, 64);
                 base = __shfl((unsigned long long)(L.dst0 + L.n), fl, 64);
                 chain_done = true;
                 break;
