@@ -27,7 +27,7 @@ using namespace inf;
 
 constexpr uint32_t LB = 10;                 // literal/length primary bits
 constexpr uint32_t DB = 8;                  // distance primary bits
-constexpr int BUDGET = 16;                  // tokens per emit step
+constexpr int BUDGET = 32;                  // tokens per emit step
 // table entry: [4:0] code length (0: longer than the primary), [8:5] extra bits, [10:9] kind,
 // [31:16] literal byte / run base / distance base
 enum : uint32_t { K_LIT = 0, K_LEN = 1, K_EOB = 2, K_BAD = 3 };
@@ -115,27 +115,36 @@ __device__ __forceinline__ RB make_rb(const In& in, uint64_t rs) {
     RB b;
     b.base = rs & ~127ull;
     b.gp = (const u32x4*)in.w + (b.base >> 7);
+
     b.gmax = (uint32_t)((in.nwords + 3) / 4 + 1 - (b.base >> 7));
     b.nb = (uint32_t)min(in.nbits - min(in.nbits, b.base), (uint64_t)0xFFFFFFFFu);
     return b;
 }
 struct Rq {
+    // `cur` is the group being consumed; the next group is in flight into `nxt`.  At a group
+    // boundary `cur = nxt` is materialised BEFORE the next load is issued (compiler barrier), so
+    // the load can land in nxt's own registers: no copy of in-flight data, no early s_waitcnt.
     uint64_t bb;
     uint32_t bn, ci, qw, pos;
-    u32x4 cur, nxt, nx2;
+    u32x4 cur, nxt;
     __device__ __forceinline__ static uint32_t pick(const u32x4& v, uint32_t i) {
         uint32_t a = (i & 1) ? v.y : v.x, b = (i & 1) ? v.w : v.z;
         return (i & 2) ? b : a;
     }
     __device__ __forceinline__ void adv(const RB& b) {
-        if (++ci == 4) { cur = nxt; nxt = nx2; qw++; nx2 = b.gp[min(qw + 2, b.gmax)]; ci = 0; }
+        if (++ci == 4) {
+            ci = 0;
+            qw++;
+            cur = nxt;
+            asm volatile("" : "+v"(cur) :: "memory");
+            nxt = b.gp[min(qw + 1, b.gmax)];
+        }
     }
     __device__ __forceinline__ void init(const RB& b, uint32_t p) {
         pos = p;
         qw = p >> 7;
         cur = b.gp[min(qw, b.gmax)];
         nxt = b.gp[min(qw + 1, b.gmax)];
-        nx2 = b.gp[min(qw + 2, b.gmax)];
         ci = (p >> 5) & 3;
         bb = (uint64_t)(pick(cur, ci) >> (p & 31));
         bn = 32 - (p & 31);
@@ -536,32 +545,76 @@ __device__ __forceinline__ uint64_t next_cand(const uint64_t* cands, uint32_t nc
 }
 
 // ---- emit: write pass of one lane ---------------------------------------------------------------
+// Output bytes are assembled into aligned 32-bit words; completed words wait in a 4-word queue that
+// is stored right after the bit reader crosses a 16-byte input group.  On this ISA stores and loads
+// share one counter (vmcnt), and the reader waits for its prefetched group at every group
+// boundary: stores issued just after that wait have a whole group's decode time to complete, so
+// the next boundary's wait does not stall on them.
+typedef __attribute__((address_space(1))) uint8_t gu8;       // global (not flat) pointers
+typedef __attribute__((address_space(1))) uint32_t gu32;
+typedef __attribute__((address_space(1))) u32x4 gu32x4;
+
 struct WLane {
     Rq rd;
     uint32_t end;               // round-relative stop bit (segment exit)
     uint64_t dst0, n, cnt;
     uint32_t cp_len, cp_dist, lastb, wc, wcn;
+    uint32_t q0, q1, q2, q3, qn, lastqw;
+    uint64_t qaddr;             // byte address of q0
     uint32_t kind, reason;      // final state (T_ERR also for COPY_BEFORE found here)
     bool active, tainted;
 };
 
-__device__ __forceinline__ void wputb(WLane& L, uint8_t* out, uint64_t P, uint32_t b) {
+__device__ __forceinline__ void wq_flush(WLane& L, gu8* out) {
+    if (L.qn == 0) return;
+    gu32* p = (gu32*)(out + L.qaddr);
+    if (L.qn == 4 && (L.qaddr & 15) == 0) {
+        u32x4 v; v.x = L.q0; v.y = L.q1; v.z = L.q2; v.w = L.q3;
+        *(gu32x4*)p = v;
+    } else {
+        p[0] = L.q0;
+        if (L.qn > 1) p[1] = L.q1;
+        if (L.qn > 2) p[2] = L.q2;
+        if (L.qn > 3) p[3] = L.q3;
+    }
+    L.qn = 0;
+}
+__device__ __forceinline__ void wq_push(WLane& L, gu8* out, uint64_t addr, uint32_t v) {
+    // (pushes are consecutive: direct stores elsewhere are preceded by wq_flush)
+    if (L.qn == 0) L.qaddr = addr;
+    L.q0 = L.qn == 0 ? v : L.q0;
+    L.q1 = L.qn == 1 ? v : L.q1;
+    L.q2 = L.qn == 2 ? v : L.q2;
+    L.q3 = L.qn == 3 ? v : L.q3;
+    if (++L.qn == 4) wq_flush(L, out);
+}
+__device__ __forceinline__ void wputb(WLane& L, gu8* out, uint64_t P, uint32_t b) {
     if (L.wcn == 0 && (P & 3)) { out[P] = (uint8_t)b; return; }
     L.wc |= b << (8 * (uint32_t)(P & 3));
     L.wcn++;
-    if ((P & 3) == 3) { *(uint32_t*)(out + P - 3) = L.wc; L.wc = 0; L.wcn = 0; }
+    if ((P & 3) == 3) { wq_push(L, out, P - 3, L.wc); L.wc = 0; L.wcn = 0; }
 }
-__device__ __forceinline__ void wflush(WLane& L, uint8_t* out, uint64_t Pnext) {
+// as wputb, but a completed word is stored at once (copy loops read back what they just wrote)
+__device__ __forceinline__ void wputb_now(WLane& L, gu8* out, uint64_t P, uint32_t b) {
+    if (L.wcn == 0 && (P & 3)) { out[P] = (uint8_t)b; return; }
+    L.wc |= b << (8 * (uint32_t)(P & 3));
+    L.wcn++;
+    if ((P & 3) == 3) { *(gu32*)(out + P - 3) = L.wc; L.wc = 0; L.wcn = 0; }
+}
+// store everything pending (queue, then the partial word ending at Pnext)
+__device__ __forceinline__ void wflush(WLane& L, gu8* out, uint64_t Pnext) {
+    wq_flush(L, out);
     for (uint32_t k = 0; k < L.wcn; k++) out[Pnext - L.wcn + k] = (uint8_t)(L.wc >> (8 * k));
     L.wc = 0; L.wcn = 0;
 }
-__device__ __forceinline__ void wcopy(WLane& L, uint8_t* out, uint64_t dst, uint64_t src, uint32_t len, uint32_t dist) {
+__device__ __forceinline__ void wcopy(WLane& L, gu8* out, uint64_t dst, uint64_t src, uint32_t len, uint32_t dist) {
     if (dist == 1) {
         const uint32_t v = (L.n > 0) ? L.lastb : (uint32_t)out[src];
         uint32_t k = 0;
         for (; k < len && (L.wcn > 0 || ((dst + k) & 3)); k++) wputb(L, out, dst + k, v);
         const uint32_t v4 = v * 0x01010101u;
-        for (; k + 4 <= len; k += 4) *(uint32_t*)(out + dst + k) = v4;
+        if (k + 4 <= len) wq_flush(L, out);        // the queue stays the newest consecutive words
+        for (; k + 4 <= len; k += 4) *(gu32*)(out + dst + k) = v4;
         for (; k < len; k++) wputb(L, out, dst + k, v);
         L.lastb = v;
         return;
@@ -571,7 +624,9 @@ __device__ __forceinline__ void wcopy(WLane& L, uint8_t* out, uint64_t dst, uint
         wflush(L, out, dst);
         for (uint32_t k = 0; k < len; k++) { b = out[src + k]; out[dst + k] = (uint8_t)b; }
     } else {
-        for (uint32_t k = 0; k < len; k++) { b = out[src + k]; wputb(L, out, dst + k, b); }
+        // sources lie >= 4 bytes back: before the partial word, possibly in the queue
+        wq_flush(L, out);
+        for (uint32_t k = 0; k < len; k++) { b = out[src + k]; wputb_now(L, out, dst + k, b); }
     }
     L.lastb = b;
 }
@@ -675,6 +730,7 @@ ndfl_inflate_emit_wave_kernel(const uint32_t* w, uint64_t nwords, uint64_t nbits
     __shared__ Shared S;
     __shared__ uint32_t s_ticket;
     const int lane = threadIdx.x;
+    gu8* gout = (gu8*)out;
     if (lane == 0) s_ticket = atomicAdd(ticket, 1u);
     __syncthreads();
     const uint32_t k = s_ticket;
@@ -753,6 +809,7 @@ ndfl_inflate_emit_wave_kernel(const uint32_t* w, uint64_t nwords, uint64_t nbits
             L.rd.init(rb, (uint32_t)(r.start - rb.base));
             L.dst0 = base + pre; L.n = 0; L.cnt = mycnt; L.end = (uint32_t)(r.end - rb.base);
             L.cp_len = 0; L.cp_dist = 0; L.lastb = 0; L.wc = 0; L.wcn = 0;
+            L.q0 = L.q1 = L.q2 = L.q3 = 0; L.qn = 0; L.qaddr = 0; L.lastqw = L.rd.qw;
             L.kind = r.kind; L.reason = r.reason;
             L.active = live; L.tainted = false;
             uint32_t waits = 0;
@@ -766,7 +823,8 @@ ndfl_inflate_emit_wave_kernel(const uint32_t* w, uint64_t nwords, uint64_t nbits
                             Tok tk;
                             next_tok(L.rd, rb, S.t, ed, tk);
                             if (tk.kind == K_LIT) {
-                                wputb(L, out, L.dst0 + L.n, tk.val);
+                                wputb(L, gout, L.dst0 + L.n, tk.val);
+                                if (L.rd.qw != L.lastqw) { wq_flush(L, gout); L.lastqw = L.rd.qw; }
                                 L.lastb = tk.val;
                                 L.n++;
                                 continue;
@@ -811,22 +869,25 @@ ndfl_inflate_emit_wave_kernel(const uint32_t* w, uint64_t nwords, uint64_t nbits
                                     for (uint32_t j = lo; j <= need_hi; j++) L.tainted |= taint[j] != 0;
                             }
                             if (!ok) { waiting = true; break; }
+                            // the sources were stored by this wave (same vmcnt) or published by an
+                            // earlier chain (agent release): drain, then invalidate L1 before reading
+                            asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
                             __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
                         }
-                        wcopy(L, out, dst, src, L.cp_len, L.cp_dist);
+                        wcopy(L, gout, dst, src, L.cp_len, L.cp_dist);
                         L.n += L.cp_len;
                         L.cp_len = 0;
                     }
-                    if (!L.active) wflush(L, out, L.dst0 + L.n);
+                    if (!L.active) wflush(L, gout, L.dst0 + L.n);
                     if (waiting && ++waits > (1u << 24)) {          // safety net: never hang the device
                         L.active = false; L.kind = T_ERR; L.reason = R_INTERNAL;
                     }
                 }
-                __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
-                // a lane that stopped on an error releases its waiters: what follows an error is
+                // progress = bytes issued to memory; a reader drains the wave's vmcnt before using
+                // them.  A lane that stopped on an error releases its waiters: what follows an error is
                 // never reported, so they may read anything
                 S.prog[lane] = (!L.active && L.kind == T_ERR) ? 0xFFFFFFFFu
-                                                              : (uint32_t)min(L.n - L.wcn, (uint64_t)0xFFFFFFFFu);
+                                                              : (uint32_t)min(L.n - L.wcn - 4 * L.qn, (uint64_t)0xFFFFFFFFu);
                 __syncthreads();
                 if (__all(!L.active || waiting)) { if (++idle > 2) __builtin_amdgcn_s_sleep(2); }
                 else idle = 0;
