@@ -6,6 +6,8 @@
 
 #include <hip/hip_runtime.h>
 #include <string.h>
+#include <stdio.h>
+#include <algorithm>
 #include <stdlib.h>
 #include <vector>
 
@@ -220,6 +222,9 @@ int ndfl_deflate_chunks(ndfl_ctx* c, const uint8_t* hist, uint32_t hist_len, uin
     a.crc_raw = crc_inout ? c->d_crc.as<uint32_t>() : nullptr;
     a.crc_tab = c->d_tabs.as<uint32_t>();
     a.crc_x = c->d_tabs.as<uint32_t>() + 1024;
+    a.prof = nullptr;
+    const bool prof = getenv("NDFL_DEFLATE_PROFILE") != nullptr;
+    if (prof) HIPCHK(hipMalloc(&a.prof, (size_t)nch * 64));
     HIPCHK(hipEventRecord(c->ev0, s));
     hipLaunchKernelGGL(ndfl_deflate_chunks_kernel, dim3(nch), dim3(1024), 0, s, a);
     HIPCHK(hipGetLastError());
@@ -240,6 +245,20 @@ int ndfl_deflate_chunks(ndfl_ctx* c, const uint8_t* hist, uint32_t hist_len, uin
     hipEventElapsedTime(&ms, c->ev0, c->ev1);
     c->last_ms = ms;
     c->deflate_ms = ms;
+    if (prof) {
+        std::vector<uint64_t> h((size_t)nch * 8);
+        HIPCHK(hipMemcpy(h.data(), a.prof, (size_t)nch * 64, hipMemcpyDeviceToHost));
+        hipFree(a.prof);
+        double sum[7] = {0}, tmin = 1e300, tmax = 0;
+        for (uint32_t k = 0; k < nch; k++) {
+            for (int p = 0; p < 7; p++) sum[p] += (double)(h[k * 8 + p + 1] - h[k * 8 + p]);
+            tmin = std::min(tmin, (double)h[k * 8]); tmax = std::max(tmax, (double)h[k * 8 + 7]);
+        }
+        // wall_clock64 runs at 100 MHz
+        fprintf(stderr, "[ndfl] deflate phases (us/chunk): load+crc %.2f hist %.2f codes %.2f bits+scan %.2f emit %.2f "
+                "lookback %.2f store %.2f; span %.2f ms\n", sum[0] / nch / 100, sum[1] / nch / 100, sum[2] / nch / 100,
+                sum[3] / nch / 100, sum[4] / nch / 100, sum[5] / nch / 100, sum[6] / nch / 100, (tmax - tmin) / 1e5);
+    }
     uint64_t st;
     memcpy(&st, c->h_pinned, 8);
     const uint64_t end_bits = st & ST_VAL;

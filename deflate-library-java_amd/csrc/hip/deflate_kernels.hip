@@ -92,20 +92,8 @@ struct Args {
     uint32_t* crc_raw;        // optional [nchunks]
     const uint32_t* crc_tab;  // slicing-by-4 tables (1024 u32)
     const uint32_t* crc_x;    // x^(8k) k<64 then x^(8*64k) k<1024
+    uint64_t* prof;           // optional [nchunks][8] phase timestamps (wall clock)
 };
-
-__device__ __forceinline__ uint32_t byte_at(const uint32_t (&w)[16], int i) {
-    // select tree over 16 registers (i is lane-divergent)
-    const int wi = i >> 2;
-    uint32_t a0 = (wi & 1) ? w[1] : w[0],  a1 = (wi & 1) ? w[3] : w[2];
-    uint32_t a2 = (wi & 1) ? w[5] : w[4],  a3 = (wi & 1) ? w[7] : w[6];
-    uint32_t a4 = (wi & 1) ? w[9] : w[8],  a5 = (wi & 1) ? w[11] : w[10];
-    uint32_t a6 = (wi & 1) ? w[13] : w[12], a7 = (wi & 1) ? w[15] : w[14];
-    uint32_t b0 = (wi & 2) ? a1 : a0, b1 = (wi & 2) ? a3 : a2, b2 = (wi & 2) ? a5 : a4, b3 = (wi & 2) ? a7 : a6;
-    uint32_t c0 = (wi & 4) ? b1 : b0, c1 = (wi & 4) ? b3 : b2;
-    uint32_t d = (wi & 8) ? c1 : c0;
-    return (d >> ((i & 3) * 8)) & 0xFFu;
-}
 
 // Length symbol / extra bits of a run 3..258 (D/comp/Lz77Huffman.java:92-111).
 __device__ __forceinline__ void run_sym(uint32_t run, uint32_t& sym, uint32_t& ne, uint32_t& ex) {
@@ -291,6 +279,7 @@ ndfl_deflate_chunks_kernel(Args a) {
     const int tid = threadIdx.x;
     const int lane = tid & 63, wid = tid >> 6;
 
+    const uint64_t tp0 = wall_clock64();
     if (tid == 0) ps.chunk = atomicAdd(a.ticket, 1u);
     if (tid < 288) hlit[tid] = 0;
     if (tid < 32) hdist[tid] = 0;
@@ -324,7 +313,14 @@ ndfl_deflate_chunks_kernel(Args a) {
             w[k] = x;
         }
     }
-    if (vcnt > 0) lastb[tid] = (uint8_t)byte_at(w, vcnt - 1);
+    if (vcnt > 0) {
+        uint32_t lv = w[15] >> 24;
+        if (vcnt < 64) {                    // only the chunk's last lane; static indices keep w[] in registers
+#pragma unroll
+            for (int i = 0; i < 64; i++) if (i == vcnt - 1) lv = (w[i >> 2] >> (8 * (i & 3))) & 0xFFu;
+        }
+        lastb[tid] = (uint8_t)lv;
+    }
 
     // ---- CRC-32 (raw, init 0) of this lane's bytes, combined across the chunk ----------------
     if (a.crc_raw) {
@@ -341,7 +337,11 @@ ndfl_deflate_chunks_kernel(Args a) {
                 cr = T3[x & 0xFF] ^ T2[(x >> 8) & 0xFF] ^ T1[(x >> 16) & 0xFF] ^ T0[x >> 24];
             }
         }
-        for (int i = nfull * 4; i < vcnt; i++) cr = T0[(cr ^ byte_at(w, i)) & 0xFF] ^ (cr >> 8);
+        if (vcnt & 3) {
+#pragma unroll
+            for (int i = 0; i < 64; i++)
+                if (i >= nfull * 4 && i < vcnt) cr = T0[(cr ^ (w[i >> 2] >> (8 * (i & 3)))) & 0xFF] ^ (cr >> 8);
+        }
         uint32_t contrib = 0;
         if (vcnt > 0) {
             // shift by the bytes that follow this lane inside the chunk
@@ -361,6 +361,7 @@ ndfl_deflate_chunks_kernel(Args a) {
         a.crc_raw[c] = x;
     }
 
+    const uint64_t tp1 = wall_clock64();
     // ---- 2. run pieces ------------------------------------------------------------------------
     const bool has_prev0 = (c > 0) ? (a.hist_enabled != 0) : (a.prev_byte >= 0);
     const uint32_t prev0 = (c > 0) ? (uint32_t)src[-1] : (uint32_t)(a.prev_byte & 0xFF);
@@ -388,39 +389,70 @@ ndfl_deflate_chunks_kernel(Args a) {
         if (gpos == 0) return (has_prev0 && prev0 == v) ? 0u : 1u;
         return 1u;
     };
+    // pieces of length 1 (the next byte starts a piece, or the chunk ends) are exactly one literal
+    // whatever their lead; they take the fast path below
+    uint64_t S1 = 0;
+    if (vcnt > 0) {
+        const uint64_t nxt = (F >> 1) | (nextStart == t0 + 64 ? (1ull << 63) : 0ull);
+        const uint64_t beyond = vcnt >= 64 ? 0ull : (~0ull << (vcnt - 1));
+        S1 = F & (nxt | beyond);
+    }
+    // visit this lane's pieces in order: BODY sees (gpos, v, pend, single).  Outer loop over 8-byte
+    // groups (select tree on the uniform group index: a dynamic register index would put w[] in
+    // scratch memory), inner loop unrolled: byte extraction is a constant shift.  A macro rather than
+    // a lambda: capturing w[] by reference also demotes it to scratch.
+#define NDFL_FOR_PIECES(...)                                                                           \
+    _Pragma("unroll 1") for (int o_ = 0; o_ < 8; o_++) {                                               \
+        const uint32_t g_ = (uint32_t)(F >> (8 * o_)) & 0xFFu;                                        \
+        if (!__any(g_ != 0)) continue;                                                                 \
+        const bool o1_ = o_ & 1, o2_ = o_ & 2, o4_ = o_ & 4;                                           \
+        const uint32_t a0_ = o1_ ? w[2] : w[0], a1_ = o1_ ? w[6] : w[4];                               \
+        const uint32_t a2_ = o1_ ? w[10] : w[8], a3_ = o1_ ? w[14] : w[12];                            \
+        const uint32_t b0_ = o1_ ? w[3] : w[1], b1_ = o1_ ? w[7] : w[5];                               \
+        const uint32_t b2_ = o1_ ? w[11] : w[9], b3_ = o1_ ? w[15] : w[13];                            \
+        const uint32_t gw0_ = o4_ ? (o2_ ? a3_ : a2_) : (o2_ ? a1_ : a0_);                             \
+        const uint32_t gw1_ = o4_ ? (o2_ ? b3_ : b2_) : (o2_ ? b1_ : b0_);                             \
+        _Pragma("unroll") for (int j_ = 0; j_ < 8; j_++) {                                             \
+            if ((g_ >> j_) & 1) {                                                                      \
+                const int i_ = 8 * o_ + j_;                                                            \
+                const uint32_t v = ((j_ < 4 ? gw0_ : gw1_) >> (8 * (j_ & 3))) & 0xFFu;                 \
+                const bool single = (S1 >> i_) & 1;                                                    \
+                const uint32_t gpos = t0 + (uint32_t)i_;                                               \
+                uint32_t pend = gpos + 1;                                                              \
+                if (!single) {                                                                         \
+                    const uint64_t rest_ = i_ < 63 ? (F >> (i_ + 1)) : 0ull;                           \
+                    pend = rest_ ? gpos + 1 + (uint32_t)__builtin_ctzll(rest_) : nextStart;            \
+                }                                                                                      \
+                __VA_ARGS__                                                                            \
+            }                                                                                          \
+        }                                                                                              \
+    }
 
     // ---- 3. histograms (closed-form greedy parse per piece, App. A.2) -------------------------
-    {
-        uint64_t Fm = F;
-        while (Fm) {
-            const int i = __builtin_ctzll(Fm);
-            Fm &= Fm - 1;
-            const uint32_t pend = Fm ? t0 + (uint32_t)__builtin_ctzll(Fm) : nextStart;
-            const uint32_t gpos = t0 + (uint32_t)i;
-            const uint32_t v = byte_at(w, i);
-            const uint32_t plen = pend - gpos;
-            const uint32_t lead = lead_of(gpos, v);
-            if (!a.rle) { atomicAdd(&hlit[v], 1u); continue; }
-            const uint32_t R = plen - lead;
-            const uint32_t n258 = R / 258, m = R % 258;
-            uint32_t nlit = lead + (m < 3 ? m : 0);
-            if (nlit) atomicAdd(&hlit[v], nlit);
-            if (n258) atomicAdd(&hlit[285], n258);
-            uint32_t nd = n258;
-            if (m >= 3) {
-                uint32_t sym, ne, ex; run_sym(m, sym, ne, ex);
-                atomicAdd(&hlit[sym], 1u);
-                nd++;
-            }
-            if (nd) atomicAdd(&hdist[0], nd);
+    NDFL_FOR_PIECES({
+        if (single || !a.rle) { atomicAdd(&hlit[v], 1u); continue; }
+        const uint32_t plen = pend - gpos;
+        const uint32_t lead = lead_of(gpos, v);
+        const uint32_t R = plen - lead;
+        const uint32_t n258 = R / 258, m = R % 258;
+        uint32_t nlit = lead + (m < 3 ? m : 0);
+        if (nlit) atomicAdd(&hlit[v], nlit);
+        if (n258) atomicAdd(&hlit[285], n258);
+        uint32_t nd = n258;
+        if (m >= 3) {
+            uint32_t sym, ne, ex; run_sym(m, sym, ne, ex);
+            atomicAdd(&hlit[sym], 1u);
+            nd++;
         }
-    }
+        if (nd) atomicAdd(&hdist[0], nd);
+    })
     if (tid == 0) {
         atomicAdd(&hlit[256], 1u);                          // end of block (:131-132)
         if (a.dynamic && len_c == 0) atomicAdd(&hlit[0], 1u);  // (:146-147)
     }
     __syncthreads();
 
+    const uint64_t tp2 = wall_clock64();
     // ---- 4. code construction -------------------------------------------------------------------
     if (!a.dynamic) {
         // fixed codes (D/comp/Lz77Huffman.java:394-410)
@@ -529,66 +561,46 @@ ndfl_deflate_chunks_kernel(Args a) {
     const uint32_t packedLo = misc[4], packedHi = misc[5];
     __syncthreads();
 
+    const uint64_t tp3 = wall_clock64();
     // ---- 5. token bits per lane, chunk size, decoupled look-back ------------------------------
     const uint32_t d0 = ps.distCode[0];
     const uint32_t c285 = ps.litCode[285];
     uint32_t mybits = 0;
-    {
-        uint64_t Fm = F;
-        while (Fm) {
-            const int i = __builtin_ctzll(Fm);
-            Fm &= Fm - 1;
-            const uint32_t pend = Fm ? t0 + (uint32_t)__builtin_ctzll(Fm) : nextStart;
-            const uint32_t gpos = t0 + (uint32_t)i;
-            const uint32_t v = byte_at(w, i);
-            const uint32_t lv = ps.litCode[v] >> 16;
-            if (!a.rle) { mybits += lv; continue; }
-            const uint32_t lead = lead_of(gpos, v);
-            const uint32_t R = pend - gpos - lead;
-            const uint32_t n258 = R / 258, m = R % 258;
-            mybits += lead * lv + n258 * ((c285 >> 16) + (d0 >> 16));
-            if (m >= 3) {
-                uint32_t sym, ne, ex; run_sym(m, sym, ne, ex);
-                mybits += (ps.litCode[sym] >> 16) + ne + (d0 >> 16);
-            } else {
-                mybits += m * lv;
-            }
+    NDFL_FOR_PIECES({
+        const uint32_t lv = ps.litCode[v] >> 16;
+        if (single || !a.rle) { mybits += lv; continue; }
+        const uint32_t lead = lead_of(gpos, v);
+        const uint32_t R = pend - gpos - lead;
+        const uint32_t n258 = R / 258, m = R % 258;
+        mybits += lead * lv + n258 * ((c285 >> 16) + (d0 >> 16));
+        if (m >= 3) {
+            uint32_t sym, ne, ex; run_sym(m, sym, ne, ex);
+            mybits += (ps.litCode[sym] >> 16) + ne + (d0 >> 16);
+        } else {
+            mybits += m * lv;
         }
-    }
+    })
+    const uint64_t tp3a = wall_clock64();
     uint32_t tokTotal;
     const uint32_t myoff = block_excl_scan<uint32_t, NW>(mybits, ps.scan32, tokTotal);
+    const uint64_t tp3b = wall_clock64();
     const uint32_t eobLen = ps.litCode[256] >> 16;
     const uint32_t hdrBits = ps.hdrBits;
     const uint64_t S = (uint64_t)hdrBits + tokTotal + eobLen;
+    // publish this chunk's size now; the look-back runs after the chunk is emitted at local bit 0,
+    // so predecessors get the emit time to publish theirs
     if (tid == 0) {
-        uint64_t P;
-        if (c == 0) {
-            P = a.base_bit;
-            st_agent(&a.status[0], ST_PRE | (P + S));
-        } else {
-            st_agent(&a.status[c], ST_AGG | S);
-            uint64_t acc = 0;
-            int64_t j = (int64_t)c - 1;
-            for (;;) {
-                uint64_t st = ld_agent(&a.status[j]);
-                if (st & ST_PRE) { acc += st & ST_VAL; break; }
-                if (st & ST_AGG) { acc += st & ST_VAL; j--; continue; }
-                __builtin_amdgcn_s_sleep(1);
-            }
-            P = acc;
-            st_agent(&a.status[c], ST_PRE | (P + S));
-        }
-        ps.P = P;
+        if (c == 0) st_agent(&a.status[0], ST_PRE | (a.base_bit + S));
+        else st_agent(&a.status[c], ST_AGG | S);
         if (a.chunk_bits) a.chunk_bits[c] = S;
     }
-    // zero the bit buffer (scratch is dead from here on)
-    const uint32_t nwords = 0;  (void)nwords;
+    const uint64_t tp4 = wall_clock64();
+    // zero the bit buffer (scratch is dead from here on); one spare word for the final shift
+    const uint32_t nwl = (uint32_t)((S + 31) >> 5) + 1;
     __syncthreads();
-    const uint64_t P = ps.P;
-    const uint32_t bit0 = (uint32_t)(P & 31);
-    const uint32_t nw = (uint32_t)((bit0 + S + 31) >> 5);
-    for (uint32_t k = (uint32_t)tid; k < nw; k += DT) obuf[k] = 0;
+    for (uint32_t k = (uint32_t)tid; k < nwl; k += DT) obuf[k] = 0;
     __syncthreads();
+    const uint32_t bit0 = 0;
 
     // ---- 6. emit ------------------------------------------------------------------------------
     if (tid == 0) {
@@ -620,15 +632,9 @@ ndfl_deflate_chunks_kernel(Args a) {
         const uint32_t d0c = d0 & 0xFFFF, d0l = d0 >> 16;
         const uint32_t m258 = (c285 & 0xFFFF) | (d0c << (c285 >> 16));
         const uint32_t m258l = (c285 >> 16) + d0l;
-        uint64_t Fm = F;
-        while (Fm) {
-            const int i = __builtin_ctzll(Fm);
-            Fm &= Fm - 1;
-            const uint32_t pend = Fm ? t0 + (uint32_t)__builtin_ctzll(Fm) : nextStart;
-            const uint32_t gpos = t0 + (uint32_t)i;
-            const uint32_t v = byte_at(w, i);
+        NDFL_FOR_PIECES({
             const uint32_t lc = ps.litCode[v];
-            if (!a.rle) { bp.put(lc & 0xFFFF, lc >> 16); continue; }
+            if (single || !a.rle) { bp.put(lc & 0xFFFF, lc >> 16); continue; }
             const uint32_t lead = lead_of(gpos, v);
             const uint32_t R = pend - gpos - lead;
             const uint32_t n258 = R / 258, m = R % 258;
@@ -643,19 +649,61 @@ ndfl_deflate_chunks_kernel(Args a) {
             } else {
                 for (uint32_t k = 0; k < m; k++) bp.put(lc & 0xFFFF, lc >> 16);
             }
-        }
+        })
         bp.flush();
     }
     __syncthreads();
 
-    // ---- 7. store: interior words directly, boundary words to the edge list ------------------
+    const uint64_t tp5e = wall_clock64();
+    // ---- 7. look-back, then store shifted to the global bit offset ---------------------------
+    if (wid == 0) {
+        // decoupled look-back, one wave: lane i polls predecessor c-1-i, so 64 predecessors cost
+        // one round trip; the closest inclusive prefix (PRE) ends the walk, aggregates (AGG)
+        // before it are summed, and a not-yet-published predecessor closer than it re-polls.
+        uint64_t P = a.base_bit;
+        if (c > 0) {
+            uint64_t acc = 0;
+            int64_t base = (int64_t)c - 1;
+            for (;;) {
+                const int64_t j = base - lane;
+                const uint64_t st = j >= 0 ? ld_agent(&a.status[j]) : ST_PRE;
+                const uint64_t pre = __ballot((st & ST_PRE) != 0);
+                const uint64_t nr = __ballot((st >> 62) == 0);
+                const int fp = pre ? (int)__builtin_ctzll(pre) : 64;
+                const int fn = nr ? (int)__builtin_ctzll(nr) : 64;
+                if (fn < fp) { __builtin_amdgcn_s_sleep(1); continue; }
+                acc += wave_sum(lane <= fp ? (st & ST_VAL) : 0ull);
+                if (fp < 64) break;
+                base -= 64;
+            }
+            P = acc;
+            if (lane == 0) st_agent(&a.status[c], ST_PRE | (P + S));
+        }
+        if (lane == 0) ps.P = P;
+    }
+    __syncthreads();
+    const uint64_t tp5 = wall_clock64();
+    const uint64_t P = ps.P;
+    const uint32_t sh = (uint32_t)(P & 31);
+    const uint32_t nw = (uint32_t)((sh + S + 31) >> 5);
     const uint64_t W0 = P >> 5;
-    for (uint32_t k = (uint32_t)tid + 1; k + 1 < nw; k += DT) a.out[W0 + k] = obuf[k];
+    auto outw = [&](uint32_t k) -> uint32_t {
+        const uint32_t cur = obuf[k];
+        const uint32_t prv = k ? obuf[k - 1] : 0u;
+        return sh ? (cur << sh) | (prv >> (32 - sh)) : cur;
+    };
+    for (uint32_t k = (uint32_t)tid + 1; k + 1 < nw; k += DT) a.out[W0 + k] = outw(k);
     if (tid == 0) {
         a.edge_w[2 * c] = W0;
-        a.edge_v[2 * c] = obuf[0];
+        a.edge_v[2 * c] = outw(0);
         a.edge_w[2 * c + 1] = W0 + nw - 1;
-        a.edge_v[2 * c + 1] = nw > 1 ? obuf[nw - 1] : 0u;
+        a.edge_v[2 * c + 1] = nw > 1 ? outw(nw - 1) : 0u;
+        if (a.prof) {
+            uint64_t* q = a.prof + (uint64_t)c * 8;
+            q[0] = tp0; q[1] = tp1; q[2] = tp2; q[3] = tp3; q[4] = tp4; q[5] = tp5e; q[6] = tp5;
+            q[7] = wall_clock64();
+            (void)tp3a; (void)tp3b;
+        }
     }
 }
 
