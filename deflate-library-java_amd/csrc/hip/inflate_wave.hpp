@@ -36,21 +36,23 @@ enum : uint32_t { T_EXIT = 0, T_EOB = 1, T_ERR = 2 };
 struct Tabs {
     uint32_t lit[1u << LB];
     uint32_t dst[1u << DB];
-    uint16_t lfirst[16], lcnt[16], loff[16];
-    uint16_t dfirst[16], dcnt[16], doff[16];
-    uint16_t lsorted[288];
-    uint16_t dsorted[32];
+    // canonical slow path for codes longer than the primary: left-justified 15-bit upper limit of
+    // each length, first code and rank offset per length, and the table entry of every symbol in
+    // canonical order
+    uint32_t llim[16], dlim[16];
+    uint16_t lfirst[16], loff[16], dfirst[16], doff[16];
+    uint32_t lent[288];
+    uint32_t dent[32];
 };
 
 struct Shared {
     Tabs t;
     uint8_t lens[320];                       // literal/length 0..287, distance at 288..319
     uint16_t cl_tab[128];                    // code-length code, full 7-bit table: sym | len << 9
-    uint32_t ph_cp[7][64];                   // fallback phases 1..7: checkpoint offset,
-    uint32_t ph_cpc[7][64];                  //   bytes before it,
+    uint32_t ph_cp[7][64];                   // fallback phases 1..7: checkpoint offset | bytes before it << 16
     uint32_t ph_end[7][64];                  //   end offset,
     uint32_t ph_cnt[7][64];                  //   bytes,
-    uint32_t ph_kr[7][64];                   //   kind << 16 | reason
+    uint8_t ph_kr[7][64];                    //   kind << 5 | reason
     uint64_t exit_[64];
     uint32_t kind_[64];
     uint64_t off_[64];                       // emit: absolute output offset per lane
@@ -80,21 +82,23 @@ __device__ __forceinline__ uint32_t dist_entry(uint32_t sym, uint32_t len) {
     return len | (K_BAD << 9);
 }
 
+// Length of a code longer than the primary: the smallest l with code < lim[l] (limits are
+// non-decreasing for a canonical code); branch-free over the five candidate lengths.
+template <uint32_t PB>
+__device__ __forceinline__ uint32_t slow_entry(uint32_t p15, const uint32_t* lim, const uint16_t* first,
+                                               const uint16_t* off, const uint32_t* ent) {
+    const uint32_t c = rev_bits(p15, 15);
+    uint32_t l = PB + 1;
+#pragma unroll
+    for (uint32_t k = PB + 1; k < 15; k++) l += c >= lim[k] ? 1u : 0u;
+    const uint32_t idx = (c >> (15 - l)) - first[l];
+    return ent[off[l] + idx];
+}
 __device__ __forceinline__ uint32_t slow_lit(uint32_t p15, const Tabs& t) {
-    const uint32_t r15 = rev_bits(p15, 15);
-    for (uint32_t l = LB + 1; l < 16; l++) {
-        const uint32_t idx = (r15 >> (15 - l)) - t.lfirst[l];
-        if (idx < t.lcnt[l]) return lit_entry(t.lsorted[t.loff[l] + idx], l);
-    }
-    return 15u | (K_BAD << 9);              // unreachable: codes are complete
+    return slow_entry<LB>(p15, t.llim, t.lfirst, t.loff, t.lent);
 }
 __device__ __forceinline__ uint32_t slow_dist(uint32_t p15, const Tabs& t) {
-    const uint32_t r15 = rev_bits(p15, 15);
-    for (uint32_t l = DB + 1; l < 16; l++) {
-        const uint32_t idx = (r15 >> (15 - l)) - t.dfirst[l];
-        if (idx < t.dcnt[l]) return dist_entry(t.dsorted[t.doff[l] + idx], l);
-    }
-    return 15u | (K_BAD << 9);
+    return slow_entry<DB>(p15, t.dlim, t.dfirst, t.doff, t.dent);
 }
 
 struct Tok {
@@ -269,7 +273,7 @@ __device__ void parse_hdr(const In& in, uint64_t p, Shared& S) {
 // Canonical code from S.lens[base .. base+n) into a primary table + slow-path arrays (wave).
 // Returns the tree check result of codeLengthsToCodeTree (D/decomp/Open.java:705-756) (uniform).
 __device__ int build_code(Shared& S, uint32_t base, uint32_t n, uint32_t* prim, uint32_t pbits, uint16_t* first,
-                          uint16_t* cntv, uint16_t* offv, uint16_t* sorted, bool is_lit, int lane) {
+                          uint32_t* lim, uint16_t* offv, uint32_t* sorted, bool is_lit, int lane) {
     for (uint32_t k = (uint32_t)lane; k < (1u << pbits); k += 64) prim[k] = 0;
     uint32_t c[16];
 #pragma unroll
@@ -303,7 +307,15 @@ __device__ int build_code(Shared& S, uint32_t base, uint32_t n, uint32_t* prim, 
             fst[l] = code; off[l] = o; o += c[l];
         }
     }
-    if (lane < 16) { first[lane] = (uint16_t)fst[lane]; cntv[lane] = (uint16_t)c[lane]; offv[lane] = (uint16_t)off[lane]; }
+    if (lane < 16) {
+        first[lane] = (uint16_t)fst[lane];
+        offv[lane] = (uint16_t)off[lane];
+        uint32_t cl = 0, ll = 0;
+#pragma unroll
+        for (int L = 1; L < 16; L++) if (lane == L) { cl = c[L]; ll = fst[L] + c[L]; }
+        lim[lane] = lane ? (ll << (15 - lane)) : 0u;
+        (void)cl;
+    }
     __syncthreads();
 #pragma unroll
     for (int q = 0; q < 5; q++) {
@@ -313,9 +325,9 @@ __device__ int build_code(Shared& S, uint32_t base, uint32_t n, uint32_t* prim, 
         uint32_t f = 0, o = 0;
 #pragma unroll
         for (int L = 1; L < 16; L++) if (l == (uint32_t)L) { f = fst[L]; o = off[L]; }
-        sorted[o + rank[q]] = (uint16_t)s;
+        const uint32_t ent = is_lit ? lit_entry(s, l) : dist_entry(s, l);
+        sorted[o + rank[q]] = ent;
         if (l <= pbits) {
-            const uint32_t ent = is_lit ? lit_entry(s, l) : dist_entry(s, l);
             for (uint32_t k = rev_bits(f + rank[q], l); k < (1u << pbits); k += (1u << l)) prim[k] = ent;
         }
     }
@@ -339,12 +351,12 @@ __device__ int build_tables(Shared& S, int lane, bool& empty_dist) {
     if (S.h_btype == 1) {
         fixed_lens(S, lane);
         __syncthreads();
-        build_code(S, 0, 288, S.t.lit, LB, S.t.lfirst, S.t.lcnt, S.t.loff, S.t.lsorted, true, lane);
-        build_code(S, 288, 32, S.t.dst, DB, S.t.dfirst, S.t.dcnt, S.t.doff, S.t.dsorted, false, lane);
+        build_code(S, 0, 288, S.t.lit, LB, S.t.lfirst, S.t.llim, S.t.loff, S.t.lent, true, lane);
+        build_code(S, 288, 32, S.t.dst, DB, S.t.dfirst, S.t.dlim, S.t.doff, S.t.dent, false, lane);
         return 0;
     }
     const uint32_t numDist = S.h_numdist;
-    int e = build_code(S, 0, 288, S.t.lit, LB, S.t.lfirst, S.t.lcnt, S.t.loff, S.t.lsorted, true, lane);
+    int e = build_code(S, 0, 288, S.t.lit, LB, S.t.lfirst, S.t.llim, S.t.loff, S.t.lent, true, lane);
     if (e) return e;
     // distance code: empty (one zero length) or one used code padded at index 31 (:398-425)
     const uint32_t dl = (lane < 32) ? S.lens[288 + lane] : 0u;
@@ -354,7 +366,7 @@ __device__ int build_tables(Shared& S, int lane, bool& empty_dist) {
     __syncthreads();
     if (ones == 1 && other == 0 && lane == 0) S.lens[288 + 31] = 1;
     __syncthreads();
-    return build_code(S, 288, 32, S.t.dst, DB, S.t.dfirst, S.t.dcnt, S.t.doff, S.t.dsorted, false, lane);
+    return build_code(S, 288, 32, S.t.dst, DB, S.t.dfirst, S.t.dlim, S.t.doff, S.t.dent, false, lane);
 }
 
 // ---- segmented speculative decode of one round ------------------------------------------------
@@ -426,11 +438,12 @@ __device__ bool verify_run(const RB& b, const Tabs& t, bool ed, uint32_t t0, uin
                 return true;
             }
             for (uint32_t f = 1; f < nph; f++) {
-                if (S.ph_cp[f - 1][lane] == off) {
+                const uint32_t pc = S.ph_cp[f - 1][lane];
+                if ((pc & 0xFFFFu) == off) {
                     r.end = s + S.ph_end[f - 1][lane];
-                    r.cnt = c + (S.ph_cnt[f - 1][lane] - S.ph_cpc[f - 1][lane]);
+                    r.cnt = c + (S.ph_cnt[f - 1][lane] - (pc >> 16));
                     const uint32_t kr = S.ph_kr[f - 1][lane];
-                    r.kind = kr >> 16; r.reason = kr & 0xFFFF;
+                    r.kind = kr >> 5; r.reason = kr & 31;
                     return true;
                 }
             }
@@ -492,10 +505,11 @@ __device__ void round_decode(const In& in, const Tabs& t, bool ed, uint64_t rs, 
             for (uint32_t f = 1; f < NPH; f++) {
                 Spec q;
                 spec_run(b, t, ed, min(s + f, e), s, C1, C1, e, q);
-                S.ph_cp[f - 1][lane] = q.cp1; S.ph_cpc[f - 1][lane] = q.cpc1;
+                // (offsets and byte counts at the first checkpoint fit 16 bits; otherwise no match)
+                S.ph_cp[f - 1][lane] = (q.cp1 < 0xFFFFu && q.cpc1 <= 0xFFFFu) ? (q.cp1 | (q.cpc1 << 16)) : 0xFFFFu;
                 S.ph_end[f - 1][lane] = q.end - s;
                 S.ph_cnt[f - 1][lane] = q.cnt;
-                S.ph_kr[f - 1][lane] = (q.kind << 16) | q.reason;
+                S.ph_kr[f - 1][lane] = (uint8_t)((q.kind << 5) | q.reason);
             }
         }
         S.exit_[lane] = r.end;
