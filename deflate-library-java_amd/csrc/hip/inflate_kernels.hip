@@ -58,6 +58,11 @@ __device__ __forceinline__ void dist_base(uint32_t d, uint32_t& base, uint32_t& 
 }
 
 constexpr uint64_t IN_PAD = 256;           // zero bytes after the staged input
+// header finder scan pattern (32-bit words): FIND_WIN_WORDS of every FIND_PERIOD_WORDS.  Dense
+// (every position) by default: sparse windows make chains span several blocks, which costs more
+// in the count/emit passes' load balance than it saves here.
+constexpr uint32_t FIND_WIN_WORDS = 32768;
+constexpr uint32_t FIND_PERIOD_WORDS = 32768;
 
 struct In {
     const uint32_t* w;
@@ -307,7 +312,7 @@ __device__ bool strict_stored(const In& in, uint64_t p) {
 // (about 1 in 1000 positions) go to a global list for the strict stage.
 extern "C" __global__ void __launch_bounds__(256)
 ndfl_inflate_find_kernel(const uint32_t* w, uint64_t nwords, uint64_t nbits, uint64_t* qlist, uint32_t* qcount,
-                         uint32_t qcap) {
+                         uint32_t qcap, uint32_t win_words, uint32_t period_words) {
     using namespace inf;
     __shared__ uint32_t lut[512];            // kraft (x128) | nonzero count << 16 for 3 lengths
     __shared__ uint64_t cand[1024];
@@ -319,7 +324,9 @@ ndfl_inflate_find_kernel(const uint32_t* w, uint64_t nwords, uint64_t nbits, uin
     }
     if (threadIdx.x == 0) ncand = 0;
     __syncthreads();
-    const uint64_t t = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    // scanned windows: win_words of every period_words input words (win == period: every position)
+    const uint64_t tt = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    const uint64_t t = (tt / win_words) * period_words + tt % win_words;     // input word index
     const uint64_t p0 = t * 32;
     In in{w, nwords, nbits};
     if (p0 < nbits) {
@@ -430,11 +437,22 @@ struct EmitChain {
     uint64_t slot;        // count-pass segment record of this chain (>= slot capacity: none)
 };
 
-// Count-pass record of a chain's first round (first block): every lane's exact segment, so the
-// emit pass decodes each segment once instead of re-running the speculation.
+// Count-pass records of every round of a chain: each lane's exact segment, so the emit pass
+// decodes each segment once instead of re-running the speculation.  Records come from a pool and
+// are linked per chain in decode order (chain slot -> head record -> next ...).
+constexpr uint32_t NOREC = 0xFFFFFFFFu;
 struct SegMeta {
-    uint32_t valid, ft, kind_ft, reason_ft;
+    uint32_t ft, kind_ft, reason_ft, next;
     uint64_t end_ft, exit63;
+};
+struct SegPool {
+    uint64_t* start;      // [nrec][64]
+    uint32_t* cnt;        // [nrec][64]
+    SegMeta* meta;        // [nrec]
+    uint32_t* head;       // [nslot] first record of the chain counted at that slot (NOREC: none)
+    uint32_t* ctr;        // records handed out
+    uint32_t nrec;
+    uint64_t nslot;
 };
 
 #include "inflate_wave.hpp"
@@ -450,8 +468,8 @@ struct InflateScratch {
     void* d_cands = nullptr; size_t d_cands_cap = 0;
     void* d_stats = nullptr;
     void* d_q = nullptr; size_t d_q_cap = 0;           // finder survivors (stage 1 -> stage 2)
-    void* d_seg = nullptr; size_t d_seg_cap = 0;      // [slots][64] u64 starts, [slots][64] u32 counts, [slots] SegMeta
-    uint64_t seg_slots = 0;
+    void* d_seg = nullptr; size_t d_seg_cap = 0;      // segment record pool (SegPool)
+    SegPool pool{};
     void* d_chains = nullptr; size_t d_chains_cap = 0;
     void* d_off = nullptr; size_t d_off_cap = 0;
     void* d_done = nullptr; size_t d_done_cap = 0;
@@ -523,14 +541,21 @@ static int inflate_run(InflateScratch& S, hipStream_t s, const uint8_t* in, uint
     INF_CHK(hipMemsetAsync(d_cnt, 0, (uint64_t)nseg * 4, s));
     INF_CHK(hipEventRecord(S.ev[0], s));
     {
-        const uint64_t nthr = (nbits + 31) / 32;
+        // sparse windows: chains then span a few blocks (the count pass decodes on through
+        // boundaries that are not candidates); every window holds a block start unless blocks
+        // are longer than the gap, in which case chains just get longer
+        const uint64_t nw32 = (nbits + 31) / 32;
+        const uint32_t period = FIND_PERIOD_WORDS, win = FIND_WIN_WORDS;
+        const uint64_t nwin = (nw32 + period - 1) / period;
+        const uint64_t nthr = nw32 <= (uint64_t)period ? nw32 : (nwin - 1) * win + std::min<uint64_t>(win, nw32 - (nwin - 1) * period);
         const uint32_t qcap = (uint32_t)std::min<uint64_t>(0x7FFFFFFFull, nbits / 256 + 65536);
         INF_CHK(inf_ensure(&S.d_q, &S.d_q_cap, (uint64_t)qcap * 8 + 64));
         uint32_t* d_qcount = (uint32_t*)S.d_stats + 8;
         uint64_t* d_qlist = (uint64_t*)((char*)S.d_q + 64);
         if (nthr) {
+            const bool dense = nw32 <= (uint64_t)period;
             hipLaunchKernelGGL(ndfl_inflate_find_kernel, dim3((uint32_t)((nthr + 255) / 256)), dim3(256), 0, s, d_w,
-                               nwords, nbits, d_qlist, d_qcount, qcap);
+                               nwords, nbits, d_qlist, d_qcount, qcap, dense ? 1u : win, dense ? 1u : period);
             INF_CHK(hipGetLastError());
             hipLaunchKernelGGL(ndfl_inflate_strict_kernel, dim3(2048), dim3(256), 0, s, d_w, nwords, nbits,
                                (const uint64_t*)d_qlist, (const uint32_t*)d_qcount, qcap, d_cnt, d_list);
@@ -569,15 +594,22 @@ static int inflate_run(InflateScratch& S, hipStream_t s, const uint8_t* in, uint
     INF_CHK(inf_ensure(&S.d_cands, &S.d_cands_cap, (ncand + 1) * 8ull));
     INF_CHK(hipMemcpyAsync(S.d_cands, sorted_cand.data(), ncand * 8ull, hipMemcpyHostToDevice, s));
     const uint64_t limit = std::min(end_bit, nbits);
-    // segment records: one slot per counted chain start (index in `starts`), with room for repairs
+    // segment records: a pool for the rounds of all chains, one head per counted chain start (index
+    // in `starts`), with room for repairs
     const uint64_t nslot = starts.size() + std::max<uint64_t>(4096, starts.size() / 2);
-    const uint64_t seg_bytes = nslot * (64 * 8 + 64 * 4 + sizeof(SegMeta));
+    const uint64_t nrec = std::min<uint64_t>(0xFFFFFFF0ull, 2 * starts.size() + nbits / (1u << 17) + 65536);
+    const uint64_t seg_bytes = nrec * (64 * 8 + 64 * 4 + sizeof(SegMeta)) + nslot * 4;
     INF_CHK(inf_ensure(&S.d_seg, &S.d_seg_cap, seg_bytes));
-    S.seg_slots = nslot;
-    uint64_t* d_seg_start = (uint64_t*)S.d_seg;
-    uint32_t* d_seg_cnt = (uint32_t*)(d_seg_start + nslot * 64);
-    SegMeta* d_seg_meta = (SegMeta*)(d_seg_cnt + nslot * 64);
-    INF_CHK(hipMemsetAsync(d_seg_meta, 0, nslot * sizeof(SegMeta), s));
+    SegPool pool;
+    pool.start = (uint64_t*)S.d_seg;
+    pool.cnt = (uint32_t*)(pool.start + nrec * 64);
+    pool.meta = (SegMeta*)(pool.cnt + nrec * 64);
+    pool.head = (uint32_t*)(pool.meta + nrec);
+    pool.ctr = (uint32_t*)S.d_stats + 12;
+    pool.nrec = (uint32_t)nrec;
+    pool.nslot = nslot;
+    S.pool = pool;
+    INF_CHK(hipMemsetAsync(pool.head, 0xFF, nslot * 4, s));
 
     auto next_after = [&](uint64_t b) -> uint64_t {
         auto ub = std::upper_bound(sorted_cand.begin(), sorted_cand.end(), b);
@@ -589,7 +621,7 @@ static int inflate_run(InflateScratch& S, hipStream_t s, const uint8_t* in, uint
         const uint64_t slot_base = starts.size() - (&st == &starts ? st.size() : 0);
         const size_t n = st.size();
         std::vector<uint64_t> sp(n);
-        for (size_t k = 0; k < n; k++) sp[k] = next_after(st[k]);
+        for (size_t k = 0; k < n; k++) sp[k] = end_bit;     // chains stop at exact candidates (kernel)
         INF_CHK(inf_ensure(&S.d_starts, &S.d_starts_cap, n * 8));
         INF_CHK(inf_ensure(&S.d_stops, &S.d_stops_cap, n * 8));
         INF_CHK(inf_ensure(&S.d_res, &S.d_res_cap, n * sizeof(ChainRes)));
@@ -599,7 +631,7 @@ static int inflate_run(InflateScratch& S, hipStream_t s, const uint8_t* in, uint
         hipLaunchKernelGGL(ndfl_inflate_count_wave_kernel, dim3((uint32_t)n), dim3(64), 0, s, d_w, nwords, nbits,
                            (const uint64_t*)S.d_starts, (const uint64_t*)S.d_stops, (uint32_t)n,
                            (const uint64_t*)S.d_cands, ncand, limit, (ChainRes*)S.d_res, (uint32_t*)S.d_stats,
-                           slot_base, nslot, d_seg_start, d_seg_cnt, d_seg_meta);
+                           slot_base, pool);
         INF_CHK(hipGetLastError());
         if (S.count_first) { INF_CHK(hipEventRecord(S.ev[3], s)); S.count_first = false; }
         r.resize(n);
@@ -714,8 +746,7 @@ static int inflate_run(InflateScratch& S, hipStream_t s, const uint8_t* in, uint
     hipLaunchKernelGGL(ndfl_inflate_emit_wave_kernel, dim3(nch), dim3(64), 0, s, d_w, nwords, nbits,
                        (const EmitChain*)S.d_chains, (const uint64_t*)S.d_off, nch, (uint32_t*)S.d_done,
                        (uint32_t*)S.d_ticket, d_out, (ChainRes*)S.d_res, (const uint64_t*)S.d_cands, ncand, dict_len,
-                       deferred ? (uint32_t*)S.d_taint : (uint32_t*)nullptr, (const uint32_t*)nullptr, nslot,
-                       (const uint64_t*)d_seg_start, (const uint32_t*)d_seg_cnt, (const SegMeta*)d_seg_meta);
+                       deferred ? (uint32_t*)S.d_taint : (uint32_t*)nullptr, (const uint32_t*)nullptr, pool);
     INF_CHK(hipGetLastError());
     INF_CHK(hipEventRecord(e3, s));
     std::vector<ChainRes> er(nch);
@@ -774,9 +805,7 @@ static int inflate_resolve(InflateScratch& S, hipStream_t s, uint64_t* n_reemitt
     hipLaunchKernelGGL(ndfl_inflate_emit_wave_kernel, dim3(nsel), dim3(64), 0, s, S.p_w, S.p_nwords, S.p_nbits,
                        (const EmitChain*)S.d_chains, (const uint64_t*)S.d_off, nsel, (uint32_t*)S.d_done,
                        (uint32_t*)S.d_ticket, S.p_out, (ChainRes*)S.d_res, (const uint64_t*)S.d_cands, S.p_ncand,
-                       S.p_dict_len, (uint32_t*)nullptr, (const uint32_t*)S.d_sel, S.seg_slots,
-                       (const uint64_t*)S.d_seg, (const uint32_t*)((const uint64_t*)S.d_seg + S.seg_slots * 64),
-                       (const SegMeta*)((const uint32_t*)((const uint64_t*)S.d_seg + S.seg_slots * 64) + S.seg_slots * 64));
+                       S.p_dict_len, (uint32_t*)nullptr, (const uint32_t*)S.d_sel, S.pool);
     INF_CHK(hipGetLastError());
     INF_CHK(hipStreamSynchronize(s));
     return 0;

@@ -550,6 +550,13 @@ __device__ __forceinline__ uint64_t wave_excl_u64(uint64_t v, int lane) {
     return x - v;
 }
 
+// Is b one of the header candidates (sorted list)?
+__device__ __forceinline__ bool is_cand(const uint64_t* cands, uint32_t ncand, uint64_t b) {
+    uint32_t lo = 0, hi = ncand;
+    while (lo < hi) { const uint32_t mid = (lo + hi) >> 1; if (cands[mid] < b) lo = mid + 1; else hi = mid; }
+    return lo < ncand && cands[lo] == b;
+}
+
 // Next header candidate strictly after b (sorted list), capped at `limit`.
 __device__ __forceinline__ uint64_t next_cand(const uint64_t* cands, uint32_t ncand, uint64_t b, uint64_t limit) {
     uint32_t lo = 0, hi = ncand;
@@ -651,8 +658,7 @@ __device__ __forceinline__ void wcopy(WLane& L, gu8* out, uint64_t dst, uint64_t
 extern "C" __global__ void __launch_bounds__(64)
 ndfl_inflate_count_wave_kernel(const uint32_t* w, uint64_t nwords, uint64_t nbits, const uint64_t* starts,
                                const uint64_t* stops, uint32_t nchains, const uint64_t* cands, uint32_t ncand,
-                               uint64_t limit, ChainRes* res, uint32_t* stats, uint64_t slot_base, uint64_t nslot,
-                               uint64_t* seg_start, uint32_t* seg_cnt, SegMeta* seg_meta) {
+                               uint64_t limit, ChainRes* res, uint32_t* stats, uint64_t slot_base, SegPool pool) {
     using namespace wv;
     __shared__ Shared S;
     const int lane = threadIdx.x;
@@ -662,8 +668,13 @@ ndfl_inflate_count_wave_kernel(const uint32_t* w, uint64_t nwords, uint64_t nbit
     const uint64_t start = starts[c], stop = stops[c];
     uint64_t cur = start, total = 0, endpos = start;
     uint32_t status = ST_BOUNDARY, reason = 0, nslow = 0, nfix = 0, nround = 0;
+    bool recording = slot_base + c < pool.nslot;
+    uint32_t prev_rec = NOREC;
+    uint64_t span_est = 1ull << 18;             // round span: the previous block's size once known
     for (int blk = 0;; blk++) {
-        if (blk > 0 && cur >= stop) { status = ST_BOUNDARY; endpos = cur; break; }
+        // a chain ends at the first later block boundary that is itself a header candidate (its own
+        // chain links on from there) or at the range end; false candidates are passed over
+        if (blk > 0 && (cur >= stop || is_cand(cands, ncand, cur))) { status = ST_BOUNDARY; endpos = cur; break; }
         for (uint32_t s = (uint32_t)lane; s < 320; s += 64) S.lens[s] = 0;
         __syncthreads();
         if (lane == 0) parse_hdr(in, cur, S);
@@ -685,27 +696,36 @@ ndfl_inflate_count_wave_kernel(const uint32_t* w, uint64_t nwords, uint64_t nbit
         uint64_t rs = d0;
         bool block_done = false, chain_done = false;
         while (!block_done) {
-            uint64_t E = min(next_cand(cands, ncand, rs, limit), rs + MAX_SPAN);
+            uint64_t E = min(next_cand(cands, ncand, rs, limit), rs + min(span_est, MAX_SPAN));
             if (E <= rs) E = rs + 1;
             Seg r;
             uint32_t ft;
             round_decode(in, S.t, ed, rs, E, S, lane, r, ft, nslow, nfix);
-            if (blk == 0 && nround == 0 && slot_base + c < nslot) {
-                // record the exact segments for the emit pass
+            if (recording) {
+                // record the exact segments of this round for the emit pass
                 const bool live = (uint32_t)lane <= ft;
+                uint32_t idx = NOREC;
                 if (__all(!live || r.cnt < 0xFFFFFFFFull)) {
-                    const uint64_t slot = slot_base + c;
-                    seg_start[slot * 64 + lane] = r.start;
-                    seg_cnt[slot * 64 + lane] = (uint32_t)r.cnt;
+                    if (lane == 0) idx = atomicAdd(pool.ctr, 1u);
+                    idx = __shfl(idx, 0, 64);
+                }
+                if (idx < pool.nrec) {
+                    pool.start[(uint64_t)idx * 64 + lane] = r.start;
+                    pool.cnt[(uint64_t)idx * 64 + lane] = (uint32_t)r.cnt;
                     const int src = ft < 64 ? (int)ft : 63;
                     const uint64_t fe = __shfl((unsigned long long)r.end, src, 64);
                     const uint32_t fk = __shfl(r.kind, src, 64), fr = __shfl(r.reason, src, 64);
                     if (lane == 0) {
                         SegMeta m;
-                        m.valid = 1; m.ft = ft; m.kind_ft = fk; m.reason_ft = fr;
+                        m.ft = ft; m.kind_ft = fk; m.reason_ft = fr; m.next = NOREC;
                         m.end_ft = fe; m.exit63 = fe;
-                        seg_meta[slot] = m;
+                        pool.meta[idx] = m;
+                        if (prev_rec == NOREC) pool.head[slot_base + c] = idx;
+                        else pool.meta[prev_rec].next = idx;
                     }
+                    prev_rec = idx;
+                } else {
+                    recording = false;          // the emit pass re-derives the remaining rounds
                 }
             }
             nround++;
@@ -716,6 +736,7 @@ ndfl_inflate_count_wave_kernel(const uint32_t* w, uint64_t nwords, uint64_t nbit
                 block_done = true;
                 if (fk == T_ERR) { status = ST_ERROR; reason = fr; endpos = fe; chain_done = true; }
                 else {
+                    span_est = max((fe - d0) + ((fe - d0) >> 3), (uint64_t)4096);
                     cur = fe;
                     if (bfinal) { status = ST_FINAL; endpos = cur; chain_done = true; }
                 }
@@ -738,8 +759,7 @@ extern "C" __global__ void __launch_bounds__(64)
 ndfl_inflate_emit_wave_kernel(const uint32_t* w, uint64_t nwords, uint64_t nbits, const EmitChain* chains,
                               const uint64_t* chain_off, uint32_t nlist, uint32_t* done, uint32_t* ticket,
                               uint8_t* out, ChainRes* res, const uint64_t* cands, uint32_t ncand, uint64_t dict_len,
-                              uint32_t* taint, const uint32_t* sel, uint64_t nslot, const uint64_t* seg_start,
-                              const uint32_t* seg_cnt, const SegMeta* seg_meta) {
+                              uint32_t* taint, const uint32_t* sel, SegPool pool) {
     using namespace wv;
     __shared__ Shared S;
     __shared__ uint32_t s_ticket;
@@ -757,6 +777,7 @@ ndfl_inflate_emit_wave_kernel(const uint32_t* w, uint64_t nwords, uint64_t nbits
     uint64_t endpos = ch.start_bit;
     bool tainted = false;
     uint32_t nslow = 0, nfix = 0;
+    uint32_t rec = ch.slot < pool.nslot ? pool.head[ch.slot] : NOREC;
     for (int blk = 0;; blk++) {
         if (blk > 0 && cur == ch.end_bit) { status = ST_BOUNDARY; endpos = cur; break; }
         for (uint32_t s = (uint32_t)lane; s < 320; s += 64) S.lens[s] = 0;
@@ -788,16 +809,16 @@ ndfl_inflate_emit_wave_kernel(const uint32_t* w, uint64_t nwords, uint64_t nbits
         if (te) { status = ST_ERROR; reason = (uint32_t)te; endpos = d0; break; }
         uint64_t rs = d0;
         bool block_done = false, chain_done = false;
-        bool first_round = blk == 0;
         while (!block_done) {
             Seg r;
             uint32_t ft;
-            if (first_round && ch.slot < nslot && seg_meta[ch.slot].valid) {
+            if (rec != NOREC) {
                 // exact segments from the count pass
-                const SegMeta m = seg_meta[ch.slot];
+                const SegMeta m = pool.meta[rec];
                 ft = m.ft;
-                r.start = seg_start[ch.slot * 64 + lane];
-                r.cnt = seg_cnt[ch.slot * 64 + lane];
+                r.start = pool.start[(uint64_t)rec * 64 + lane];
+                r.cnt = pool.cnt[(uint64_t)rec * 64 + lane];
+                rec = m.next;
                 const uint64_t nx = __shfl_down((unsigned long long)r.start, 1, 64);
                 r.end = lane < 63 ? nx : m.exit63;
                 r.kind = T_EXIT; r.reason = 0;
@@ -807,7 +828,6 @@ ndfl_inflate_emit_wave_kernel(const uint32_t* w, uint64_t nwords, uint64_t nbits
                 if (E <= rs) E = rs + 1;
                 round_decode(in, S.t, ed, rs, E, S, lane, r, ft, nslow, nfix);
             }
-            first_round = false;
             // offsets of this round's lanes
             const bool live = (uint32_t)lane <= ft;
             const uint64_t mycnt = live ? r.cnt : 0ull;
