@@ -25,6 +25,7 @@
 // first error in stream order wins.
 // D/ = /root/reference/src/io/nayuki/deflate/
 #pragma once
+#include "kraft_bits.hpp"
 #include "ndfl_common.hpp"
 #include <vector>
 #include <algorithm>
@@ -63,6 +64,7 @@ constexpr uint64_t IN_PAD = 256;           // zero bytes after the staged input
 // in the count/emit passes' load balance than it saves here.
 constexpr uint32_t FIND_WIN_WORDS = 32768;
 constexpr uint32_t FIND_PERIOD_WORDS = 32768;
+constexpr uint32_t FIND_WPT = 8;                 // finder: input words per thread
 
 struct In {
     const uint32_t* w;
@@ -305,79 +307,68 @@ __device__ bool strict_stored(const In& in, uint64_t p) {
 }  // namespace inf
 
 // Header finder over every bit position, stage 1 (quick filter).  Each thread tests 32 consecutive
-// positions: btype masks for all 32 come from two shifts of a 64-bit window.  Dynamic headers need
-// a complete code-length code (Kraft sum exactly 1 over the HCLEN+4 3-bit lengths, >= 2 codes):
-// the 19 lengths are read as six 9-bit groups + one, each group's Kraft sum and nonzero count
-// from a 512-entry LDS table.  Stored headers need zero padding and LEN == ~NLEN.  Survivors
-// (about 1 in 1000 positions) go to a global list for the strict stage.
+// positions at once, bit-sliced (bit i of every vector = position p0 + i): BTYPE from two shifts of
+// the input; dynamic headers need a complete code-length code (Kraft sum exactly 1 over the
+// HCLEN+4 3-bit lengths -- kraft_bits.hpp, generated); stored headers need LEN == ~NLEN at the
+// next byte boundary (one test per byte position) and zero padding.  Survivors (about 1 in 1000
+// positions) go to a global list for the strict stage.
 extern "C" __global__ void __launch_bounds__(256)
 ndfl_inflate_find_kernel(const uint32_t* w, uint64_t nwords, uint64_t nbits, uint64_t* qlist, uint32_t* qcount,
                          uint32_t qcap, uint32_t win_words, uint32_t period_words) {
     using namespace inf;
-    __shared__ uint32_t lut[512];            // kraft (x128) | nonzero count << 16 for 3 lengths
-    __shared__ uint64_t cand[1024];
+    __shared__ uint64_t cand[2048];
     __shared__ uint32_t ncand, gbase;
-    for (uint32_t v = threadIdx.x; v < 512; v += 256) {
-        uint32_t k = 0, nz = 0;
-        for (int f = 0; f < 3; f++) { const uint32_t l = (v >> (3 * f)) & 7u; if (l) { k += 128u >> l; nz++; } }
-        lut[v] = k | (nz << 16);
-    }
     if (threadIdx.x == 0) ncand = 0;
     __syncthreads();
     // scanned windows: win_words of every period_words input words (win == period: every position)
-    const uint64_t tt = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    // (FIND_WPT words per thread, so that one group's survivors cost one global atomic)
+    In in{w, nwords, nbits};
+    for (uint32_t kk = 0; kk < FIND_WPT; kk++) {
+    const uint64_t tt = ((uint64_t)blockIdx.x * FIND_WPT + kk) * blockDim.x + threadIdx.x;
     const uint64_t t = (tt / win_words) * period_words + tt % win_words;     // input word index
     const uint64_t p0 = t * 32;
-    In in{w, nwords, nbits};
     if (p0 < nbits) {
-        const uint32_t w0 = in.ld(t), w1 = in.ld(t + 1), w2 = in.ld(t + 2), w3 = in.ld(t + 3), w4 = in.ld(t + 4);
+        const uint32_t w0 = in.ld(t), w1 = in.ld(t + 1), w2 = in.ld(t + 2), w3 = in.ld(t + 3);
         const uint64_t W = (uint64_t)w0 | ((uint64_t)w1 << 32);
         const uint32_t b1 = (uint32_t)(W >> 1), b2 = (uint32_t)(W >> 2);
         uint32_t valid = 0xFFFFFFFFu;
         if (p0 + 35 > nbits) valid = (nbits >= p0 + 3) ? (uint32_t)((1ull << (nbits - p0 - 2)) - 1) : 0u;
-        uint32_t m2 = ~b1 & b2 & valid;
-        uint32_t m0 = ~b1 & ~b2 & valid;
-        const uint64_t lo = W, hi = (uint64_t)w2 | ((uint64_t)w3 << 32);
-        const uint64_t hw = (uint64_t)w3 | ((uint64_t)w4 << 32);
+        uint32_t m2 = ~b1 & b2 & valid & kraft_complete_mask(w0, w1, w2, w3);
+        // LEN == ~NLEN at byte positions p0 + 8j, j = 1..5; position i pads to j = (i + 10) / 8
+        const uint64_t W12 = (uint64_t)w1 | ((uint64_t)w2 << 32);
+        const uint32_t x1 = (uint32_t)(W >> 8), x2 = (uint32_t)(W >> 16), x3 = (uint32_t)(W >> 24), x4 = w1,
+                       x5 = (uint32_t)(W12 >> 8);
+#define NDFL_LENOK(x) ((((x) ^ ((x) >> 16)) & 0xFFFFu) == 0xFFFFu)
+        const uint32_t okm = (NDFL_LENOK(x1) ? 0x0000003Fu : 0u) | (NDFL_LENOK(x2) ? 0x00003FC0u : 0u) |
+                             (NDFL_LENOK(x3) ? 0x003FC000u : 0u) | (NDFL_LENOK(x4) ? 0x3FC00000u : 0u) |
+                             (NDFL_LENOK(x5) ? 0xC0000000u : 0u);
+#undef NDFL_LENOK
+        uint32_t m0 = ~b1 & ~b2 & valid & okm;
         while (m2) {
             const uint32_t o = __builtin_ctz(m2);
             m2 &= m2 - 1;
-            // 96 bits starting at position o: x0 = bits [o, o+64), x1 = bits [o+64, o+96)
-            const uint64_t x0 = o ? (lo >> o) | (hi << (64 - o)) : lo;
-            const uint32_t x1 = (uint32_t)((o ? (hi >> o) | (hw << (64 - o)) : hi));
-            const uint32_t nf3 = 3 * (((uint32_t)(x0 >> 13) & 15u) + 4);      // bits of lengths present
-            uint32_t acc = 0;
-#pragma unroll
-            for (int k = 0; k < 6; k++) {
-                const int off = 17 + 9 * k;
-                const uint32_t g = (off + 9 <= 64) ? (uint32_t)(x0 >> off) & 0x1FFu
-                                                   : ((uint32_t)(x0 >> off) | (x1 << (64 - off))) & 0x1FFu;
-                const int vb = (int)nf3 - 9 * k;
-                const uint32_t mask = vb >= 9 ? 0x1FFu : vb <= 0 ? 0u : (1u << vb) - 1u;
-                acc += lut[g & mask];
-            }
-            if (nf3 == 57) acc += lut[(x1 >> 7) & 7u];
-            if ((acc & 0xFFFFu) == 128u && (acc >> 16) >= 2u && p0 + o + 17 + nf3 <= nbits) {
+            const uint32_t nf3 = 3 * (((uint32_t)(W >> (o + 13)) & 15u) + 4);
+            if (p0 + o + 17 + nf3 <= nbits) {
                 uint32_t k = atomicAdd(&ncand, 1u);
-                if (k < 1024) cand[k] = (p0 + o) | (1ull << 63);
+                if (k < 2048) cand[k] = (p0 + o) | (1ull << 63);
             }
         }
         while (m0) {
             const uint32_t o = __builtin_ctz(m0);
             m0 &= m0 - 1;
             const uint32_t q = o + 3, al = (q + 7) & ~7u;            // al <= 40
-            const uint64_t x = al ? (lo >> al) | (hi << (64 - al)) : lo;
-            const uint32_t pad = al > q ? (uint32_t)(lo >> q) & ((1u << (al - q)) - 1u) : 0u;
+            const uint32_t pad = al > q ? (uint32_t)(W >> q) & ((1u << (al - q)) - 1u) : 0u;
             if (pad) continue;
-            const uint32_t ln = (uint32_t)x & 0xFFFFu, nln = (uint32_t)(x >> 16) & 0xFFFFu;
-            if (ln == (nln ^ 0xFFFFu) && p0 + al + 32 + 8ull * ln <= nbits) {
+            const uint32_t ln = (al < 32 ? (uint32_t)(W >> al) : (uint32_t)(W12 >> (al - 32))) & 0xFFFFu;
+            if (p0 + al + 32 + 8ull * ln <= nbits) {
                 uint32_t k = atomicAdd(&ncand, 1u);
-                if (k < 1024) cand[k] = p0 + o;
+                if (k < 2048) cand[k] = p0 + o;
             }
         }
     }
+    }
     __syncthreads();
-    const uint32_t nc = min(ncand, 1024u);
+    const uint32_t nc = min(ncand, 2048u);
     if (threadIdx.x == 0) gbase = nc ? atomicAdd(qcount, nc) : 0u;
     __syncthreads();
     for (uint32_t k = threadIdx.x; k < nc; k += blockDim.x)
@@ -554,7 +545,7 @@ static int inflate_run(InflateScratch& S, hipStream_t s, const uint8_t* in, uint
         uint64_t* d_qlist = (uint64_t*)((char*)S.d_q + 64);
         if (nthr) {
             const bool dense = nw32 <= (uint64_t)period;
-            hipLaunchKernelGGL(ndfl_inflate_find_kernel, dim3((uint32_t)((nthr + 255) / 256)), dim3(256), 0, s, d_w,
+            hipLaunchKernelGGL(ndfl_inflate_find_kernel, dim3((uint32_t)((nthr + 256 * FIND_WPT - 1) / (256 * FIND_WPT))), dim3(256), 0, s, d_w,
                                nwords, nbits, d_qlist, d_qcount, qcap, dense ? 1u : win, dense ? 1u : period);
             INF_CHK(hipGetLastError());
             hipLaunchKernelGGL(ndfl_inflate_strict_kernel, dim3(2048), dim3(256), 0, s, d_w, nwords, nbits,
