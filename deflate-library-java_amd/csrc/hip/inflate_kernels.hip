@@ -275,7 +275,7 @@ __device__ bool strict_dynamic(const In& in, uint64_t p) {
 
 // A stored block at p (LEN == ~NLEN already checked) must be final or be followed by a plausible
 // header: not btype 3; stored -> LEN == ~NLEN; dynamic -> complete code-length code.
-__device__ bool strict_stored(const In& in, uint64_t p) {
+__device__ __noinline__ bool strict_stored(const In& in, uint64_t p) {
     Rd rd; rd.init(in, p);
     const uint32_t bf = rd.get(in, 1);
     const uint64_t al = (p + 3 + 7) & ~7ull;
@@ -375,22 +375,185 @@ ndfl_inflate_find_kernel(const uint32_t* w, uint64_t nwords, uint64_t nbits, uin
         if (gbase + k < qcap) qlist[gbase + k] = cand[k];
 }
 
-// Stage 2: the reference's own header checks on every survivor, one lane each (grid-stride);
-// accepted headers go to their 64 KiB segment's list.
+namespace inf {
+// strict-stage reader: 64-bit buffer, the next 16-byte group always in flight
+struct SRd {
+    uint64_t bb, pos, qw;
+    uint32_t bn, ci;
+    u32x4 cur, nxt;
+    __device__ __forceinline__ static uint32_t pick(const u32x4& v, uint32_t i) {
+        uint32_t a = (i & 1) ? v.y : v.x, b = (i & 1) ? v.w : v.z;
+        return (i & 2) ? b : a;
+    }
+    __device__ __forceinline__ void adv(const In& in) {
+        if (++ci == 4) {
+            ci = 0;
+            qw++;
+            cur = nxt;
+            asm volatile("" : "+v"(cur) :: "memory");
+            nxt = in.ld4(qw + 1);
+        }
+    }
+    __device__ __forceinline__ void fill(const In& in) {
+        if (bn <= 32) { bb |= (uint64_t)pick(cur, ci) << bn; bn += 32; adv(in); }
+    }
+    __device__ __forceinline__ void init(const In& in, uint64_t p) {
+        pos = p;
+        qw = p >> 7;
+        cur = in.ld4(qw);
+        nxt = in.ld4(qw + 1);
+        ci = (uint32_t)(p >> 5) & 3u;
+        bb = (uint64_t)(pick(cur, ci) >> (p & 31));
+        bn = 32 - (uint32_t)(p & 31);
+        adv(in);
+        fill(in);
+    }
+    __device__ __forceinline__ uint32_t peek(uint32_t n) const { return (uint32_t)bb & ((1u << n) - 1u); }
+    __device__ __forceinline__ void skip(uint32_t n) { bb >>= n; bn -= n; pos += n; }
+    __device__ __forceinline__ uint32_t get(const In& in, uint32_t n) {
+        fill(in);
+        const uint32_t v = peek(n);
+        skip(n);
+        return v;
+    }
+};
+}  // namespace inf
+
+// Stage 2: the reference's own header checks (as strict_dynamic / strict_stored) on every
+// survivor.  Each wave takes a contiguous slice of the survivor list; a lane that finishes its
+// header takes the next one (refills are batched: at least 16 idle lanes), so short and long
+// headers do not hold each other.  Dynamic headers decode the code lengths one symbol per step
+// through a per-lane 128-entry table of the code-length code (LDS, indexed by the next 7 bits
+// MSB first: canonical codes fill it in (length, symbol) order).  Accepted headers go to their
+// 64 KiB segment's list.
 extern "C" __global__ void __launch_bounds__(256)
 ndfl_inflate_strict_kernel(const uint32_t* w, uint64_t nwords, uint64_t nbits, const uint64_t* qlist,
                            const uint32_t* qcount, uint32_t qcap, uint32_t* seg_cnt, uint64_t* seg_list) {
     using namespace inf;
+    __shared__ uint4 tabs[256 * 8];                          // 128 bytes per lane
+    uint8_t* tab = (uint8_t*)&tabs[threadIdx.x * 8];
     const uint32_t n = min(*qcount, qcap);
     In in{w, nwords, nbits};
-    for (uint32_t k = blockIdx.x * blockDim.x + threadIdx.x; k < n; k += gridDim.x * blockDim.x) {
-        const uint64_t e = qlist[k];
-        const uint64_t p = e & ~(1ull << 63);
-        const bool ok = (e >> 63) ? strict_dynamic(in, p) : strict_stored(in, p);
-        if (ok) {
-            const uint32_t seg = (uint32_t)(p / ((uint64_t)SEG_BYTES * 8));
-            uint32_t idx = atomicAdd(&seg_cnt[seg], 1u);
-            if (idx < SEG_CAP) seg_list[(uint64_t)seg * SEG_CAP + idx] = p;
+    const uint32_t lane = threadIdx.x & 63u;
+    const uint64_t nw = (uint64_t)gridDim.x * (blockDim.x / 64);
+    const uint64_t wid = (uint64_t)blockIdx.x * (blockDim.x / 64) + threadIdx.x / 64;
+    const uint32_t end = (uint32_t)((uint64_t)n * (wid + 1) / nw);
+    uint32_t next = (uint32_t)((uint64_t)n * wid / nw);
+    const uint64_t below = (1ull << lane) - 1ull;
+    auto record = [&](uint64_t p) {
+        const uint32_t seg = (uint32_t)(p / ((uint64_t)SEG_BYTES * 8));
+        const uint32_t idx = atomicAdd(&seg_cnt[seg], 1u);
+        if (idx < SEG_CAP) seg_list[(uint64_t)seg * SEG_CAP + idx] = p;
+    };
+    bool active = false;
+    uint64_t p = 0;
+    SRd rd;
+    rd.bb = 0; rd.pos = 0; rd.qw = 0; rd.bn = 0; rd.ci = 0;
+    uint32_t i = 0, total = 0, numLit = 0, numDist = 0, litK = 0, distK = 0, ones = 0, other = 0, eob = 0, d0 = 0,
+             d31 = 0;
+    int runVal = -1;
+    for (;;) {
+        const uint64_t idle = __ballot(!active);
+        const uint32_t nidle = (uint32_t)__popcll(idle);
+        if (next < end && nidle >= 16) {
+            if (!active) {
+                const uint32_t k = next + (uint32_t)__popcll(idle & below);
+                if (k < end) {
+                    const uint64_t e = qlist[k];
+                    p = e & ~(1ull << 63);
+                    if (!(e >> 63)) {
+                        if (strict_stored(in, p)) record(p);
+                    } else {
+                        rd.init(in, p + 3);
+                        const uint32_t hlit = rd.get(in, 5), hdist = rd.get(in, 5), hclen = rd.get(in, 4);
+                        numLit = hlit + 257; numDist = hdist + 1; total = numLit + numDist;
+                        const uint32_t numCl = hclen + 4;
+                        uint32_t cl[19];
+#pragma unroll
+                        for (int j = 0; j < 19; j++) cl[j] = 0;
+#pragma unroll
+                        for (int j = 0; j < 19; j++)
+                            if ((uint32_t)j < numCl) cl[CLO[j]] = rd.get(in, 3);
+                        // the stage-1 test guarantees a complete code: the runs fill all 128 entries
+                        uint32_t pos = 0;
+#pragma unroll 1
+                        for (uint32_t l = 1; l < 8; l++) {
+                            const uint32_t run = 128u >> l;
+#pragma unroll
+                            for (int sy = 0; sy < 19; sy++) {
+                                if (cl[sy] == l) {
+                                    const uint32_t v = ((uint32_t)sy | (l << 5)) * 0x01010101u;
+                                    if (run >= 16) {
+                                        for (uint32_t r = 0; r < run; r += 16) *(uint4*)(tab + pos + r) = make_uint4(v, v, v, v);
+                                    } else if (run == 8) {
+                                        *(uint2*)(tab + pos) = make_uint2(v, v);
+                                    } else if (run == 4) {
+                                        *(uint32_t*)(tab + pos) = v;
+                                    } else if (run == 2) {
+                                        *(uint16_t*)(tab + pos) = (uint16_t)v;
+                                    } else {
+                                        tab[pos] = (uint8_t)v;
+                                    }
+                                    pos += run;
+                                }
+                            }
+                        }
+                        i = 0; runVal = -1; litK = 0; distK = 0; ones = 0; other = 0; eob = 0; d0 = 0; d31 = 0;
+                        active = true;
+                    }
+                }
+            }
+            next = min(end, next + nidle);
+            continue;
+        }
+        if (!__any(active)) {
+            if (next >= end) break;
+            continue;
+        }
+        if (active) {
+            // one code-length symbol (D/decomp/Open.java's dynamic header loop, same checks)
+            rd.fill(in);
+            const uint32_t x = __builtin_bitreverse32(rd.peek(7)) >> 25;
+            const uint32_t te = tab[x];
+            const uint32_t sym = te & 31u;
+            rd.skip(te >> 5);
+            uint32_t run = 1;
+            bool bad = false;
+            if (sym < 16) runVal = (int)sym;
+            else if (sym == 16) { if (runVal < 0) bad = true; run = rd.get(in, 2) + 3; }
+            else if (sym == 17) { runVal = 0; run = rd.get(in, 3) + 3; }
+            else { runVal = 0; run = rd.get(in, 7) + 11; }
+            if (bad || i + run > total || rd.pos > in.nbits) {
+                active = false;
+            } else {
+                const uint32_t v = (uint32_t)runVal;
+                const uint32_t en = i + run;
+                if (i < numLit) {
+                    const uint32_t c = min(en, numLit) - i;
+                    if (v) { litK += c * (32768u >> v); if (litK > 32768u) active = false; }
+                    if (i <= 256 && 256 < en) eob = v;
+                }
+                if (en > numLit) {
+                    const uint32_t a0 = max(i, numLit) - numLit, b2 = en - numLit, c = b2 - a0;
+                    if (v) {
+                        distK += c * (32768u >> v);
+                        if (distK > 32768u) active = false;
+                        if (v == 1) ones += c; else other += c;
+                    }
+                    if (a0 == 0) d0 = v;
+                    if (a0 <= 31 && 31 < b2) d31 = v;
+                }
+                i = en;
+                if (active && i >= total) {
+                    active = false;
+                    bool ok;
+                    if (eob == 0 || litK != 32768u) ok = false;
+                    else if (numDist == 1 && d0 == 0) ok = true;
+                    else if (ones == 1 && other == 0) ok = !(numDist == 32 && d31 == 1);
+                    else ok = distK == 32768u;
+                    if (ok) record(p);
+                }
+            }
         }
     }
 }
