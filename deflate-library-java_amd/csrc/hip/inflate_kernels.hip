@@ -65,6 +65,7 @@ constexpr uint64_t IN_PAD = 256;           // zero bytes after the staged input
 constexpr uint32_t FIND_WIN_WORDS = 32768;
 constexpr uint32_t FIND_PERIOD_WORDS = 32768;
 constexpr uint32_t FIND_WPT = 8;                 // finder: input words per thread
+constexpr uint32_t COUNT_WAVES = 256 * 16;       // count pass: persistent waves
 
 struct In {
     const uint32_t* w;
@@ -630,6 +631,8 @@ struct InflateScratch {
     void* d_taint = nullptr; size_t d_taint_cap = 0;
     void* d_sel = nullptr; size_t d_sel_cap = 0;
     void* d_ticket = nullptr;
+    void* d_ph = nullptr;                             // count pass: phase-fallback slot per wave
+    void* d_cticket = nullptr;                        // count pass: chain tickets (one per launch)
     void* d_out = nullptr; size_t d_out_cap = 0;
     double last_ms_find = 0, last_ms_count = 0, last_ms_emit = 0, last_ms_wall = 0;
     hipEvent_t ev[6] = {nullptr, nullptr, nullptr, nullptr, nullptr, nullptr};
@@ -643,7 +646,7 @@ struct InflateScratch {
     uint32_t p_nch = 0, p_ncand = 0;
     void release() {
         void** ps[] = {&d_in, &d_cand, &d_starts, &d_stops, &d_res, &d_cands, &d_stats, &d_q, &d_seg, &d_chains, &d_off,
-                       &d_done, &d_taint, &d_sel, &d_ticket, &d_out};
+                       &d_done, &d_taint, &d_sel, &d_ticket, &d_ph, &d_cticket, &d_out};
         for (void** p : ps) { if (*p) hipFree(*p); *p = nullptr; }
         for (auto& e : ev) { if (e) hipEventDestroy(e); e = nullptr; }
         d_in_cap = d_cand_cap = d_starts_cap = d_stops_cap = d_res_cap = d_cands_cap = d_seg_cap = d_q_cap = d_chains_cap = 0;
@@ -685,8 +688,8 @@ static int inflate_run(InflateScratch& S, hipStream_t s, const uint8_t* in, uint
     if (in_len) INF_CHK(hipMemcpyAsync(S.d_in, in, in_len, (flags & 1u) ? hipMemcpyDeviceToDevice : hipMemcpyHostToDevice, s));
     INF_CHK(hipMemsetAsync((char*)S.d_in + in_len, 0, nwords * 4 + IN_PAD - in_len, s));
     const uint32_t* d_w = (const uint32_t*)S.d_in;
-    if (!S.d_stats) INF_CHK(hipMalloc(&S.d_stats, 64));
-    INF_CHK(hipMemsetAsync(S.d_stats, 0, 64, s));
+    if (!S.d_stats) INF_CHK(hipMalloc(&S.d_stats, 256));
+    INF_CHK(hipMemsetAsync(S.d_stats, 0, 256, s));
     if (!S.ev[0]) for (auto& e : S.ev) INF_CHK(hipEventCreate(&e));
     const uint32_t nseg = (uint32_t)std::max<uint64_t>(1, (in_len + SEG_BYTES - 1) / SEG_BYTES);
     INF_CHK(inf_ensure(&S.d_cand, &S.d_cand_cap, (uint64_t)nseg * SEG_CAP * 8ull + (uint64_t)nseg * 4 + 64));
@@ -770,6 +773,7 @@ static int inflate_run(InflateScratch& S, hipStream_t s, const uint8_t* in, uint
         const uint64_t nx = ub != sorted_cand.end() ? *ub : NONE;
         return std::min(nx, end_bit);
     };
+    static const bool stats_on = getenv("NDFL_STATS") != nullptr;
     std::vector<ChainRes> res;
     auto run_count = [&](const std::vector<uint64_t>& st, std::vector<ChainRes>& r) -> int {
         const uint64_t slot_base = starts.size() - (&st == &starts ? st.size() : 0);
@@ -781,11 +785,15 @@ static int inflate_run(InflateScratch& S, hipStream_t s, const uint8_t* in, uint
         INF_CHK(inf_ensure(&S.d_res, &S.d_res_cap, n * sizeof(ChainRes)));
         INF_CHK(hipMemcpyAsync(S.d_starts, st.data(), n * 8, hipMemcpyHostToDevice, s));
         INF_CHK(hipMemcpyAsync(S.d_stops, sp.data(), n * 8, hipMemcpyHostToDevice, s));
+        if (!S.d_ph) INF_CHK(hipMalloc(&S.d_ph, (size_t)COUNT_WAVES * sizeof(wv::PhArr)));
+        if (!S.d_cticket) INF_CHK(hipMalloc(&S.d_cticket, 64));
+        INF_CHK(hipMemsetAsync(S.d_cticket, 0, 4, s));
         if (S.count_first) INF_CHK(hipEventRecord(S.ev[2], s));
-        hipLaunchKernelGGL(ndfl_inflate_count_wave_kernel, dim3((uint32_t)n), dim3(64), 0, s, d_w, nwords, nbits,
+        hipLaunchKernelGGL(ndfl_inflate_count_wave_kernel, dim3((uint32_t)std::min<size_t>(n, COUNT_WAVES)), dim3(64), 0, s,
+                           d_w, nwords, nbits,
                            (const uint64_t*)S.d_starts, (const uint64_t*)S.d_stops, (uint32_t)n,
-                           (const uint64_t*)S.d_cands, ncand, limit, (ChainRes*)S.d_res, (uint32_t*)S.d_stats,
-                           slot_base, pool);
+                           (const uint64_t*)S.d_cands, ncand, limit, (ChainRes*)S.d_res, stats_on ? (uint32_t*)S.d_stats : nullptr,
+                           slot_base, pool, (uint32_t*)S.d_cticket, (wv::PhArr*)S.d_ph);
         INF_CHK(hipGetLastError());
         if (S.count_first) { INF_CHK(hipEventRecord(S.ev[3], s)); S.count_first = false; }
         r.resize(n);
@@ -864,12 +872,16 @@ static int inflate_run(InflateScratch& S, hipStream_t s, const uint8_t* in, uint
     S.chains = chains.size();
     S.candidates = sorted_cand.size();
     if (getenv("NDFL_STATS")) {
-        uint32_t st[16] = {0};
-        INF_CHK(hipMemcpy(st, S.d_stats, 64, hipMemcpyDeviceToHost));
+        uint32_t st[64] = {0};
+        INF_CHK(hipMemcpy(st, S.d_stats, 256, hipMemcpyDeviceToHost));
         st[4] = st[8];
         fprintf(stderr, "[ndfl] finder quick survivors %u; count pass: chains %zu candidates %zu repairs %llu "
                 "slow-verify lanes %u fixups %u rounds %u\n", st[4], chains.size(), sorted_cand.size(),
                 (unsigned long long)S.repairs, st[0], st[1], st[2]);
+        const uint64_t* t64 = (const uint64_t*)(st + 32);
+        fprintf(stderr, "[ndfl] count wave-time (ms x waves, 100 MHz clock): header %.1f spec %.1f verify %.1f phases %.1f "
+                "serial %.1f record %.1f build %.1f\n", t64[0] * 1e-5, t64[1] * 1e-5, t64[2] * 1e-5, t64[3] * 1e-5,
+                t64[4] * 1e-5, t64[5] * 1e-5, t64[6] * 1e-5);
     }
     const uint64_t total = off - dict_len;
     if (total > out_cap) { *out_len = total; return -3; }

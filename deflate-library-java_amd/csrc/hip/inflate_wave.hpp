@@ -49,18 +49,20 @@ struct Shared {
     Tabs t;
     uint8_t lens[320];                       // literal/length 0..287, distance at 288..319
     uint16_t cl_tab[128];                    // code-length code, full 7-bit table: sym | len << 9
-    uint32_t ph_cp[7][64];                   // fallback phases 1..7: checkpoint offset | bytes before it << 16
-    uint32_t ph_end[7][64];                  //   end offset,
-    uint32_t ph_cnt[7][64];                  //   bytes,
-    uint8_t ph_kr[7][64];                    //   kind << 5 | reason
     uint64_t exit_[64];
     uint32_t kind_[64];
-    uint64_t off_[64];                       // emit: absolute output offset per lane
-    uint64_t cnt_[64];                       // emit: output bytes per lane
-    uint32_t prog[64];                       // emit: bytes durably written per lane
     // header broadcast (lane 0 -> wave)
     uint64_t h_pos, h_d0;
     uint32_t h_err, h_bfinal, h_btype, h_len, h_numlit, h_numdist;
+};
+
+// phase-fallback results (phases 1..7) of one wave: per lane, written and read by that lane only,
+// so they may live in LDS (emit) or in a per-wave global slot (count)
+struct PhArr {
+    uint32_t cp[7][64];                      // checkpoint offset | bytes before it << 16
+    uint32_t end[7][64];                     // end offset
+    uint32_t cnt[7][64];                     // bytes
+    uint8_t kr[7][64];                       // kind << 5 | reason
 };
 
 __device__ __forceinline__ uint32_t lit_entry(uint32_t sym, uint32_t len) {
@@ -422,7 +424,7 @@ __device__ void spec_run(const RB& b, const Tabs& t, bool ed, uint32_t st, uint3
 // 1..nph-1 (LDS); at C2 with phase 0 again; on a match take that run's end state, otherwise
 // decode the rest of the segment (authoritative).  Returns true when it synchronised.
 __device__ bool verify_run(const RB& b, const Tabs& t, bool ed, uint32_t t0, uint32_t s, uint32_t C1, uint32_t C2,
-                           uint32_t e, const Spec& p0, const Shared& S, int lane, uint32_t nph, SegR& r) {
+                           uint32_t e, const Spec& p0, const PhArr* ph, int lane, uint32_t nph, SegR& r) {
     Rq rd;
     rd.init(b, t0);
     uint32_t c = 0, stage = 0;
@@ -438,11 +440,11 @@ __device__ bool verify_run(const RB& b, const Tabs& t, bool ed, uint32_t t0, uin
                 return true;
             }
             for (uint32_t f = 1; f < nph; f++) {
-                const uint32_t pc = S.ph_cp[f - 1][lane];
+                const uint32_t pc = ph->cp[f - 1][lane];
                 if ((pc & 0xFFFFu) == off) {
-                    r.end = s + S.ph_end[f - 1][lane];
-                    r.cnt = c + (S.ph_cnt[f - 1][lane] - (pc >> 16));
-                    const uint32_t kr = S.ph_kr[f - 1][lane];
+                    r.end = s + ph->end[f - 1][lane];
+                    r.cnt = c + (ph->cnt[f - 1][lane] - (pc >> 16));
+                    const uint32_t kr = ph->kr[f - 1][lane];
                     r.kind = kr >> 5; r.reason = kr & 31;
                     return true;
                 }
@@ -468,8 +470,13 @@ __device__ bool verify_run(const RB& b, const Tabs& t, bool ed, uint32_t t0, uin
 
 // One round over [rs, E) (E - rs <= MAX_SPAN): exact per-lane segments; first_term = first lane
 // ending the block (64: none).  All lanes call.
+struct PhaseClock {                            // count-pass phase times (wall clock ticks), wave-uniform
+    uint64_t hdr, spec, verify, phases, serial, rec, build;
+};
 __device__ void round_decode(const In& in, const Tabs& t, bool ed, uint64_t rs, uint64_t E, Shared& S, int lane,
-                             Seg& out, uint32_t& first_term, uint32_t& nslow, uint32_t& nfix) {
+                             Seg& out, uint32_t& first_term, uint32_t& nslow, uint32_t& nfix, PhArr* ph,
+                             PhaseClock* pc = nullptr) {
+    uint64_t tk0 = pc ? wall_clock64() : 0;
     const RB b = make_rb(in, rs);
     const uint32_t r0 = (uint32_t)(rs - b.base), re = (uint32_t)(E - b.base);
     const uint32_t span = re - r0;
@@ -481,16 +488,18 @@ __device__ void round_decode(const In& in, const Tabs& t, bool ed, uint64_t rs, 
     spec_run(b, t, ed, s, s, C1, C2, e, p0);
     S.exit_[lane] = p0.end;
     __syncthreads();
+    if (pc) { const uint64_t x = wall_clock64(); pc->spec += x - tk0; tk0 = x; }
     SegR r;
     bool fin;                                   // r is this lane's exact result
     if (lane == 0) {
         r.start = s; r.end = p0.end; r.cnt = p0.cnt; r.kind = p0.kind; r.reason = p0.reason;
         fin = true;
     } else {
-        fin = verify_run(b, t, ed, (uint32_t)S.exit_[lane - 1], s, C1, C2, e, p0, S, lane, 1, r);
+        fin = verify_run(b, t, ed, (uint32_t)S.exit_[lane - 1], s, C1, C2, e, p0, ph, lane, 1, r);
     }
     // exact prefix: lanes before the first unsynchronised lane
     const uint64_t um = __ballot(!fin);
+    if (pc) { const uint64_t x = wall_clock64(); pc->verify += x - tk0; tk0 = x; }
     const uint32_t j0 = um ? (uint32_t)__builtin_ctzll(um) : 64u;
     const uint64_t tm = __ballot(fin && r.kind != T_EXIT);
     const uint32_t t0 = tm ? (uint32_t)__builtin_ctzll(tm) : 64u;
@@ -506,15 +515,16 @@ __device__ void round_decode(const In& in, const Tabs& t, bool ed, uint64_t rs, 
                 Spec q;
                 spec_run(b, t, ed, min(s + f, e), s, C1, C1, e, q);
                 // (offsets and byte counts at the first checkpoint fit 16 bits; otherwise no match)
-                S.ph_cp[f - 1][lane] = (q.cp1 < 0xFFFFu && q.cpc1 <= 0xFFFFu) ? (q.cp1 | (q.cpc1 << 16)) : 0xFFFFu;
-                S.ph_end[f - 1][lane] = q.end - s;
-                S.ph_cnt[f - 1][lane] = q.cnt;
-                S.ph_kr[f - 1][lane] = (uint8_t)((q.kind << 5) | q.reason);
+                ph->cp[f - 1][lane] = (q.cp1 < 0xFFFFu && q.cpc1 <= 0xFFFFu) ? (q.cp1 | (q.cpc1 << 16)) : 0xFFFFu;
+                ph->end[f - 1][lane] = q.end - s;
+                ph->cnt[f - 1][lane] = q.cnt;
+                ph->kr[f - 1][lane] = (uint8_t)((q.kind << 5) | q.reason);
             }
         }
         S.exit_[lane] = r.end;
         S.kind_[lane] = r.kind;
         __syncthreads();
+        if (pc) { const uint64_t x = wall_clock64(); pc->phases += x - tk0; tk0 = x; }
         first_term = (r.kind != T_EXIT && (uint32_t)lane == j0) ? j0 : 64u;
         first_term = __shfl(first_term, (int)j0, 64);
         for (uint32_t j = j0 + 1; j < 64 && first_term == 64; j++) {
@@ -522,7 +532,7 @@ __device__ void round_decode(const In& in, const Tabs& t, bool ed, uint64_t rs, 
             if ((uint32_t)lane == j) {
                 const uint32_t st = (uint32_t)S.exit_[j - 1];
                 if (!(fin && st == r.start)) {
-                    verify_run(b, t, ed, st, s, C1, C2, e, p0, S, lane, nph, r);
+                    verify_run(b, t, ed, st, s, C1, C2, e, p0, ph, lane, nph, r);
                     S.exit_[lane] = r.end;
                     S.kind_[lane] = r.kind;
                 }
@@ -530,6 +540,7 @@ __device__ void round_decode(const In& in, const Tabs& t, bool ed, uint64_t rs, 
             __syncthreads();
             if (S.kind_[j] != T_EXIT) first_term = j;
         }
+        if (pc) { const uint64_t x = wall_clock64(); pc->serial += x - tk0; tk0 = x; }
     }
     out.start = b.base + r.start; out.end = b.base + r.end; out.cnt = r.cnt;
     out.kind = r.kind; out.reason = r.reason;
@@ -654,23 +665,34 @@ __device__ __forceinline__ void wcopy(WLane& L, gu8* out, uint64_t dst, uint64_t
 
 }  // namespace wv
 
-// Count pass: one wave per candidate chain.
-extern "C" __global__ void __launch_bounds__(64)
+// Count pass: persistent waves, each claiming candidate chains through `ticket`; the phase-fallback
+// arrays live in the wave's own global slot (ph_all[blockIdx.x]), keeping LDS to the tables.
+extern "C" __global__ void __launch_bounds__(64, 4)
 ndfl_inflate_count_wave_kernel(const uint32_t* w, uint64_t nwords, uint64_t nbits, const uint64_t* starts,
                                const uint64_t* stops, uint32_t nchains, const uint64_t* cands, uint32_t ncand,
-                               uint64_t limit, ChainRes* res, uint32_t* stats, uint64_t slot_base, SegPool pool) {
+                               uint64_t limit, ChainRes* res, uint32_t* stats, uint64_t slot_base, SegPool pool,
+                               uint32_t* ticket, wv::PhArr* ph_all) {
     using namespace wv;
     __shared__ Shared S;
+    __shared__ uint32_t s_ticket;
     const int lane = threadIdx.x;
-    const uint32_t c = blockIdx.x;
-    if (c >= nchains) return;
+    PhArr* ph = ph_all + blockIdx.x;
     const In in{w, nwords, nbits};
+    for (;;) {
+    __syncthreads();
+    if (lane == 0) s_ticket = atomicAdd(ticket, 1u);
+    __syncthreads();
+    const uint32_t c = s_ticket;
+    if (c >= nchains) break;
     const uint64_t start = starts[c], stop = stops[c];
     uint64_t cur = start, total = 0, endpos = start;
     uint32_t status = ST_BOUNDARY, reason = 0, nslow = 0, nfix = 0, nround = 0;
     bool recording = slot_base + c < pool.nslot;
     uint32_t prev_rec = NOREC;
     uint64_t span_est = 1ull << 18;             // round span: the previous block's size once known
+    PhaseClock pcl = {0, 0, 0, 0, 0, 0, 0};
+    PhaseClock* pc = stats ? &pcl : nullptr;
+    uint64_t tb = pc ? wall_clock64() : 0;
     for (int blk = 0;; blk++) {
         // a chain ends at the first later block boundary that is itself a header candidate (its own
         // chain links on from there) or at the range end; false candidates are passed over
@@ -691,8 +713,10 @@ ndfl_inflate_count_wave_kernel(const uint32_t* w, uint64_t nwords, uint64_t nbit
             continue;
         }
         bool ed;
+        if (pc) { const uint64_t x = wall_clock64(); pc->hdr += x - tb; tb = x; }
         const int te = build_tables(S, lane, ed);
         if (te) { status = ST_ERROR; reason = (uint32_t)te; endpos = d0; break; }
+        if (pc) { const uint64_t x = wall_clock64(); pc->build += x - tb; tb = x; }
         uint64_t rs = d0;
         bool block_done = false, chain_done = false;
         while (!block_done) {
@@ -700,7 +724,8 @@ ndfl_inflate_count_wave_kernel(const uint32_t* w, uint64_t nwords, uint64_t nbit
             if (E <= rs) E = rs + 1;
             Seg r;
             uint32_t ft;
-            round_decode(in, S.t, ed, rs, E, S, lane, r, ft, nslow, nfix);
+            round_decode(in, S.t, ed, rs, E, S, lane, r, ft, nslow, nfix, ph, pc);
+            if (pc) tb = wall_clock64();
             if (recording) {
                 // record the exact segments of this round for the emit pass
                 const bool live = (uint32_t)lane <= ft;
@@ -729,6 +754,7 @@ ndfl_inflate_count_wave_kernel(const uint32_t* w, uint64_t nwords, uint64_t nbit
                 }
             }
             nround++;
+            if (pc) { const uint64_t x = wall_clock64(); pc->rec += x - tb; tb = x; }
             total += wave_sum_u64((uint32_t)lane <= ft ? r.cnt : 0ull);
             if (ft < 64) {
                 const uint64_t fe = __shfl((unsigned long long)r.end, (int)ft, 64);
@@ -750,7 +776,14 @@ ndfl_inflate_count_wave_kernel(const uint32_t* w, uint64_t nwords, uint64_t nbit
         ChainRes o;
         o.end_bit = endpos; o.out_count = total; o.status = status; o.reason = reason;
         res[c] = o;
-        if (stats) { atomicAdd(&stats[0], nslow); atomicAdd(&stats[1], nfix); atomicAdd(&stats[2], nround); }
+        if (stats) {
+            atomicAdd(&stats[0], nslow); atomicAdd(&stats[1], nfix); atomicAdd(&stats[2], nround);
+            unsigned long long* st64 = (unsigned long long*)(stats + 32);
+            atomicAdd(&st64[0], pcl.hdr); atomicAdd(&st64[1], pcl.spec); atomicAdd(&st64[2], pcl.verify);
+            atomicAdd(&st64[3], pcl.phases); atomicAdd(&st64[4], pcl.serial); atomicAdd(&st64[5], pcl.rec);
+            atomicAdd(&st64[6], pcl.build);
+        }
+    }
     }
 }
 
@@ -762,6 +795,10 @@ ndfl_inflate_emit_wave_kernel(const uint32_t* w, uint64_t nwords, uint64_t nbits
                               uint32_t* taint, const uint32_t* sel, SegPool pool) {
     using namespace wv;
     __shared__ Shared S;
+    __shared__ PhArr S_ph;
+    __shared__ uint64_t E_off[64];               // absolute output offset per lane
+    __shared__ uint64_t E_cnt[64];               // output bytes per lane
+    __shared__ uint32_t E_prog[64];              // bytes durably written per lane
     __shared__ uint32_t s_ticket;
     const int lane = threadIdx.x;
     gu8* gout = (gu8*)out;
@@ -826,16 +863,16 @@ ndfl_inflate_emit_wave_kernel(const uint32_t* w, uint64_t nwords, uint64_t nbits
             } else {
                 uint64_t E = min(next_cand(cands, ncand, rs, ch.end_bit), rs + MAX_SPAN);
                 if (E <= rs) E = rs + 1;
-                round_decode(in, S.t, ed, rs, E, S, lane, r, ft, nslow, nfix);
+                round_decode(in, S.t, ed, rs, E, S, lane, r, ft, nslow, nfix, &S_ph);
             }
             // offsets of this round's lanes
             const bool live = (uint32_t)lane <= ft;
             const uint64_t mycnt = live ? r.cnt : 0ull;
             const uint64_t pre = wave_excl_u64(mycnt, lane);
             const uint64_t rsum = wave_sum_u64(mycnt);
-            S.off_[lane] = base + pre;
-            S.cnt_[lane] = mycnt;
-            S.prog[lane] = 0;
+            E_off[lane] = base + pre;
+            E_cnt[lane] = mycnt;
+            E_prog[lane] = 0;
             __syncthreads();
             // write pass (budgeted steps; a lane waiting on another lane or chain skips its turn)
             WLane L;
@@ -876,12 +913,12 @@ ndfl_inflate_emit_wave_kernel(const uint32_t* w, uint64_t nwords, uint64_t nbits
                             if (src < dict_len) L.tainted = true;
                             bool ok = true;
                             // bytes of earlier lanes of this round
-                            if (src_end > S.off_[0]) {
+                            if (src_end > E_off[0]) {
                                 for (int j = lane - 1; j >= 0; j--) {
-                                    const uint64_t o = S.off_[j];
-                                    if (o + S.cnt_[j] <= src) break;
-                                    const uint64_t need = min(o + S.cnt_[j], src_end) - max(o, src);
-                                    const uint64_t have = S.prog[j];
+                                    const uint64_t o = E_off[j];
+                                    if (o + E_cnt[j] <= src) break;
+                                    const uint64_t need = min(o + E_cnt[j], src_end) - max(o, src);
+                                    const uint64_t have = E_prog[j];
                                     if (max(o, src) + need > o + have) { ok = false; break; }
                                     if (o <= src) break;
                                 }
@@ -920,7 +957,7 @@ ndfl_inflate_emit_wave_kernel(const uint32_t* w, uint64_t nwords, uint64_t nbits
                 // progress = bytes issued to memory; a reader drains the wave's vmcnt before using
                 // them.  A lane that stopped on an error releases its waiters: what follows an error is
                 // never reported, so they may read anything
-                S.prog[lane] = (!L.active && L.kind == T_ERR) ? 0xFFFFFFFFu
+                E_prog[lane] = (!L.active && L.kind == T_ERR) ? 0xFFFFFFFFu
                                                               : (uint32_t)min(L.n - L.wcn - 4 * L.qn, (uint64_t)0xFFFFFFFFu);
                 __syncthreads();
                 if (__all(!L.active || waiting)) { if (++idle > 2) __builtin_amdgcn_s_sleep(2); }
