@@ -909,10 +909,12 @@ static int inflate_run(InflateScratch& S, hipStream_t s, const uint8_t* in, uint
     }
     hipEvent_t e2 = S.ev[4], e3 = S.ev[5];
     INF_CHK(hipEventRecord(e2, s));
-    hipLaunchKernelGGL(ndfl_inflate_emit_wave_kernel, dim3(nch), dim3(64), 0, s, d_w, nwords, nbits,
-                       (const EmitChain*)S.d_chains, (const uint64_t*)S.d_off, nch, (uint32_t*)S.d_done,
+    if (!S.d_ph) INF_CHK(hipMalloc(&S.d_ph, (size_t)COUNT_WAVES * sizeof(wv::PhArr)));
+    hipLaunchKernelGGL(ndfl_inflate_emit_wave_kernel, dim3(std::min<uint32_t>(nch, COUNT_WAVES)), dim3(64), 0, s, d_w,
+                       nwords, nbits, (const EmitChain*)S.d_chains, (const uint64_t*)S.d_off, nch, (uint32_t*)S.d_done,
                        (uint32_t*)S.d_ticket, d_out, (ChainRes*)S.d_res, (const uint64_t*)S.d_cands, ncand, dict_len,
-                       deferred ? (uint32_t*)S.d_taint : (uint32_t*)nullptr, (const uint32_t*)nullptr, pool);
+                       deferred ? (uint32_t*)S.d_taint : (uint32_t*)nullptr, (const uint32_t*)nullptr, pool,
+                       (wv::PhArr*)S.d_ph);
     INF_CHK(hipGetLastError());
     INF_CHK(hipEventRecord(e3, s));
     std::vector<ChainRes> er(nch);
@@ -968,10 +970,12 @@ static int inflate_resolve(InflateScratch& S, hipStream_t s, uint64_t* n_reemitt
     INF_CHK(hipMemcpyAsync(S.d_sel, sel.data(), nsel * 4ull, hipMemcpyHostToDevice, s));
     INF_CHK(hipMemcpyAsync(S.d_done, done.data(), nch * 4ull, hipMemcpyHostToDevice, s));
     INF_CHK(hipMemsetAsync(S.d_ticket, 0, 64, s));
-    hipLaunchKernelGGL(ndfl_inflate_emit_wave_kernel, dim3(nsel), dim3(64), 0, s, S.p_w, S.p_nwords, S.p_nbits,
-                       (const EmitChain*)S.d_chains, (const uint64_t*)S.d_off, nsel, (uint32_t*)S.d_done,
-                       (uint32_t*)S.d_ticket, S.p_out, (ChainRes*)S.d_res, (const uint64_t*)S.d_cands, S.p_ncand,
-                       S.p_dict_len, (uint32_t*)nullptr, (const uint32_t*)S.d_sel, S.pool);
+    if (!S.d_ph) INF_CHK(hipMalloc(&S.d_ph, (size_t)COUNT_WAVES * sizeof(wv::PhArr)));
+    hipLaunchKernelGGL(ndfl_inflate_emit_wave_kernel, dim3(std::min<uint32_t>(nsel, COUNT_WAVES)), dim3(64), 0, s,
+                       S.p_w, S.p_nwords, S.p_nbits, (const EmitChain*)S.d_chains, (const uint64_t*)S.d_off, nsel,
+                       (uint32_t*)S.d_done, (uint32_t*)S.d_ticket, S.p_out, (ChainRes*)S.d_res,
+                       (const uint64_t*)S.d_cands, S.p_ncand, S.p_dict_len, (uint32_t*)nullptr,
+                       (const uint32_t*)S.d_sel, S.pool, (wv::PhArr*)S.d_ph);
     INF_CHK(hipGetLastError());
     INF_CHK(hipStreamSynchronize(s));
     return 0;

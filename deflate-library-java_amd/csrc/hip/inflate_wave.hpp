@@ -787,25 +787,28 @@ ndfl_inflate_count_wave_kernel(const uint32_t* w, uint64_t nwords, uint64_t nbit
     }
 }
 
-// Emit pass: one wave per linked chain, claimed in stream order through `ticket`.
-extern "C" __global__ void __launch_bounds__(64)
+// Emit pass: persistent waves claiming the linked chains in stream order through `ticket` (a
+// claimed chain is always running, so waiting on earlier chains cannot deadlock).
+extern "C" __global__ void __launch_bounds__(64, 4)
 ndfl_inflate_emit_wave_kernel(const uint32_t* w, uint64_t nwords, uint64_t nbits, const EmitChain* chains,
                               const uint64_t* chain_off, uint32_t nlist, uint32_t* done, uint32_t* ticket,
                               uint8_t* out, ChainRes* res, const uint64_t* cands, uint32_t ncand, uint64_t dict_len,
-                              uint32_t* taint, const uint32_t* sel, SegPool pool) {
+                              uint32_t* taint, const uint32_t* sel, SegPool pool, wv::PhArr* ph_all) {
     using namespace wv;
     __shared__ Shared S;
-    __shared__ PhArr S_ph;
     __shared__ uint64_t E_off[64];               // absolute output offset per lane
     __shared__ uint64_t E_cnt[64];               // output bytes per lane
     __shared__ uint32_t E_prog[64];              // bytes durably written per lane
     __shared__ uint32_t s_ticket;
     const int lane = threadIdx.x;
     gu8* gout = (gu8*)out;
+    PhArr* S_ph = ph_all + blockIdx.x;
+    for (;;) {
+    __syncthreads();
     if (lane == 0) s_ticket = atomicAdd(ticket, 1u);
     __syncthreads();
     const uint32_t k = s_ticket;
-    if (k >= nlist) return;
+    if (k >= nlist) break;
     const uint32_t ci = sel ? sel[k] : k;
     const In in{w, nwords, nbits};
     const EmitChain ch = chains[ci];
@@ -863,7 +866,7 @@ ndfl_inflate_emit_wave_kernel(const uint32_t* w, uint64_t nwords, uint64_t nbits
             } else {
                 uint64_t E = min(next_cand(cands, ncand, rs, ch.end_bit), rs + MAX_SPAN);
                 if (E <= rs) E = rs + 1;
-                round_decode(in, S.t, ed, rs, E, S, lane, r, ft, nslow, nfix, &S_ph);
+                round_decode(in, S.t, ed, rs, E, S, lane, r, ft, nslow, nfix, S_ph);
             }
             // offsets of this round's lanes
             const bool live = (uint32_t)lane <= ft;
@@ -1000,5 +1003,6 @@ ndfl_inflate_emit_wave_kernel(const uint32_t* w, uint64_t nwords, uint64_t nbits
         res[ci] = o;
         __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
         __hip_atomic_store(&done[ci], 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    }
     }
 }
