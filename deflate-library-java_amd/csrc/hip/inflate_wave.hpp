@@ -691,7 +691,11 @@ ndfl_inflate_count_wave_kernel(const uint32_t* w, uint64_t nwords, uint64_t nbit
     uint32_t prev_rec = NOREC;
     uint64_t span_est = 1ull << 18;             // round span: the previous block's size once known
     PhaseClock pcl = {0, 0, 0, 0, 0, 0, 0};
-    PhaseClock* pc = stats ? &pcl : nullptr;
+#ifdef NDFL_PHASE_CLOCK
+    PhaseClock* pc = stats ? &pcl : nullptr;     // costs registers: build with -DNDFL_PHASE_CLOCK to profile
+#else
+    PhaseClock* pc = nullptr;
+#endif
     uint64_t tb = pc ? wall_clock64() : 0;
     for (int blk = 0;; blk++) {
         // a chain ends at the first later block boundary that is itself a header candidate (its own
