@@ -104,8 +104,8 @@ __device__ __forceinline__ uint32_t slow_dist(uint32_t p15, const Tabs& t) {
 }
 
 struct Tok {
-    uint32_t kind;      // K_LIT (val = byte), K_LEN (val = run, dist), K_EOB, K_BAD (val = reason)
-    uint32_t val, dist;
+    uint32_t kind;      // K_LIT (val = n bytes), K_LEN (val = run, dist), K_EOB, K_BAD (val = reason)
+    uint32_t val, dist, n;
 };
 
 // Round-relative bit reader: positions are 32-bit offsets from a 128-bit-aligned round base, so
@@ -171,14 +171,26 @@ struct Rq {
 };
 
 // One token of a Huffman block, with the reference's check order (D/decomp/Open.java:446-618).
-__device__ __forceinline__ void next_tok(Rq& rd, const RB& b, const Tabs& t, bool empty_dist, Tok& tk) {
+// Two literals whose codes fit the primary table together come as one step (tk.n = 2), except
+// when the first one already reaches `stop` (a checkpoint or the segment end): every decode then
+// stands on the first token boundary at or past each stop, whatever its grouping before it.
+__device__ __forceinline__ void next_tok(Rq& rd, const RB& b, const Tabs& t, bool empty_dist, uint32_t stop,
+                                         Tok& tk) {
     rd.fill(b);
     uint32_t e = t.lit[rd.peek(LB)];
+    if (e >> 31) {
+        const uint32_t l1 = e & 15, l2 = (e >> 4) & 15;
+        const bool two = ((e >> 8) & 1) && rd.pos + l1 < stop && rd.pos + l2 <= b.nb;
+        rd.skip(two ? l2 : l1);
+        if (rd.pos > b.nb) { tk.kind = K_BAD; tk.val = R_UEOS; return; }
+        tk.kind = K_LIT; tk.n = two ? 2u : 1u; tk.val = (e >> 9) & (two ? 0xFFFFu : 0xFFu);
+        return;
+    }
     if (!(e & 31)) e = slow_lit(rd.peek(15), t);
     rd.skip(e & 31);
     if (rd.pos > b.nb) { tk.kind = K_BAD; tk.val = R_UEOS; return; }
     const uint32_t k = (e >> 9) & 3;
-    if (k == K_LIT) { tk.kind = K_LIT; tk.val = e >> 16; return; }
+    if (k == K_LIT) { tk.kind = K_LIT; tk.n = 1; tk.val = e >> 16; return; }
     if (k == K_EOB) { tk.kind = K_EOB; return; }
     if (k == K_BAD) { tk.kind = K_BAD; tk.val = R_RESERVED_LEN; return; }
     const uint32_t run = (e >> 16) + rd.get(b, (e >> 5) & 15);
@@ -337,6 +349,33 @@ __device__ int build_code(Shared& S, uint32_t base, uint32_t n, uint32_t* prim, 
     return 0;
 }
 
+// Literal pairs in the primary table: an entry whose code is a literal becomes
+// 1 << 31 | l1 | l12 << 4 | pair << 8 | b1 << 9 | b2 << 17, with l12 = l1 + l2 and pair set when the
+// next LB - l1 bits start with a second literal code (its length l2 <= LB - l1).
+__device__ void group_lits(Tabs& t, int lane) {
+    uint32_t nv[(1u << LB) / 64];
+#pragma unroll
+    for (uint32_t q = 0; q < (1u << LB) / 64; q++) {
+        const uint32_t k = q * 64 + (uint32_t)lane;
+        const uint32_t e1 = t.lit[k];
+        const uint32_t l1 = e1 & 31;
+        uint32_t v = e1;
+        if (l1 && ((e1 >> 9) & 3) == K_LIT) {
+            const uint32_t b1 = (e1 >> 16) & 0xFFu;
+            v = (1u << 31) | l1 | (l1 << 4) | (b1 << 9);
+            const uint32_t e2 = t.lit[k >> l1];
+            const uint32_t l2 = e2 & 31;
+            if (l1 < LB && l2 && l1 + l2 <= LB && ((e2 >> 9) & 3) == K_LIT)
+                v = (1u << 31) | l1 | ((l1 + l2) << 4) | (1u << 8) | (b1 << 9) | (((e2 >> 16) & 0xFFu) << 17);
+        }
+        nv[q] = v;
+    }
+    __syncthreads();
+#pragma unroll
+    for (uint32_t q = 0; q < (1u << LB) / 64; q++) t.lit[q * 64 + (uint32_t)lane] = nv[q];
+    __syncthreads();
+}
+
 // Fixed code lengths (D/decomp/Open.java:812-830) into S.lens.
 __device__ void fixed_lens(Shared& S, int lane) {
     for (uint32_t s = (uint32_t)lane; s < 320; s += 64) {
@@ -360,6 +399,7 @@ __device__ int build_tables(Shared& S, int lane, bool& empty_dist) {
     const uint32_t numDist = S.h_numdist;
     int e = build_code(S, 0, 288, S.t.lit, LB, S.t.lfirst, S.t.llim, S.t.loff, S.t.lent, true, lane);
     if (e) return e;
+    group_lits(S.t, lane);
     // distance code: empty (one zero length) or one used code padded at index 31 (:398-425)
     const uint32_t dl = (lane < 32) ? S.lens[288 + lane] : 0u;
     empty_dist = numDist == 1 && S.lens[288] == 0;
@@ -410,8 +450,8 @@ __device__ void spec_run(const RB& b, const Tabs& t, bool ed, uint32_t st, uint3
             if (rd.pos >= C2) { o.cp2 = rd.pos - s; o.cpc2 = cnt; }
         }
         if (rd.pos >= e) break;
-        next_tok(rd, b, t, ed, tk);
-        if (tk.kind == K_LIT) { cnt++; continue; }
+        next_tok(rd, b, t, ed, o.cp1 == NOCP ? C1 : o.cp2 == NOCP ? C2 : e, tk);
+        if (tk.kind == K_LIT) { cnt += tk.n; continue; }
         if (tk.kind == K_LEN) { cnt += tk.val; continue; }
         kind = tk.kind == K_EOB ? T_EOB : T_ERR;
         reason = tk.kind == K_EOB ? 0u : tk.val;
@@ -458,8 +498,8 @@ __device__ bool verify_run(const RB& b, const Tabs& t, bool ed, uint32_t t0, uin
             }
         }
         if (q >= e) { r.end = q; r.cnt = c; r.kind = T_EXIT; r.reason = 0; return false; }
-        next_tok(rd, b, t, ed, tk);
-        if (tk.kind == K_LIT) { c++; continue; }
+        next_tok(rd, b, t, ed, stage == 0 ? C1 : stage == 1 ? C2 : e, tk);
+        if (tk.kind == K_LIT) { c += tk.n; continue; }
         if (tk.kind == K_LEN) { c += tk.val; continue; }
         r.end = rd.pos; r.cnt = c;
         r.kind = tk.kind == K_EOB ? T_EOB : T_ERR;
@@ -899,12 +939,13 @@ ndfl_inflate_emit_wave_kernel(const uint32_t* w, uint64_t nwords, uint64_t nbits
                         if (L.cp_len == 0) {
                             if (L.rd.pos >= L.end && L.kind == T_EXIT) { L.active = false; break; }
                             Tok tk;
-                            next_tok(L.rd, rb, S.t, ed, tk);
+                            next_tok(L.rd, rb, S.t, ed, L.end, tk);
                             if (tk.kind == K_LIT) {
-                                wputb(L, gout, L.dst0 + L.n, tk.val);
-                                if (L.rd.qw != L.lastqw) { wq_flush(L, gout); L.lastqw = L.rd.qw; }
-                                L.lastb = tk.val;
+                                wputb(L, gout, L.dst0 + L.n, tk.val & 0xFFu);
                                 L.n++;
+                                if (tk.n == 2) { wputb(L, gout, L.dst0 + L.n, tk.val >> 8); L.n++; }
+                                if (L.rd.qw != L.lastqw) { wq_flush(L, gout); L.lastqw = L.rd.qw; }
+                                L.lastb = tk.val >> (tk.n == 2 ? 8 : 0);
                                 continue;
                             }
                             if (tk.kind != K_LEN) { L.active = false; break; }     // EOB or error (as verified)
@@ -946,13 +987,18 @@ ndfl_inflate_emit_wave_kernel(const uint32_t* w, uint64_t nwords, uint64_t nbits
                                 if (ok && taint)
                                     for (uint32_t j = lo; j <= need_hi; j++) L.tainted |= taint[j] != 0;
                             }
+#ifdef NDFL_EXP_NOWAIT
+                            ok = true;
+#endif
                             if (!ok) { waiting = true; break; }
                             // the sources were stored by this wave (same vmcnt) or published by an
                             // earlier chain (agent release): drain, then invalidate L1 before reading
                             asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
                             __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
                         }
+#ifndef NDFL_EXP_NOCOPY
                         wcopy(L, gout, dst, src, L.cp_len, L.cp_dist);
+#endif
                         L.n += L.cp_len;
                         L.cp_len = 0;
                     }

@@ -24,6 +24,7 @@ for name in (sys.argv[2].split(",") if len(sys.argv) > 2 else gens):
         eb, _ = ctx.deflate_chunks_raw(None, 0, 32768, x.data_ptr(), n, 65536, 3, True, 0, comp.data_ptr(), cap, D)
         r, olen, bits = ctx.inflate_raw(comp.data_ptr(), (eb + 7) // 8, dec.data_ptr(), dec.numel(), D)
         assert r == 0 and olen == n
-    assert torch.equal(dec[:n], x)
+    if not os.environ.get("NDFL_NOCHECK"):
+        assert torch.equal(dec[:n], x)
     t = ctx.timings()
     print(f"{name:7s} ratio {eb / 8 / n:.3f} " + " ".join(f"{k}={v:.2f}" for k, v in t.items() if isinstance(v, float)), flush=True)
