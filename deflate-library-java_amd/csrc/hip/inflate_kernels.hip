@@ -780,11 +780,33 @@ static int inflate_run(InflateScratch& S, hipStream_t s, const uint8_t* in, uint
         const size_t n = st.size();
         std::vector<uint64_t> sp(n);
         for (size_t k = 0; k < n; k++) sp[k] = end_bit;     // chains stop at exact candidates (kernel)
+        // claim order: longest first (by the bits to the next start), so that no long chain is
+        // left for the end of the launch; bucketed by 32 Kibit
+        std::vector<uint32_t> order(n);
+        {
+            constexpr int NB = 24;
+            uint32_t bc[NB + 1] = {0};
+            auto bucket = [&](size_t k) {
+                const uint64_t nx = k + 1 < n ? st[k + 1] : end_bit;
+                const uint64_t len = nx > st[k] ? nx - st[k] : 0;
+                return NB - 1 - (int)std::min<uint64_t>(NB - 1, len >> 15);
+            };
+            const bool sorted_st = std::is_sorted(st.begin(), st.end());
+            if (sorted_st) {
+                for (size_t k = 0; k < n; k++) bc[bucket(k) + 1]++;
+                for (int b = 0; b < NB; b++) bc[b + 1] += bc[b];
+                for (size_t k = 0; k < n; k++) order[bc[bucket(k)]++] = (uint32_t)k;
+            } else {
+                for (size_t k = 0; k < n; k++) order[k] = (uint32_t)k;
+            }
+        }
         INF_CHK(inf_ensure(&S.d_starts, &S.d_starts_cap, n * 8));
-        INF_CHK(inf_ensure(&S.d_stops, &S.d_stops_cap, n * 8));
+        INF_CHK(inf_ensure(&S.d_stops, &S.d_stops_cap, n * 12));
         INF_CHK(inf_ensure(&S.d_res, &S.d_res_cap, n * sizeof(ChainRes)));
         INF_CHK(hipMemcpyAsync(S.d_starts, st.data(), n * 8, hipMemcpyHostToDevice, s));
         INF_CHK(hipMemcpyAsync(S.d_stops, sp.data(), n * 8, hipMemcpyHostToDevice, s));
+        uint32_t* d_order = (uint32_t*)((char*)S.d_stops + n * 8);
+        INF_CHK(hipMemcpyAsync(d_order, order.data(), n * 4, hipMemcpyHostToDevice, s));
         if (!S.d_ph) INF_CHK(hipMalloc(&S.d_ph, (size_t)COUNT_WAVES * sizeof(wv::PhArr)));
         if (!S.d_cticket) INF_CHK(hipMalloc(&S.d_cticket, 64));
         INF_CHK(hipMemsetAsync(S.d_cticket, 0, 4, s));
@@ -793,7 +815,7 @@ static int inflate_run(InflateScratch& S, hipStream_t s, const uint8_t* in, uint
                            d_w, nwords, nbits,
                            (const uint64_t*)S.d_starts, (const uint64_t*)S.d_stops, (uint32_t)n,
                            (const uint64_t*)S.d_cands, ncand, limit, (ChainRes*)S.d_res, stats_on ? (uint32_t*)S.d_stats : nullptr,
-                           slot_base, pool, (uint32_t*)S.d_cticket, (wv::PhArr*)S.d_ph);
+                           slot_base, pool, (uint32_t*)S.d_cticket, (wv::PhArr*)S.d_ph, (const uint32_t*)d_order);
         INF_CHK(hipGetLastError());
         if (S.count_first) { INF_CHK(hipEventRecord(S.ev[3], s)); S.count_first = false; }
         r.resize(n);

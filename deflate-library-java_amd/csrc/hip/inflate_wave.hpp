@@ -586,6 +586,150 @@ __device__ void round_decode(const In& in, const Tabs& t, bool ed, uint64_t rs, 
     out.kind = r.kind; out.reason = r.reason;
 }
 
+// ---- phase-mapped rounds (codes of (nearly) all-equal length, which never resynchronise) -------
+// Every lane decodes its segment from all 8 bit phases s..s+7.  Where the true decode enters lane j
+// decides which phase run it follows: an entry x with x - s < 8 is phase x - s; a later entry is the
+// phase whose first token ends at x.  Lane j turns lane j-1's 8 phase ends into a map (phase of
+// lane j-1 -> phase of lane j); a wave prefix scan composes the maps, lane 0 being phase 0.  Only
+// lanes whose entry matches no phase fall back to an in-order decode.
+struct PhMap {
+    uint32_t cnt[8][64];                     // bytes of the phase run
+    uint32_t fbc[8][64];                     // bytes of its first token
+    uint8_t kr[8][64];                       // kind << 5 | reason
+};
+static_assert(sizeof(PhMap) <= sizeof(PhArr), "phase map shares the fallback slot");
+
+// count run from st to the first token boundary at or past e (or the block end); the first step is
+// a single token whose end and bytes are returned in fb / fbc (fb = NOCP: none)
+__device__ void phase_run(const RB& b, const Tabs& t, bool ed, uint32_t st, uint32_t e, uint32_t& end,
+                          uint32_t& cnt, uint32_t& kr, uint32_t& fb, uint32_t& fbc) {
+    Rq rd;
+    rd.init(b, st);
+    uint32_t c = 0;
+    kr = T_EXIT << 5; fb = NOCP; fbc = 0;
+    Tok tk;
+    while (rd.pos < e) {
+        next_tok(rd, b, t, ed, fb == NOCP ? rd.pos + 1 : e, tk);
+        uint32_t add;
+        if (tk.kind == K_LIT) add = tk.n;
+        else if (tk.kind == K_LEN) add = tk.val;
+        else { kr = tk.kind == K_EOB ? (T_EOB << 5) : ((T_ERR << 5) | tk.val); break; }
+        c += add;
+        if (fb == NOCP) { fb = rd.pos; fbc = add; }
+    }
+    end = rd.pos; cnt = c;
+}
+
+__device__ __forceinline__ uint32_t sel8(const uint32_t (&v)[8], uint32_t i) {
+    uint32_t r = v[0];
+#pragma unroll
+    for (uint32_t k = 1; k < 8; k++) r = i == k ? v[k] : r;
+    return r;
+}
+// phase of an entry at offset d from s: bits 0..3 phase (8 = none), bit 4 entered at its first boundary
+__device__ __forceinline__ uint32_t phase_of(uint32_t d, uint32_t fbl, uint32_t fbh) {
+    if (d < 8) return d;
+    uint32_t r = 8;
+#pragma unroll
+    for (uint32_t f = 0; f < 8; f++) {
+        const uint32_t fo = ((f < 4 ? fbl : fbh) >> (8 * (f & 3))) & 0xFFu;
+        if (r == 8 && fo == d) r = f | 16u;
+    }
+    return r;
+}
+// (A after B): entry f = A[B[f]], 8 stays 8
+__device__ __forceinline__ uint32_t map_compose(uint32_t A, uint32_t B) {
+    uint32_t r = 0;
+#pragma unroll
+    for (uint32_t f = 0; f < 8; f++) {
+        const uint32_t bf = (B >> (4 * f)) & 15u;
+        const uint32_t v = bf < 8 ? (A >> (4 * bf)) & 15u : 8u;
+        r |= v << (4 * f);
+    }
+    return r;
+}
+
+__device__ __noinline__ void round_decode_phased(const In& in, const Tabs& t, bool ed, uint64_t rs, uint64_t E, Shared& S,
+                                    int lane, Seg& out, uint32_t& first_term, uint32_t& nfix, PhArr* ph) {
+    const RB b = make_rb(in, rs);
+    const uint32_t r0 = (uint32_t)(rs - b.base), re = (uint32_t)(E - b.base);
+    const uint32_t span = re - r0;
+    const uint32_t per = (span + 63) / 64;
+    const uint32_t s = min(r0 + (uint32_t)lane * per, re);
+    const uint32_t e = (lane == 63) ? re : min(r0 + (uint32_t)(lane + 1) * per, re);
+    PhMap* pm = (PhMap*)ph;
+    uint32_t endv[8];
+    uint32_t fbl = 0, fbh = 0;
+    for (uint32_t f = 0; f < 8; f++) {
+        uint32_t en, cn, kr, fb, fbc;
+        phase_run(b, t, ed, s + f, e, en, cn, kr, fb, fbc);      // (past e: empty, ends at s + f)
+#pragma unroll
+        for (uint32_t k = 0; k < 8; k++) endv[k] = k == f ? en : endv[k];
+        pm->cnt[f][lane] = cn;
+        pm->fbc[f][lane] = fbc;
+        pm->kr[f][lane] = (uint8_t)kr;
+        const uint32_t fo = (fb != NOCP && fb - s < 255u) ? fb - s : 255u;
+        if (f < 4) fbl |= fo << (8 * f); else fbh |= fo << (8 * (f - 4));
+    }
+    // map of lane j: phase of lane j-1 -> phase of lane j
+    uint32_t Q = 0;                             // lane 0: always phase 0
+#pragma unroll
+    for (uint32_t f = 0; f < 8; f++) {
+        const uint32_t x = __shfl_up(endv[f], 1, 64);
+        const uint32_t v = phase_of(x - s, fbl, fbh) & 15u;
+        if (lane > 0) Q |= v << (4 * f);
+    }
+#pragma unroll
+    for (int k = 1; k < 64; k <<= 1) {
+        const uint32_t B = __shfl_up(Q, k, 64);
+        if (lane >= k) Q = map_compose(Q, B);
+    }
+    const uint32_t myph = Q & 15u;
+    const uint32_t xsel = myph < 8 ? sel8(endv, myph) : NOCP;
+    uint32_t x = __shfl_up(xsel, 1, 64);
+    if (lane == 0) x = s;
+    SegR r;
+    r.start = x; r.end = x; r.cnt = 0; r.kind = T_ERR; r.reason = R_INTERNAL;
+    bool known = false;
+    if (myph < 8) {
+        const uint32_t pc = phase_of(x - s, fbl, fbh);
+        const uint32_t f = pc & 15u;
+        if (f == myph) {
+            known = true;
+            const uint32_t kr = pm->kr[f][lane];
+            r.end = sel8(endv, f);
+            r.cnt = pm->cnt[f][lane] - ((pc & 16u) ? pm->fbc[f][lane] : 0u);
+            r.kind = kr >> 5; r.reason = kr & 31u;
+        }
+    }
+    const uint64_t km = __ballot(!known);
+    const uint32_t u = km ? (uint32_t)__builtin_ctzll(km) : 64u;
+    const uint64_t tm = __ballot(known && r.kind != T_EXIT);
+    const uint32_t t0 = tm ? (uint32_t)__builtin_ctzll(tm) : 64u;
+    first_term = min(t0, 64u);
+    if (u < t0) {
+        // in-order decode from lane u on (its predecessor is exact)
+        S.exit_[lane] = r.end;
+        __syncthreads();
+        first_term = 64;
+        for (uint32_t j = u; j < 64 && first_term == 64; j++) {
+            nfix++;
+            if ((uint32_t)lane == j) {
+                const uint32_t st = j ? (uint32_t)S.exit_[j - 1] : s;
+                uint32_t en, cn, kr, fb, fbc;
+                phase_run(b, t, ed, st, e, en, cn, kr, fb, fbc);
+                r.start = st; r.end = en; r.cnt = cn; r.kind = kr >> 5; r.reason = kr & 31u;
+                S.exit_[lane] = en;
+                S.kind_[lane] = r.kind;
+            }
+            __syncthreads();
+            if (S.kind_[j] != T_EXIT) first_term = j;
+        }
+    }
+    out.start = b.base + r.start; out.end = b.base + r.end; out.cnt = r.cnt;
+    out.kind = r.kind; out.reason = r.reason;
+}
+
 __device__ __forceinline__ uint64_t wave_sum_u64(uint64_t x) {
 #pragma unroll
     for (int o = 32; o > 0; o >>= 1) x += __shfl_xor((unsigned long long)x, o, 64);
@@ -711,7 +855,7 @@ extern "C" __global__ void __launch_bounds__(64, 4)
 ndfl_inflate_count_wave_kernel(const uint32_t* w, uint64_t nwords, uint64_t nbits, const uint64_t* starts,
                                const uint64_t* stops, uint32_t nchains, const uint64_t* cands, uint32_t ncand,
                                uint64_t limit, ChainRes* res, uint32_t* stats, uint64_t slot_base, SegPool pool,
-                               uint32_t* ticket, wv::PhArr* ph_all) {
+                               uint32_t* ticket, wv::PhArr* ph_all, const uint32_t* order) {
     using namespace wv;
     __shared__ Shared S;
     __shared__ uint32_t s_ticket;
@@ -722,8 +866,8 @@ ndfl_inflate_count_wave_kernel(const uint32_t* w, uint64_t nwords, uint64_t nbit
     __syncthreads();
     if (lane == 0) s_ticket = atomicAdd(ticket, 1u);
     __syncthreads();
-    const uint32_t c = s_ticket;
-    if (c >= nchains) break;
+    if (s_ticket >= nchains) break;
+    const uint32_t c = order[s_ticket];
     const uint64_t start = starts[c], stop = stops[c];
     uint64_t cur = start, total = 0, endpos = start;
     uint32_t status = ST_BOUNDARY, reason = 0, nslow = 0, nfix = 0, nround = 0;
@@ -763,12 +907,28 @@ ndfl_inflate_count_wave_kernel(const uint32_t* w, uint64_t nwords, uint64_t nbit
         if (pc) { const uint64_t x = wall_clock64(); pc->build += x - tb; tb = x; }
         uint64_t rs = d0;
         bool block_done = false, chain_done = false;
+        // literal/length codes mostly of one length 8 resynchronise rarely: phase-mapped rounds
+        bool phased = false;
+        {
+            uint32_t n8 = 0;
+            for (uint32_t q = 0; q < 5; q++) {
+                const uint32_t sy = q * 64 + (uint32_t)lane;
+                n8 += (uint32_t)__popcll(__ballot(sy < 288 && S.lens[sy] == 8));
+            }
+            phased = n8 >= 192;
+        }
         while (!block_done) {
             uint64_t E = min(next_cand(cands, ncand, rs, limit), rs + min(span_est, MAX_SPAN));
             if (E <= rs) E = rs + 1;
             Seg r;
             uint32_t ft;
-            round_decode(in, S.t, ed, rs, E, S, lane, r, ft, nslow, nfix, ph, pc);
+            if (phased) {
+                round_decode_phased(in, S.t, ed, rs, E, S, lane, r, ft, nfix, ph);
+            } else {
+                const uint32_t ns0 = nslow;
+                round_decode(in, S.t, ed, rs, E, S, lane, r, ft, nslow, nfix, ph, pc);
+                if (nslow - ns0 > 32) phased = true;    // phase-locked code: map the next rounds
+            }
             if (pc) tb = wall_clock64();
             if (recording) {
                 // record the exact segments of this round for the emit pass
