@@ -35,7 +35,7 @@ def main():
     ap.add_argument("--steps", type=int, default=5)
     ap.add_argument("--warmup", type=int, default=2)
     ap.add_argument("--size", type=int, default=4 << 30, help="bytes per rank")
-    ap.add_argument("--cpu-sample", type=int, default=256 << 20, help="bytes for the CPU baseline leg")
+    ap.add_argument("--cpu-sample", type=int, default=1 << 30, help="bytes for the CPU baseline leg (about 20 s of oracle work)")
     ap.add_argument("--no-cpu", action="store_true")
     ap.add_argument("--no-verify", action="store_true")
     ap.add_argument("--backend", default="nccl", help="nccl (= RCCL over xGMI); gloo only to rehearse N>1 on one GPU")
@@ -137,10 +137,11 @@ def main():
     kd, ke = state["t_deflate"], state["t_emit"]
     alg = n + state["cbytes"]
     if ke >= kd:
-        dom, kms = "ndfl_inflate_emit_kernel", ke
+        dom, kms = "ndfl_inflate_emit_wave_kernel", ke
     else:
         dom, kms = "ndfl_deflate_chunks_kernel", kd
     achieved = alg / (kms / 1e3)
+    traffic, traffic_src = pmc_traffic(dom, n)
 
     cpu = None
     if rank == 0 and not args.no_cpu:
@@ -170,13 +171,28 @@ def main():
                           "inflate_chains": int(state["chains"]), "inflate_repairs": int(state["repairs"]),
                           "inflate_candidates": int(state["cands"])},
             "roofline": {"bound": "hbm", "kernel": dom, "achieved": round(achieved / 1e9, 2), "peak": HBM_PEAK / 1e9,
-                         "unit": "GB/s", "frac": round(achieved / HBM_PEAK, 4), "traffic": None,
+                         "unit": "GB/s", "frac": round(achieved / HBM_PEAK, 4), "traffic": traffic,
+                         "traffic_source": traffic_src,
                          "algorithmic_bytes_per_launch": alg, "avg_kernel_ms": round(kms, 3)},
             "cpu_baseline": cpu,
         }
         print(json.dumps(line), flush=True)
     if dist is not None:
         dist.destroy_process_group()
+
+
+def pmc_traffic(kernel, n):
+    """HBM bytes per launch of `kernel` from the committed rocprofv3 --pmc summary of this same bench
+    command (profiles/r01_traffic.json, made by scripts/profile_bench.sh + scripts/traffic_summary.py:
+    FETCH_SIZE and WRITE_SIZE passes, gfx950 corrections applied).  Counters cannot be read from inside
+    the timed run, so the value is the profiled one, quoted only for the default 4 GiB workload."""
+    path = os.path.join(ROOT, "profiles", "r01_traffic.json")
+    if n != 4 << 30 or not os.path.exists(path):
+        return None, None
+    rec = json.load(open(path)).get(kernel)
+    if rec is None:
+        return None, None
+    return rec["traffic_bytes"], f"profiles/r01_traffic.json (fetch {rec['fetch_bytes']} B + write {rec['write_bytes']} B per launch)"
 
 
 def cpu_baseline(data_dev, sample_bytes):
