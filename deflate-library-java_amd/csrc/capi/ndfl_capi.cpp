@@ -2,6 +2,7 @@
 // Compiled as HIP for gfx950 together with the kernels (single translation unit).
 #include "../../../include/ndfl.h"
 #include "../hip/deflate_kernels.hip"
+#include "../hip/lz77_kernels.hip"
 #include "../hip/inflate_kernels.hip"
 
 #include <hip/hip_runtime.h>
@@ -59,6 +60,7 @@ struct ndfl_ctx {
     double last_ms = 0;
     double deflate_ms = 0;
     DevBuf d_in, d_out, d_status, d_ticket, d_edge_w, d_edge_v, d_crc, d_crc1, d_tabs, d_hostio;
+    DevBuf d_lz, d_link, d_match;   // LZ77 path: staging [pad|hist|data], hash links, per-position matches
     InflateScratch inf;
     uint32_t* h_pinned = nullptr;   // small pinned area for results
 };
@@ -118,7 +120,7 @@ int ndfl_ctx_destroy(ndfl_ctx* c) {
     hipSetDevice(c->device);
     hipStreamSynchronize(c->stream);
     DevBuf* bufs[] = {&c->d_in, &c->d_out, &c->d_status, &c->d_ticket, &c->d_edge_w, &c->d_edge_v,
-                      &c->d_crc, &c->d_crc1, &c->d_tabs, &c->d_hostio};
+                      &c->d_crc, &c->d_crc1, &c->d_tabs, &c->d_hostio, &c->d_lz, &c->d_link, &c->d_match};
     for (DevBuf* b : bufs) b->release();
     c->inf.release();
     if (c->h_pinned) hipHostFree(c->h_pinned);
@@ -169,7 +171,11 @@ int ndfl_deflate_chunks(ndfl_ctx* c, const uint8_t* hist, uint32_t hist_len, uin
         case NDFL_LITERAL_DYNAMIC: rle = 0; dyn = 1; break;
         case NDFL_RLE_STATIC: rle = 1; dyn = 0; break;
         case NDFL_RLE_DYNAMIC: rle = 1; dyn = 1; break;
-        case NDFL_FULL_STATIC: case NDFL_FULL_DYNAMIC: case NDFL_UNCOMPRESSED: return NDFL_E_UNSUPPORTED;
+        case NDFL_FULL_STATIC: case NDFL_FULL_DYNAMIC:
+            return ndfl_deflate_chunks_lz77(c, hist, hist_len, hist_limit, data, len, chunk_len,
+                                            strategy == NDFL_FULL_DYNAMIC, 3, 258, 1, 32768, final_flag,
+                                            start_bitpos, out, out_cap, out_end_bits, crc_inout, flags);
+        case NDFL_UNCOMPRESSED: return NDFL_E_UNSUPPORTED;
         default: return NDFL_E_ARG;
     }
     if (chunk_len > (uint32_t)MAX_CHUNK) return NDFL_E_UNSUPPORTED;
@@ -268,6 +274,121 @@ int ndfl_deflate_chunks(ndfl_ctx* c, const uint8_t* hist, uint32_t hist_len, uin
         uint32_t raw = c->h_pinned[4];
         uint32_t dc = ~(crc_multmodp(crc_x8n(len), 0xFFFFFFFFu) ^ raw);
         *crc_inout = ndfl_crc32_combine(*crc_inout, dc, len);
+    }
+    if (!direct) {
+        if (nbytes > out_cap) return NDFL_E_CAPACITY;
+        HIPCHK(hipMemcpyAsync(out, d_out, nbytes,
+                              (flags & NDFL_OUT_DEVICE) ? hipMemcpyDeviceToDevice : hipMemcpyDeviceToHost, s));
+        HIPCHK(hipStreamSynchronize(s));
+    }
+    return NDFL_OK;
+}
+
+// Lz77Huffman(dynamic, minRun, maxRun, minDist, maxDist) over K chunks (D/comp/Lz77Huffman.java:20-130):
+// staging copy, then per batch of chunks links -> matches -> parse/encode; edges and CRC at the end.
+int ndfl_deflate_chunks_lz77(ndfl_ctx* c, const uint8_t* hist, uint32_t hist_len, uint32_t hist_limit,
+                             const uint8_t* data, uint64_t len, uint32_t chunk_len, int dynamic, int min_run,
+                             int max_run, int min_dist, int max_dist, int final_flag, uint32_t start_bitpos,
+                             uint8_t* out, uint64_t out_cap, uint64_t* out_end_bits, uint32_t* crc_inout,
+                             uint32_t flags) {
+    if (!c || !out_end_bits || (!data && len) || (!hist && hist_len) || !out) return NDFL_E_ARG;
+    if (start_bitpos > 7 || hist_limit > 32768 || hist_len > hist_limit || chunk_len == 0) return NDFL_E_ARG;
+    if (!final_flag && (len == 0 || len % chunk_len != 0)) return NDFL_E_ARG;
+    const bool literal_only = min_run == 0 && max_run == 0 && min_dist == 0 && max_dist == 0;   // (:29-31)
+    if (!literal_only && !(3 <= min_run && min_run <= max_run && max_run <= 258 && 1 <= min_dist &&
+                           min_dist <= max_dist && max_dist <= 32768))
+        return NDFL_E_ARG;                                                                     // (:32-38)
+    if (literal_only || (min_run == 3 && max_run == 258 && min_dist == 1 && max_dist == 1))
+        return ndfl_deflate_chunks(c, hist, hist_len, hist_limit, data, len, chunk_len,
+                                   literal_only ? (dynamic ? NDFL_LITERAL_DYNAMIC : NDFL_LITERAL_STATIC)
+                                                : (dynamic ? NDFL_RLE_DYNAMIC : NDFL_RLE_STATIC),
+                                   final_flag, start_bitpos, out, out_cap, out_end_bits, crc_inout, flags);
+    if (chunk_len > (uint32_t)MAX_CHUNK) return NDFL_E_UNSUPPORTED;
+    HIPCHK(hipSetDevice(c->device));
+    const uint64_t nch64 = final_flag ? (len == 0 ? 1 : (len + chunk_len - 1) / chunk_len) : len / chunk_len;
+    if (nch64 > 0xFFFFFFFFull) return NDFL_E_UNSUPPORTED;
+    const uint32_t nch = (uint32_t)nch64;
+    hipStream_t s = c->stream;
+
+    // staging buffer: data at LZ_DS, the history right before it
+    const uint64_t total = LZ_DS + len;
+    HIPCHK(c->d_lz.ensure(total + 64));
+    uint8_t* buf = c->d_lz.as<uint8_t>();
+    const hipMemcpyKind kin = (flags & NDFL_IN_DEVICE) ? hipMemcpyDeviceToDevice : hipMemcpyHostToDevice;
+    if (hist_len) HIPCHK(hipMemcpyAsync(buf + LZ_DS - hist_len, hist, hist_len, kin, s));
+    if (len) HIPCHK(hipMemcpyAsync(buf + LZ_DS, data, len, kin, s));
+    HIPCHK(hipMemsetAsync(buf + total, 0, 64, s));
+
+    const uint64_t bound = ndfl_deflate_bound(len, chunk_len);
+    const uint64_t bound_words = (bound + 3) / 4 + 2;
+    uint32_t* d_out;
+    bool direct = (flags & NDFL_OUT_DEVICE) && (((uintptr_t)out & 3) == 0) && out_cap >= bound_words * 4;
+    if (direct) d_out = (uint32_t*)out;
+    else { HIPCHK(c->d_out.ensure(bound_words * 4)); d_out = c->d_out.as<uint32_t>(); }
+    HIPCHK(c->d_status.ensure(nch * sizeof(uint64_t)));
+    HIPCHK(c->d_ticket.ensure(64));
+    HIPCHK(c->d_edge_w.ensure(2ull * nch * sizeof(uint64_t)));
+    HIPCHK(c->d_edge_v.ensure(2ull * nch * sizeof(uint32_t)));
+    HIPCHK(hipMemsetAsync(c->d_status.p, 0, nch * sizeof(uint64_t), s));
+
+    // batches of whole chunks, <= 256 MiB of data each (matches: 4 B per byte, links: 2 B)
+    const uint32_t batch_ch = std::max<uint32_t>(1, (uint32_t)((256ull << 20) / chunk_len));
+    const uint64_t batch_bytes = std::min<uint64_t>((uint64_t)batch_ch * chunk_len, std::max<uint64_t>(len, 1));
+    HIPCHK(c->d_match.ensure(batch_bytes * 4));
+    HIPCHK(c->d_link.ensure((batch_bytes + LZ_SEG) * 2));
+
+    LzArgs la;
+    la.buf = buf; la.total = total; la.vstart = LZ_DS - hist_len; la.chunk_len = chunk_len;
+    la.hist_limit = hist_limit; la.min_run = (uint32_t)min_run; la.max_run = (uint32_t)max_run;
+    la.min_dist = (uint32_t)min_dist; la.max_dist = (uint32_t)max_dist;
+    la.link = c->d_link.as<uint16_t>(); la.match = c->d_match.as<uint32_t>();
+    LzEncArgs ea;
+    ea.match = c->d_match.as<uint32_t>(); ea.n = len; ea.chunk_len = chunk_len; ea.nchunks = nch;
+    ea.final_last = final_flag ? 1 : 0; ea.dynamic = dynamic ? 1 : 0; ea.base_bit = start_bitpos;
+    ea.out = d_out; ea.status = c->d_status.as<uint64_t>(); ea.ticket = c->d_ticket.as<uint32_t>();
+    ea.edge_w = c->d_edge_w.as<uint64_t>(); ea.edge_v = c->d_edge_v.as<uint32_t>();
+
+    HIPCHK(hipEventRecord(c->ev0, s));
+    for (uint32_t cb = 0; cb < nch; cb += batch_ch) {
+        const uint32_t ce = std::min(nch, cb + batch_ch);
+        const uint64_t x0 = (uint64_t)cb * chunk_len, x1 = std::min<uint64_t>((uint64_t)ce * chunk_len, len);
+        const uint64_t P0 = LZ_DS + x0, P1 = LZ_DS + x1;
+        if (P1 > P0) {
+            const uint64_t L0 = std::max<uint64_t>(la.vstart, P0 - LZ_SEG);
+            hipLaunchKernelGGL(ndfl_lz_links_kernel, dim3((uint32_t)((P1 - L0 + LZ_SEG - 1) / LZ_SEG)), dim3(64), 0, s,
+                               (const uint8_t*)buf, total, la.vstart, L0, P1, c->d_link.as<uint16_t>());
+            HIPCHK(hipGetLastError());
+            la.L0 = L0; la.p_begin = P0; la.p_end = P1;
+            hipLaunchKernelGGL(ndfl_lz_match_kernel, dim3((uint32_t)((P1 - P0 + LZ_TILE - 1) / LZ_TILE)), dim3(1024), 0, s, la);
+            HIPCHK(hipGetLastError());
+        }
+        HIPCHK(hipMemsetAsync(c->d_ticket.p, 0, 64, s));
+        ea.batch_x0 = x0; ea.chunk_base = cb; ea.nchunks_batch = ce - cb;
+        hipLaunchKernelGGL(ndfl_lz_encode_kernel, dim3(ce - cb), dim3(1024), 0, s, ea);
+        HIPCHK(hipGetLastError());
+    }
+    HIPCHK(hipEventRecord(c->ev1, s));
+    const uint32_t ne = 2 * nch;
+    hipLaunchKernelGGL(ndfl_edge_fixup_kernel, dim3((ne + 255) / 256), dim3(256), 0, s,
+                       (const uint64_t*)ea.edge_w, (const uint32_t*)ea.edge_v, ne, d_out);
+    HIPCHK(hipGetLastError());
+    HIPCHK(hipMemcpyAsync(c->h_pinned, ea.status + (nch - 1), 8, hipMemcpyDeviceToHost, s));
+    HIPCHK(hipStreamSynchronize(s));
+    float ms = 0;
+    hipEventElapsedTime(&ms, c->ev0, c->ev1);
+    c->last_ms = ms;
+    c->deflate_ms = ms;
+    uint64_t st;
+    memcpy(&st, c->h_pinned, 8);
+    const uint64_t end_bits = st & ST_VAL;
+    *out_end_bits = end_bits;
+    const uint64_t nbytes = (end_bits + 7) / 8;
+    if (crc_inout && len) {
+        uint32_t cr = *crc_inout;
+        int rc = ndfl_crc32(c, &cr, buf + LZ_DS, len, NDFL_IN_DEVICE);
+        if (rc) return rc;
+        *crc_inout = cr;
+        c->last_ms = ms;
     }
     if (!direct) {
         if (nbytes > out_cap) return NDFL_E_CAPACITY;

@@ -261,6 +261,217 @@ struct BitPut {
 
 constexpr uint32_t CL_EXTRA_BITS[3] = {2, 3, 7};
 
+// Code construction for one block, histograms already final (EOB counted).  Dynamic:
+// D/comp/Lz77Huffman.java:143-265 (trim, single-distance fix-up, package-merge lengths, canonical
+// codes, code-length RLE, code-length code, header sizes); static: the fixed codes of :394-410.
+// Leaves the code tables and header layout in `ps` and the reordered 3-bit code-length-code
+// lengths packed in misc[4..5] of the scratch.  All threads must call.
+__device__ __forceinline__ void build_block_codes(bool dynamic, char* scr, Persist& ps) {
+    uint32_t* hlit = (uint32_t*)(scr + SCR_HLIT);
+    uint32_t* hdist = (uint32_t*)(scr + SCR_HDIST);
+    uint8_t* lens = (uint8_t*)(scr + SCR_LEN);
+    uint8_t* clLen = (uint8_t*)(scr + SCR_CLLEN);
+    uint32_t* clh = (uint32_t*)(scr + SCR_CLH);
+    uint32_t* misc = (uint32_t*)(scr + SCR_MISC);
+    const int tid = threadIdx.x;
+    if (!dynamic) {
+        // fixed codes (D/comp/Lz77Huffman.java:394-410)
+        if (tid < 288) {
+            uint32_t l = tid < 144 ? 8 : tid < 256 ? 9 : tid < 280 ? 7 : 8;
+            uint32_t code = tid < 144 ? 0x30 + tid : tid < 256 ? 0x190 + (tid - 144) : tid < 280 ? (tid - 256) : 0xC0 + (tid - 280);
+            ps.litCode[tid] = (__brev(code) >> (32 - l)) | (l << 16);
+        }
+        if (tid < 32) ps.distCode[tid] = (__brev((uint32_t)tid) >> 27) | (5u << 16);
+        if (tid == 0) { ps.hdrBits = 3; ps.nsym = 0; }
+        __syncthreads();
+    } else {
+        // trim litlen histogram, keep >= 257 (:148-151)
+        if (tid == 0) {
+            int ln = 286;
+            while (ln > 257 && hlit[ln - 1] == 0) ln--;
+            misc[0] = (uint32_t)ln;
+            // single used distance code -> dummy neighbour (:155-171)
+            int used = 0, first = -1;
+            for (int i = 0; i < 30; i++) if (hdist[i]) { used++; if (first < 0) first = i; }
+            if (used == 1) { if (first < 29) hdist[first + 1] = 1; else hdist[first - 1] = 1; }
+            int dn = 30;
+            while (dn > 1 && hdist[dn - 1] == 0) dn--;
+            misc[1] = (uint32_t)dn;
+            misc[2] = (dn == 1 && hdist[0] == 0) ? 1u : 0u;   // empty distance code
+        }
+        __syncthreads();
+        const int ln = (int)misc[0], dn = (int)misc[1];
+        const bool emptyDist = misc[2] != 0;
+        pm_lengths(hlit, ln, 15, lens, scr);
+        if (emptyDist) { if (tid == 0) lens[ln] = 0; __syncthreads(); }
+        else pm_lengths(hdist, dn, 15, lens + ln, scr);
+        canon_codes(lens, ln, ps.litCode, scr);
+        canon_codes(lens + ln, dn, ps.distCode, scr);
+        // code-length sequence RLE (:187-223) as maximal-run decomposition
+        const int nc = ln + dn;
+        uint32_t rstart = 0xFFFFFFFFu;
+        uint32_t v = 0;
+        if (tid < nc) {
+            v = lens[tid];
+            if (tid == 0 || lens[tid - 1] != v) rstart = (uint32_t)tid;
+        }
+        uint32_t rnext = min(block_excl_suffix_min<NW>(rstart, 0xFFFFFFFFu, ps.scan32), (uint32_t)nc);
+        uint32_t cnt = 0, Z = 0;
+        if (rstart != 0xFFFFFFFFu) {
+            Z = rnext - rstart;
+            if (v == 0) {
+                uint32_t q = Z / 138, r = Z % 138;
+                cnt = q + (r >= 3 ? 1 : r);
+            } else {
+                uint32_t rest = Z - 1, q = rest / 6, r = rest % 6;
+                cnt = 1 + q + (r >= 3 ? 1 : r);
+            }
+        }
+        uint32_t tot;
+        uint32_t off = block_excl_scan<uint32_t, NW>(cnt, ps.scan32, tot);
+        if (rstart != 0xFFFFFFFFu) {
+            uint32_t k = off;
+            if (v == 0) {
+                uint32_t L = Z;
+                while (L > 0) {
+                    uint32_t r = min(L, 138u);
+                    if (r < 3) { ps.clSym[k] = 0; ps.clExtra[k++] = 0; L -= 1; }
+                    else if (r < 11) { ps.clSym[k] = 17; ps.clExtra[k++] = (uint8_t)(r - 3); L -= r; }
+                    else { ps.clSym[k] = 18; ps.clExtra[k++] = (uint8_t)(r - 11); L -= r; }
+                }
+            } else {
+                ps.clSym[k] = (uint8_t)v; ps.clExtra[k++] = 0;
+                uint32_t L = Z - 1;
+                while (L >= 3) { uint32_t r = min(L, 6u); ps.clSym[k] = 16; ps.clExtra[k++] = (uint8_t)(r - 3); L -= r; }
+                while (L > 0) { ps.clSym[k] = (uint8_t)v; ps.clExtra[k++] = 0; L--; }
+            }
+        }
+        if (tid < 20) clh[tid] = 0;
+        __syncthreads();
+        if ((uint32_t)tid < tot) atomicAdd(&clh[ps.clSym[tid]], 1u);
+        __syncthreads();
+        pm_lengths(clh, 19, 7, clLen, scr);
+        canon_codes(clLen, 19, ps.clCode, scr);
+        // per-symbol header bit offsets
+        uint32_t sb = 0;
+        if ((uint32_t)tid < tot) {
+            uint32_t sy = ps.clSym[tid];
+            sb = (ps.clCode[sy] >> 16) + (sy >= 16 ? CL_EXTRA_BITS[sy - 16] : 0);
+        }
+        uint32_t body;
+        uint32_t so = block_excl_scan<uint32_t, NW>(sb, ps.scan32, body);
+        if ((uint32_t)tid < tot) ps.clOff[tid] = (uint16_t)so;
+        if (tid == 0) {
+            const int order[19] = {16, 17, 18, 0, 8, 7, 9, 6, 10, 5, 11, 4, 12, 3, 13, 2, 14, 1, 15};
+            int ncl = 19;
+            while (ncl > 4 && clLen[order[ncl - 1]] == 0) ncl--;    // (:230-234)
+            ps.ncl = (uint32_t)ncl;
+            ps.nsym = tot;
+            ps.hlit = (uint32_t)(ln - 257);
+            ps.hdist = (uint32_t)(dn - 1);
+            ps.clBodyBits = body;
+            ps.hdrBits = 3 + 14 + 3 * (uint32_t)ncl + body;
+            // stash reordered code-length-code lengths in misc[4..] (3 bits each, packed)
+            uint64_t packed = 0;
+            for (int i = 0; i < ncl; i++) packed |= (uint64_t)clLen[order[i]] << (3 * i);
+            misc[4] = (uint32_t)packed; misc[5] = (uint32_t)(packed >> 32);
+        }
+        __syncthreads();
+    }
+}
+
+// Block header (bfinal, btype, HLIT/HDIST/HCLEN, code-length-code lengths, code-length symbols:
+// D/comp/Lz77Huffman.java:134-135,236-258) and the end-of-block code after `tokTotal` token bits
+// (:285), ORed into the LDS bit buffer at local bit 0.  All threads must call (no barrier).
+__device__ __forceinline__ void emit_block_header(uint32_t* obuf, bool is_final, bool dynamic, const Persist& ps,
+                                                  uint32_t packedLo, uint32_t packedHi, uint32_t hdrBits,
+                                                  uint32_t tokTotal, uint32_t eobLen) {
+    const int tid = threadIdx.x;
+    const uint32_t bit0 = 0;
+    if (tid == 0) {
+        BitPut bp; bp.init(obuf, bit0);
+        bp.put(is_final ? 1u : 0u, 1);
+        bp.put(dynamic ? 2u : 1u, 2);
+        if (dynamic) {
+            bp.put(ps.hlit, 5);
+            bp.put(ps.hdist, 5);
+            bp.put(ps.ncl - 4, 4);
+            uint64_t packed = (uint64_t)packedLo | (uint64_t)packedHi << 32;
+            for (uint32_t i = 0; i < ps.ncl; i++) bp.put((uint32_t)(packed >> (3 * i)) & 7u, 3);
+        }
+        bp.flush();
+        // end-of-block symbol
+        BitPut be; be.init(obuf, bit0 + hdrBits + tokTotal);
+        be.put(ps.litCode[256] & 0xFFFF, eobLen);
+        be.flush();
+    }
+    if (dynamic && (uint32_t)tid < ps.nsym) {
+        const uint32_t sy = ps.clSym[tid];
+        BitPut bp; bp.init(obuf, bit0 + 17 + 3 * ps.ncl + ps.clOff[tid]);
+        bp.put(ps.clCode[sy] & 0xFFFF, ps.clCode[sy] >> 16);
+        if (sy >= 16) bp.put(ps.clExtra[tid], CL_EXTRA_BITS[sy - 16]);
+        bp.flush();
+    }
+}
+
+// Decoupled look-back (one wave): the chunk's global bit offset from its predecessors' status words,
+// then its inclusive prefix published.  Lane i polls predecessor c-1-i, so 64 predecessors cost one
+// round trip; the closest inclusive prefix (PRE) ends the walk, aggregates (AGG) before it are
+// summed, and a not-yet-published predecessor closer than it re-polls.  Chunk ids come from a
+// ticket, so a workgroup only waits on workgroups that already started.  Result in ps.P.
+__device__ __forceinline__ void block_lookback(uint32_t c, uint64_t base_bit, uint64_t S, uint64_t* status, Persist& ps) {
+    const int tid = threadIdx.x;
+    const int lane = tid & 63, wid = tid >> 6;
+    if (wid == 0) {
+        // decoupled look-back, one wave: lane i polls predecessor c-1-i, so 64 predecessors cost
+        // one round trip; the closest inclusive prefix (PRE) ends the walk, aggregates (AGG)
+        // before it are summed, and a not-yet-published predecessor closer than it re-polls.
+        uint64_t P = base_bit;
+        if (c > 0) {
+            uint64_t acc = 0;
+            int64_t base = (int64_t)c - 1;
+            for (;;) {
+                const int64_t j = base - lane;
+                const uint64_t st = j >= 0 ? ld_agent(&status[j]) : ST_PRE;
+                const uint64_t pre = __ballot((st & ST_PRE) != 0);
+                const uint64_t nr = __ballot((st >> 62) == 0);
+                const int fp = pre ? (int)__builtin_ctzll(pre) : 64;
+                const int fn = nr ? (int)__builtin_ctzll(nr) : 64;
+                if (fn < fp) { __builtin_amdgcn_s_sleep(1); continue; }
+                acc += wave_sum(lane <= fp ? (st & ST_VAL) : 0ull);
+                if (fp < 64) break;
+                base -= 64;
+            }
+            P = acc;
+            if (lane == 0) st_agent(&status[c], ST_PRE | (P + S));
+        }
+        if (lane == 0) ps.P = P;
+    }
+    __syncthreads();
+}
+
+// Store the LDS bit buffer (S bits at local bit 0) at global bit ps.P: interior words with plain
+// coalesced stores, the first and last word to the edge list merged by ndfl_edge_fixup_kernel.
+__device__ __forceinline__ void block_store(const uint32_t* obuf, uint64_t P, uint64_t S, uint32_t c, uint32_t* out,
+                                            uint64_t* edge_w, uint32_t* edge_v) {
+    const int tid = threadIdx.x;
+    const uint32_t sh = (uint32_t)(P & 31);
+    const uint32_t nw = (uint32_t)((sh + S + 31) >> 5);
+    const uint64_t W0 = P >> 5;
+    auto outw = [&](uint32_t k) -> uint32_t {
+        const uint32_t cur = obuf[k];
+        const uint32_t prv = k ? obuf[k - 1] : 0u;
+        return sh ? (cur << sh) | (prv >> (32 - sh)) : cur;
+    };
+    for (uint32_t k = (uint32_t)tid + 1; k + 1 < nw; k += DT) out[W0 + k] = outw(k);
+    if (tid == 0) {
+        edge_w[2 * c] = W0;
+        edge_v[2 * c] = outw(0);
+        edge_w[2 * c + 1] = W0 + nw - 1;
+        edge_v[2 * c + 1] = nw > 1 ? outw(nw - 1) : 0u;
+    }
+}
+
 }  // namespace
 
 extern "C" __global__ void __launch_bounds__(DT, 8)
@@ -271,9 +482,6 @@ ndfl_deflate_chunks_kernel(Args a) {
     uint32_t* hlit = (uint32_t*)(scr + SCR_HLIT);
     uint32_t* hdist = (uint32_t*)(scr + SCR_HDIST);
     uint8_t* lastb = (uint8_t*)(scr + SCR_LAST);
-    uint8_t* lens = (uint8_t*)(scr + SCR_LEN);
-    uint8_t* clLen = (uint8_t*)(scr + SCR_CLLEN);
-    uint32_t* clh = (uint32_t*)(scr + SCR_CLH);
     uint32_t* misc = (uint32_t*)(scr + SCR_MISC);
 
     const int tid = threadIdx.x;
@@ -454,110 +662,7 @@ ndfl_deflate_chunks_kernel(Args a) {
 
     const uint64_t tp2 = wall_clock64();
     // ---- 4. code construction -------------------------------------------------------------------
-    if (!a.dynamic) {
-        // fixed codes (D/comp/Lz77Huffman.java:394-410)
-        if (tid < 288) {
-            uint32_t l = tid < 144 ? 8 : tid < 256 ? 9 : tid < 280 ? 7 : 8;
-            uint32_t code = tid < 144 ? 0x30 + tid : tid < 256 ? 0x190 + (tid - 144) : tid < 280 ? (tid - 256) : 0xC0 + (tid - 280);
-            ps.litCode[tid] = (__brev(code) >> (32 - l)) | (l << 16);
-        }
-        if (tid < 32) ps.distCode[tid] = (__brev((uint32_t)tid) >> 27) | (5u << 16);
-        if (tid == 0) { ps.hdrBits = 3; ps.nsym = 0; }
-        __syncthreads();
-    } else {
-        // trim litlen histogram, keep >= 257 (:148-151)
-        if (tid == 0) {
-            int ln = 286;
-            while (ln > 257 && hlit[ln - 1] == 0) ln--;
-            misc[0] = (uint32_t)ln;
-            // single used distance code -> dummy neighbour (:155-171)
-            int used = 0, first = -1;
-            for (int i = 0; i < 30; i++) if (hdist[i]) { used++; if (first < 0) first = i; }
-            if (used == 1) { if (first < 29) hdist[first + 1] = 1; else hdist[first - 1] = 1; }
-            int dn = 30;
-            while (dn > 1 && hdist[dn - 1] == 0) dn--;
-            misc[1] = (uint32_t)dn;
-            misc[2] = (dn == 1 && hdist[0] == 0) ? 1u : 0u;   // empty distance code
-        }
-        __syncthreads();
-        const int ln = (int)misc[0], dn = (int)misc[1];
-        const bool emptyDist = misc[2] != 0;
-        pm_lengths(hlit, ln, 15, lens, scr);
-        if (emptyDist) { if (tid == 0) lens[ln] = 0; __syncthreads(); }
-        else pm_lengths(hdist, dn, 15, lens + ln, scr);
-        canon_codes(lens, ln, ps.litCode, scr);
-        canon_codes(lens + ln, dn, ps.distCode, scr);
-        // code-length sequence RLE (:187-223) as maximal-run decomposition
-        const int nc = ln + dn;
-        uint32_t rstart = 0xFFFFFFFFu;
-        uint32_t v = 0;
-        if (tid < nc) {
-            v = lens[tid];
-            if (tid == 0 || lens[tid - 1] != v) rstart = (uint32_t)tid;
-        }
-        uint32_t rnext = min(block_excl_suffix_min<NW>(rstart, 0xFFFFFFFFu, ps.scan32), (uint32_t)nc);
-        uint32_t cnt = 0, Z = 0;
-        if (rstart != 0xFFFFFFFFu) {
-            Z = rnext - rstart;
-            if (v == 0) {
-                uint32_t q = Z / 138, r = Z % 138;
-                cnt = q + (r >= 3 ? 1 : r);
-            } else {
-                uint32_t rest = Z - 1, q = rest / 6, r = rest % 6;
-                cnt = 1 + q + (r >= 3 ? 1 : r);
-            }
-        }
-        uint32_t tot;
-        uint32_t off = block_excl_scan<uint32_t, NW>(cnt, ps.scan32, tot);
-        if (rstart != 0xFFFFFFFFu) {
-            uint32_t k = off;
-            if (v == 0) {
-                uint32_t L = Z;
-                while (L > 0) {
-                    uint32_t r = min(L, 138u);
-                    if (r < 3) { ps.clSym[k] = 0; ps.clExtra[k++] = 0; L -= 1; }
-                    else if (r < 11) { ps.clSym[k] = 17; ps.clExtra[k++] = (uint8_t)(r - 3); L -= r; }
-                    else { ps.clSym[k] = 18; ps.clExtra[k++] = (uint8_t)(r - 11); L -= r; }
-                }
-            } else {
-                ps.clSym[k] = (uint8_t)v; ps.clExtra[k++] = 0;
-                uint32_t L = Z - 1;
-                while (L >= 3) { uint32_t r = min(L, 6u); ps.clSym[k] = 16; ps.clExtra[k++] = (uint8_t)(r - 3); L -= r; }
-                while (L > 0) { ps.clSym[k] = (uint8_t)v; ps.clExtra[k++] = 0; L--; }
-            }
-        }
-        if (tid < 20) clh[tid] = 0;
-        __syncthreads();
-        if ((uint32_t)tid < tot) atomicAdd(&clh[ps.clSym[tid]], 1u);
-        __syncthreads();
-        pm_lengths(clh, 19, 7, clLen, scr);
-        canon_codes(clLen, 19, ps.clCode, scr);
-        // per-symbol header bit offsets
-        uint32_t sb = 0;
-        if ((uint32_t)tid < tot) {
-            uint32_t sy = ps.clSym[tid];
-            sb = (ps.clCode[sy] >> 16) + (sy >= 16 ? CL_EXTRA_BITS[sy - 16] : 0);
-        }
-        uint32_t body;
-        uint32_t so = block_excl_scan<uint32_t, NW>(sb, ps.scan32, body);
-        if ((uint32_t)tid < tot) ps.clOff[tid] = (uint16_t)so;
-        if (tid == 0) {
-            const int order[19] = {16, 17, 18, 0, 8, 7, 9, 6, 10, 5, 11, 4, 12, 3, 13, 2, 14, 1, 15};
-            int ncl = 19;
-            while (ncl > 4 && clLen[order[ncl - 1]] == 0) ncl--;    // (:230-234)
-            ps.ncl = (uint32_t)ncl;
-            ps.nsym = tot;
-            ps.hlit = (uint32_t)(ln - 257);
-            ps.hdist = (uint32_t)(dn - 1);
-            ps.clBodyBits = body;
-            ps.hdrBits = 3 + 14 + 3 * (uint32_t)ncl + body;
-            // stash reordered code-length-code lengths in misc[4..] (3 bits each, packed)
-            uint64_t packed = 0;
-            for (int i = 0; i < ncl; i++) packed |= (uint64_t)clLen[order[i]] << (3 * i);
-            misc[4] = (uint32_t)packed; misc[5] = (uint32_t)(packed >> 32);
-        }
-        __syncthreads();
-    }
+    build_block_codes(a.dynamic != 0, scr, ps);
     const uint32_t packedLo = misc[4], packedHi = misc[5];
     __syncthreads();
 
@@ -603,30 +708,7 @@ ndfl_deflate_chunks_kernel(Args a) {
     const uint32_t bit0 = 0;
 
     // ---- 6. emit ------------------------------------------------------------------------------
-    if (tid == 0) {
-        BitPut bp; bp.init(obuf, bit0);
-        bp.put(is_final ? 1u : 0u, 1);
-        bp.put(a.dynamic ? 2u : 1u, 2);
-        if (a.dynamic) {
-            bp.put(ps.hlit, 5);
-            bp.put(ps.hdist, 5);
-            bp.put(ps.ncl - 4, 4);
-            uint64_t packed = (uint64_t)packedLo | (uint64_t)packedHi << 32;
-            for (uint32_t i = 0; i < ps.ncl; i++) bp.put((uint32_t)(packed >> (3 * i)) & 7u, 3);
-        }
-        bp.flush();
-        // end-of-block symbol
-        BitPut be; be.init(obuf, bit0 + hdrBits + tokTotal);
-        be.put(ps.litCode[256] & 0xFFFF, eobLen);
-        be.flush();
-    }
-    if (a.dynamic && (uint32_t)tid < ps.nsym) {
-        const uint32_t sy = ps.clSym[tid];
-        BitPut bp; bp.init(obuf, bit0 + 17 + 3 * ps.ncl + ps.clOff[tid]);
-        bp.put(ps.clCode[sy] & 0xFFFF, ps.clCode[sy] >> 16);
-        if (sy >= 16) bp.put(ps.clExtra[tid], CL_EXTRA_BITS[sy - 16]);
-        bp.flush();
-    }
+    emit_block_header(obuf, is_final, a.dynamic != 0, ps, packedLo, packedHi, hdrBits, tokTotal, eobLen);
     {
         BitPut bp; bp.init(obuf, bit0 + hdrBits + myoff);
         const uint32_t d0c = d0 & 0xFFFF, d0l = d0 >> 16;
@@ -656,48 +738,11 @@ ndfl_deflate_chunks_kernel(Args a) {
 
     const uint64_t tp5e = wall_clock64();
     // ---- 7. look-back, then store shifted to the global bit offset ---------------------------
-    if (wid == 0) {
-        // decoupled look-back, one wave: lane i polls predecessor c-1-i, so 64 predecessors cost
-        // one round trip; the closest inclusive prefix (PRE) ends the walk, aggregates (AGG)
-        // before it are summed, and a not-yet-published predecessor closer than it re-polls.
-        uint64_t P = a.base_bit;
-        if (c > 0) {
-            uint64_t acc = 0;
-            int64_t base = (int64_t)c - 1;
-            for (;;) {
-                const int64_t j = base - lane;
-                const uint64_t st = j >= 0 ? ld_agent(&a.status[j]) : ST_PRE;
-                const uint64_t pre = __ballot((st & ST_PRE) != 0);
-                const uint64_t nr = __ballot((st >> 62) == 0);
-                const int fp = pre ? (int)__builtin_ctzll(pre) : 64;
-                const int fn = nr ? (int)__builtin_ctzll(nr) : 64;
-                if (fn < fp) { __builtin_amdgcn_s_sleep(1); continue; }
-                acc += wave_sum(lane <= fp ? (st & ST_VAL) : 0ull);
-                if (fp < 64) break;
-                base -= 64;
-            }
-            P = acc;
-            if (lane == 0) st_agent(&a.status[c], ST_PRE | (P + S));
-        }
-        if (lane == 0) ps.P = P;
-    }
-    __syncthreads();
+    block_lookback(c, a.base_bit, S, a.status, ps);
     const uint64_t tp5 = wall_clock64();
     const uint64_t P = ps.P;
-    const uint32_t sh = (uint32_t)(P & 31);
-    const uint32_t nw = (uint32_t)((sh + S + 31) >> 5);
-    const uint64_t W0 = P >> 5;
-    auto outw = [&](uint32_t k) -> uint32_t {
-        const uint32_t cur = obuf[k];
-        const uint32_t prv = k ? obuf[k - 1] : 0u;
-        return sh ? (cur << sh) | (prv >> (32 - sh)) : cur;
-    };
-    for (uint32_t k = (uint32_t)tid + 1; k + 1 < nw; k += DT) a.out[W0 + k] = outw(k);
+    block_store(obuf, P, S, c, a.out, a.edge_w, a.edge_v);
     if (tid == 0) {
-        a.edge_w[2 * c] = W0;
-        a.edge_v[2 * c] = outw(0);
-        a.edge_w[2 * c + 1] = W0 + nw - 1;
-        a.edge_v[2 * c + 1] = nw > 1 ? outw(nw - 1) : 0u;
         if (a.prof) {
             uint64_t* q = a.prof + (uint64_t)c * 8;
             q[0] = tp0; q[1] = tp1; q[2] = tp2; q[3] = tp3; q[4] = tp4; q[5] = tp5e; q[6] = tp5;

@@ -627,30 +627,31 @@ struct InflateScratch {
     SegPool pool{};
     void* d_chains = nullptr; size_t d_chains_cap = 0;
     void* d_off = nullptr; size_t d_off_cap = 0;
-    void* d_done = nullptr; size_t d_done_cap = 0;
-    void* d_taint = nullptr; size_t d_taint_cap = 0;
-    void* d_sel = nullptr; size_t d_sel_cap = 0;
+    void* d_ref = nullptr; size_t d_ref_cap = 0;      // emit: back-reference per output byte (deferred copies)
+    void* d_pend = nullptr; size_t d_pend_cap = 0;    // emit: pending bit per output byte
+    void* d_rl = nullptr; size_t d_rl_cap = 0;        // resolve: two group lists + round bits
     void* d_ticket = nullptr;
     void* d_ph = nullptr;                             // count pass: phase-fallback slot per wave
     void* d_cticket = nullptr;                        // count pass: chain tickets (one per launch)
     void* d_out = nullptr; size_t d_out_cap = 0;
     double last_ms_find = 0, last_ms_count = 0, last_ms_emit = 0, last_ms_wall = 0;
     hipEvent_t ev[6] = {nullptr, nullptr, nullptr, nullptr, nullptr, nullptr};
-    uint64_t repairs = 0, chains = 0, candidates = 0;
+    uint64_t repairs = 0, chains = 0, candidates = 0, resolved_groups = 0;
+    void* h_cnt = nullptr;                            // pinned: resolve list size
     bool count_first = false;
     // state kept for ndfl_inflate_resolve after a deferred-window range decode
     bool pending = false;
-    const uint32_t* p_w = nullptr;
-    uint64_t p_nwords = 0, p_nbits = 0, p_dict_len = 0;
     uint8_t* p_out = nullptr;
-    uint32_t p_nch = 0, p_ncand = 0;
+    uint64_t p_nbytes = 0;
     void release() {
         void** ps[] = {&d_in, &d_cand, &d_starts, &d_stops, &d_res, &d_cands, &d_stats, &d_q, &d_seg, &d_chains, &d_off,
-                       &d_done, &d_taint, &d_sel, &d_ticket, &d_ph, &d_cticket, &d_out};
+                       &d_ref, &d_pend, &d_rl, &d_ticket, &d_ph, &d_cticket, &d_out};
         for (void** p : ps) { if (*p) hipFree(*p); *p = nullptr; }
         for (auto& e : ev) { if (e) hipEventDestroy(e); e = nullptr; }
+        if (h_cnt) hipHostFree(h_cnt);
+        h_cnt = nullptr;
         d_in_cap = d_cand_cap = d_starts_cap = d_stops_cap = d_res_cap = d_cands_cap = d_seg_cap = d_q_cap = d_chains_cap = 0;
-        d_off_cap = d_done_cap = d_taint_cap = d_sel_cap = d_out_cap = 0;
+        d_off_cap = d_ref_cap = d_pend_cap = d_rl_cap = d_out_cap = 0;
         pending = false;
     }
 };
@@ -666,6 +667,51 @@ static hipError_t inf_ensure(void** p, size_t* cap, size_t n) {
 
 
 #define INF_CHK(x) do { hipError_t _e = (x); if (_e != hipSuccess) return -4; } while (0)
+
+// Resolve the deferred copies of an emit pass: pointer-jumping rounds over the pending 32-byte
+// groups of out[0, nbytes) until none is left.  *groups = pending groups at the start.
+static int resolve_rounds(InflateScratch& S, hipStream_t s, uint8_t* d_out, uint64_t nbytes, uint64_t* groups) {
+    using namespace inf;
+    *groups = 0;
+    const uint64_t npw = (nbytes + 31) / 32;
+    if (npw == 0) return 0;
+    if (npw > 0xFFFFFFFFull) return -2;
+    INF_CHK(inf_ensure(&S.d_rl, &S.d_rl_cap, npw * 12 + 64));
+    uint32_t* cnt = (uint32_t*)S.d_rl;                       // [0], [1]: list sizes
+    uint32_t* lst[2] = {(uint32_t*)((char*)S.d_rl + 64), (uint32_t*)((char*)S.d_rl + 64) + npw};
+    uint32_t* nb = lst[1] + npw;
+    uint32_t* pend = (uint32_t*)S.d_pend;
+    uint32_t* ref = (uint32_t*)S.d_ref;
+    INF_CHK(hipMemsetAsync(cnt, 0, 8, s));
+    hipLaunchKernelGGL(ndfl_inflate_pending_list_kernel, dim3((uint32_t)((npw + 255) / 256)), dim3(256), 0, s,
+                       (const uint32_t*)pend, (uint64_t)0, npw, lst[0], cnt);
+    INF_CHK(hipGetLastError());
+    uint32_t* h = (uint32_t*)S.h_cnt;
+    // rounds are queued four at a time on grid-stride kernels; the host reads the list size between
+    // batches only (pointer jumping needs ~log2(reference depth) rounds)
+    int cur = 0;
+    uint32_t n = 0;
+    for (int round = 0;; round++) {
+        if ((round & 3) == 0) {
+            INF_CHK(hipMemcpyAsync(h, cnt + cur, 4, hipMemcpyDeviceToHost, s));
+            INF_CHK(hipStreamSynchronize(s));
+            n = *h;
+            if (round == 0) *groups = n;
+            if (n == 0) return 0;
+            if (round >= 48) return R_INTERNAL;              // distances double each round: unreachable
+        }
+        INF_CHK(hipMemsetAsync(cnt + (cur ^ 1), 0, 4, s));
+        const uint32_t gb = (uint32_t)std::min<uint64_t>(4096, ((uint64_t)n * 32 + 255) / 256);
+        hipLaunchKernelGGL(ndfl_inflate_resolve_kernel, dim3(gb), dim3(256), 0, s,
+                           (const uint32_t*)lst[cur], (const uint32_t*)(cnt + cur), (const uint32_t*)pend, ref, d_out, nb);
+        INF_CHK(hipGetLastError());
+        hipLaunchKernelGGL(ndfl_inflate_resolve_apply_kernel, dim3((uint32_t)std::min<uint64_t>(1024, (n + 255) / 256)),
+                           dim3(256), 0, s, (const uint32_t*)lst[cur], (const uint32_t*)(cnt + cur), pend,
+                           (const uint32_t*)nb, lst[cur ^ 1], cnt + (cur ^ 1));
+        INF_CHK(hipGetLastError());
+        cur ^= 1;
+    }
+}
 
 // Decode one raw DEFLATE stream, or the block-aligned range [start_bit, end_bit) of one.
 //   out       the window start: out[0, dict_len) holds the dict_len bytes of output preceding the
@@ -911,15 +957,9 @@ static int inflate_run(InflateScratch& S, hipStream_t s, const uint8_t* in, uint
     // emit pass
     const uint32_t nch = (uint32_t)chains.size();
     INF_CHK(inf_ensure(&S.d_chains, &S.d_chains_cap, nch * sizeof(EmitChain)));
-    INF_CHK(inf_ensure(&S.d_off, &S.d_off_cap, (nch + 1) * 8ull));
-    INF_CHK(inf_ensure(&S.d_done, &S.d_done_cap, nch * 4ull));
     INF_CHK(inf_ensure(&S.d_res, &S.d_res_cap, nch * sizeof(ChainRes)));
-    if (deferred) INF_CHK(inf_ensure(&S.d_taint, &S.d_taint_cap, nch * 4ull));
     if (!S.d_ticket) INF_CHK(hipMalloc(&S.d_ticket, 64));
     INF_CHK(hipMemcpyAsync(S.d_chains, chains.data(), nch * sizeof(EmitChain), hipMemcpyHostToDevice, s));
-    offs.push_back(off);
-    INF_CHK(hipMemcpyAsync(S.d_off, offs.data(), (nch + 1) * 8ull, hipMemcpyHostToDevice, s));
-    INF_CHK(hipMemsetAsync(S.d_done, 0, nch * 4ull, s));
     INF_CHK(hipMemsetAsync(S.d_ticket, 0, 64, s));
     uint8_t* d_out;
     const bool direct = (flags & 2u) != 0;
@@ -929,14 +969,20 @@ static int inflate_run(InflateScratch& S, hipStream_t s, const uint8_t* in, uint
         d_out = (uint8_t*)S.d_out;
         if (dict_len) INF_CHK(hipMemcpyAsync(d_out, out, dict_len, hipMemcpyHostToDevice, s));
     }
+    const uint64_t nbytes = dict_len + total;
+    if (nbytes > (1ull << 32)) return -2;                    // u32 back-references (indices < 2^32)
+    const uint64_t npw = (nbytes + 31) / 32;
+    INF_CHK(inf_ensure(&S.d_ref, &S.d_ref_cap, nbytes * 4 + 64));
+    INF_CHK(inf_ensure(&S.d_pend, &S.d_pend_cap, npw * 4 + 64));
+    INF_CHK(hipMemsetAsync(S.d_pend, 0, npw * 4 + 64, s));
+    if (!S.h_cnt) INF_CHK(hipHostMalloc(&S.h_cnt, 64, 0));
     hipEvent_t e2 = S.ev[4], e3 = S.ev[5];
     INF_CHK(hipEventRecord(e2, s));
     if (!S.d_ph) INF_CHK(hipMalloc(&S.d_ph, (size_t)COUNT_WAVES * sizeof(wv::PhArr)));
     hipLaunchKernelGGL(ndfl_inflate_emit_wave_kernel, dim3(std::min<uint32_t>(nch, COUNT_WAVES)), dim3(64), 0, s, d_w,
-                       nwords, nbits, (const EmitChain*)S.d_chains, (const uint64_t*)S.d_off, nch, (uint32_t*)S.d_done,
-                       (uint32_t*)S.d_ticket, d_out, (ChainRes*)S.d_res, (const uint64_t*)S.d_cands, ncand, dict_len,
-                       deferred ? (uint32_t*)S.d_taint : (uint32_t*)nullptr, (const uint32_t*)nullptr, pool,
-                       (wv::PhArr*)S.d_ph);
+                       nwords, nbits, (const EmitChain*)S.d_chains, nch, (uint32_t*)S.d_ticket, d_out,
+                       (ChainRes*)S.d_res, (const uint64_t*)S.d_cands, ncand, (uint32_t*)S.d_ref, (uint32_t*)S.d_pend,
+                       pool, (wv::PhArr*)S.d_ph);
     INF_CHK(hipGetLastError());
     INF_CHK(hipEventRecord(e3, s));
     std::vector<ChainRes> er(nch);
@@ -945,14 +991,22 @@ static int inflate_run(InflateScratch& S, hipStream_t s, const uint8_t* in, uint
     float ms = 0;
     hipEventElapsedTime(&ms, e2, e3);
     S.last_ms_emit = ms;
+    if (deferred) {
+        S.pending = true;
+        S.p_out = d_out; S.p_nbytes = nbytes;
+    } else {
+        uint64_t groups = 0;
+        const int rr = resolve_rounds(S, s, d_out, nbytes, &groups);
+        if (rr) return rr;
+        S.resolved_groups = groups;
+    }
+    INF_CHK(hipEventRecord(e3, s));
+    INF_CHK(hipStreamSynchronize(s));
     float ms2 = 0;
     hipEventElapsedTime(&ms2, S.ev[0], e3);
     S.last_ms_wall = ms2;
-    *last_ms = ms;
-    if (deferred) {
-        S.pending = true;
-        S.p_w = d_w; S.p_nwords = nwords; S.p_nbits = nbits; S.p_dict_len = dict_len; S.p_out = d_out; S.p_nch = nch; S.p_ncand = ncand;
-    }
+    hipEventElapsedTime(&ms2, e2, e3);
+    *last_ms = ms2;
     // first error in stream order (the emit pass also checks the dictionary bound exactly)
     for (uint32_t k = 0; k < nch; k++) {
         if (er[k].status == ST_ERROR) {
@@ -970,35 +1024,15 @@ static int inflate_run(InflateScratch& S, hipStream_t s, const uint8_t* in, uint
 }
 
 // Second half of a deferred-window range decode: the caller has written the window
-// (out[0, dict_len)); re-emit, in stream order, exactly the chains that read it.
-static int inflate_resolve(InflateScratch& S, hipStream_t s, uint64_t* n_reemitted) {
+// (out[0, dict_len)); resolve every deferred copy (those that read the window directly or through
+// other copies included).  *n_resolved = pending 32-byte groups at the start.
+static int inflate_resolve(InflateScratch& S, hipStream_t s, uint64_t* n_resolved) {
     using namespace inf;
-    *n_reemitted = 0;
+    *n_resolved = 0;
     if (!S.pending) return -5;
     S.pending = false;
-    const uint32_t nch = S.p_nch;
-    std::vector<uint32_t> taint(nch);
-    INF_CHK(hipMemcpyAsync(taint.data(), S.d_taint, nch * 4ull, hipMemcpyDeviceToHost, s));
-    INF_CHK(hipStreamSynchronize(s));
-    std::vector<uint32_t> sel, done(nch);
-    for (uint32_t k = 0; k < nch; k++) {
-        done[k] = taint[k] ? 0u : 1u;
-        if (taint[k]) sel.push_back(k);
-    }
-    *n_reemitted = sel.size();
-    if (sel.empty()) return 0;
-    const uint32_t nsel = (uint32_t)sel.size();
-    INF_CHK(inf_ensure(&S.d_sel, &S.d_sel_cap, nsel * 4ull));
-    INF_CHK(hipMemcpyAsync(S.d_sel, sel.data(), nsel * 4ull, hipMemcpyHostToDevice, s));
-    INF_CHK(hipMemcpyAsync(S.d_done, done.data(), nch * 4ull, hipMemcpyHostToDevice, s));
-    INF_CHK(hipMemsetAsync(S.d_ticket, 0, 64, s));
-    if (!S.d_ph) INF_CHK(hipMalloc(&S.d_ph, (size_t)COUNT_WAVES * sizeof(wv::PhArr)));
-    hipLaunchKernelGGL(ndfl_inflate_emit_wave_kernel, dim3(std::min<uint32_t>(nsel, COUNT_WAVES)), dim3(64), 0, s,
-                       S.p_w, S.p_nwords, S.p_nbits, (const EmitChain*)S.d_chains, (const uint64_t*)S.d_off, nsel,
-                       (uint32_t*)S.d_done, (uint32_t*)S.d_ticket, S.p_out, (ChainRes*)S.d_res,
-                       (const uint64_t*)S.d_cands, S.p_ncand, S.p_dict_len, (uint32_t*)nullptr,
-                       (const uint32_t*)S.d_sel, S.pool, (wv::PhArr*)S.d_ph);
-    INF_CHK(hipGetLastError());
-    INF_CHK(hipStreamSynchronize(s));
+    const int rr = resolve_rounds(S, s, S.p_out, S.p_nbytes, n_resolved);
+    if (rr) return rr;
+    S.resolved_groups = *n_resolved;
     return 0;
 }

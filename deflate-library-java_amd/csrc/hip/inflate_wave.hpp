@@ -991,18 +991,18 @@ ndfl_inflate_count_wave_kernel(const uint32_t* w, uint64_t nwords, uint64_t nbit
     }
 }
 
-// Emit pass: persistent waves claiming the linked chains in stream order through `ticket` (a
-// claimed chain is always running, so waiting on earlier chains cannot deadlock).
+// Emit pass: persistent waves claiming the linked chains through `ticket`.  No lane and no chain
+// ever waits on another: a copy whose source lies before the lane's own output (an earlier lane,
+// an earlier chain, the window), or reaches the lane's first deferred byte, is not executed but
+// deferred -- its bytes get a back-reference (ref[i] = distance to a byte holding the same value)
+// and a pending bit, and ndfl_inflate_resolve_kernel rounds resolve them afterwards by pointer
+// jumping.  So every chain decodes in parallel whatever the LZ77 distances.
 extern "C" __global__ void __launch_bounds__(64, 4)
 ndfl_inflate_emit_wave_kernel(const uint32_t* w, uint64_t nwords, uint64_t nbits, const EmitChain* chains,
-                              const uint64_t* chain_off, uint32_t nlist, uint32_t* done, uint32_t* ticket,
-                              uint8_t* out, ChainRes* res, const uint64_t* cands, uint32_t ncand, uint64_t dict_len,
-                              uint32_t* taint, const uint32_t* sel, SegPool pool, wv::PhArr* ph_all) {
+                              uint32_t nlist, uint32_t* ticket, uint8_t* out, ChainRes* res, const uint64_t* cands,
+                              uint32_t ncand, uint32_t* ref, uint32_t* pend, SegPool pool, wv::PhArr* ph_all) {
     using namespace wv;
     __shared__ Shared S;
-    __shared__ uint64_t E_off[64];               // absolute output offset per lane
-    __shared__ uint64_t E_cnt[64];               // output bytes per lane
-    __shared__ uint32_t E_prog[64];              // bytes durably written per lane
     __shared__ uint32_t s_ticket;
     const int lane = threadIdx.x;
     gu8* gout = (gu8*)out;
@@ -1011,15 +1011,13 @@ ndfl_inflate_emit_wave_kernel(const uint32_t* w, uint64_t nwords, uint64_t nbits
     __syncthreads();
     if (lane == 0) s_ticket = atomicAdd(ticket, 1u);
     __syncthreads();
-    const uint32_t k = s_ticket;
-    if (k >= nlist) break;
-    const uint32_t ci = sel ? sel[k] : k;
+    const uint32_t ci = s_ticket;
+    if (ci >= nlist) break;
     const In in{w, nwords, nbits};
     const EmitChain ch = chains[ci];
     uint64_t cur = ch.start_bit, base = ch.out_off;
     uint32_t status = ST_BOUNDARY, reason = 0;
     uint64_t endpos = ch.start_bit;
-    bool tainted = false;
     uint32_t nslow = 0, nfix = 0;
     uint32_t rec = ch.slot < pool.nslot ? pool.head[ch.slot] : NOREC;
     for (int blk = 0;; blk++) {
@@ -1040,9 +1038,6 @@ ndfl_inflate_emit_wave_kernel(const uint32_t* w, uint64_t nwords, uint64_t nbits
                 out[base + i] = (uint8_t)(in.ld(b >> 2) >> (8 * (uint32_t)(b & 3)));
             }
             base += take;
-            __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
-            __syncthreads();
-            __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup");
             if (take < ln) { status = ST_ERROR; reason = R_UEOS; endpos = d0 + 8 * avail; break; }
             cur = d0 + 8 * ln;
             if (bfinal) { status = ST_FINAL; endpos = cur; break; }
@@ -1072,16 +1067,11 @@ ndfl_inflate_emit_wave_kernel(const uint32_t* w, uint64_t nwords, uint64_t nbits
                 if (E <= rs) E = rs + 1;
                 round_decode(in, S.t, ed, rs, E, S, lane, r, ft, nslow, nfix, S_ph);
             }
-            // offsets of this round's lanes
             const bool live = (uint32_t)lane <= ft;
             const uint64_t mycnt = live ? r.cnt : 0ull;
             const uint64_t pre = wave_excl_u64(mycnt, lane);
             const uint64_t rsum = wave_sum_u64(mycnt);
-            E_off[lane] = base + pre;
-            E_cnt[lane] = mycnt;
-            E_prog[lane] = 0;
-            __syncthreads();
-            // write pass (budgeted steps; a lane waiting on another lane or chain skips its turn)
+            // write pass: every lane runs its segment to the end on its own
             WLane L;
             const RB rb = make_rb(in, rs);
             L.rd.init(rb, (uint32_t)(r.start - rb.base));
@@ -1089,97 +1079,51 @@ ndfl_inflate_emit_wave_kernel(const uint32_t* w, uint64_t nwords, uint64_t nbits
             L.cp_len = 0; L.cp_dist = 0; L.lastb = 0; L.wc = 0; L.wcn = 0;
             L.q0 = L.q1 = L.q2 = L.q3 = 0; L.qn = 0; L.qaddr = 0; L.lastqw = L.rd.qw;
             L.kind = r.kind; L.reason = r.reason;
-            L.active = live; L.tainted = false;
-            uint32_t waits = 0;
-            int idle = 0;
-            while (__any(L.active)) {
-                bool waiting = false;
-                if (L.active) {
-                    for (int b = 0; b < BUDGET; b++) {
-                        if (L.cp_len == 0) {
-                            if (L.rd.pos >= L.end && L.kind == T_EXIT) { L.active = false; break; }
-                            Tok tk;
-                            next_tok(L.rd, rb, S.t, ed, L.end, tk);
-                            if (tk.kind == K_LIT) {
-                                wputb(L, gout, L.dst0 + L.n, tk.val & 0xFFu);
-                                L.n++;
-                                if (tk.n == 2) { wputb(L, gout, L.dst0 + L.n, tk.val >> 8); L.n++; }
-                                if (L.rd.qw != L.lastqw) { wq_flush(L, gout); L.lastqw = L.rd.qw; }
-                                L.lastb = tk.val >> (tk.n == 2 ? 8 : 0);
-                                continue;
-                            }
-                            if (tk.kind != K_LEN) { L.active = false; break; }     // EOB or error (as verified)
-                            if ((uint64_t)tk.dist > L.dst0 + L.n) {
-                                L.kind = T_ERR; L.reason = R_COPY_BEFORE; L.end = L.rd.pos; L.active = false; break;
-                            }
-                            L.cp_len = tk.val; L.cp_dist = tk.dist;
-                        }
-                        const uint64_t dst = L.dst0 + L.n;
-                        const uint64_t src = dst - L.cp_dist;
-                        if (src < L.dst0 && !(L.cp_dist == 1 && L.n > 0)) {
-                            const uint64_t src_end = min(dst, src + L.cp_len);
-                            if (src < dict_len) L.tainted = true;
-                            bool ok = true;
-                            // bytes of earlier lanes of this round
-                            if (src_end > E_off[0]) {
-                                for (int j = lane - 1; j >= 0; j--) {
-                                    const uint64_t o = E_off[j];
-                                    if (o + E_cnt[j] <= src) break;
-                                    const uint64_t need = min(o + E_cnt[j], src_end) - max(o, src);
-                                    const uint64_t have = E_prog[j];
-                                    if (max(o, src) + need > o + have) { ok = false; break; }
-                                    if (o <= src) break;
-                                }
-                            }
-                            // bytes of earlier chains
-                            if (ok && src < ch.out_off && src_end > dict_len) {
-                                const uint64_t s0 = max(src, dict_len);
-                                const uint64_t se = min(src_end, ch.out_off);
-                                uint32_t lo = 0, hi = ci;
-                                while (lo + 1 < hi) {
-                                    const uint32_t mid = (lo + hi) >> 1;
-                                    if (chain_off[mid] <= s0) lo = mid; else hi = mid;
-                                }
-                                uint32_t need_hi = lo;
-                                while (need_hi + 1 < ci && chain_off[need_hi + 1] < se) need_hi++;
-                                for (uint32_t j = lo; j <= need_hi && ok; j++)
-                                    if (__hip_atomic_load(&done[j], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == 0) ok = false;
-                                if (ok && taint)
-                                    for (uint32_t j = lo; j <= need_hi; j++) L.tainted |= taint[j] != 0;
-                            }
-#ifdef NDFL_EXP_NOWAIT
-                            ok = true;
-#endif
-                            if (!ok) { waiting = true; break; }
-                            // the sources were stored by this wave (same vmcnt) or published by an
-                            // earlier chain (agent release): drain, then invalidate L1 before reading
-                            asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-                            __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
-                        }
-#ifndef NDFL_EXP_NOCOPY
-                        wcopy(L, gout, dst, src, L.cp_len, L.cp_dist);
-#endif
-                        L.n += L.cp_len;
-                        L.cp_len = 0;
-                    }
-                    if (!L.active) wflush(L, gout, L.dst0 + L.n);
-                    if (waiting && ++waits > (1u << 24)) {          // safety net: never hang the device
-                        L.active = false; L.kind = T_ERR; L.reason = R_INTERNAL;
-                    }
+            L.active = live;
+            uint64_t dfr = ~0ull;           // first deferred byte of this lane (absolute)
+            uint64_t lastsrc = 0;           // a byte holding the value of the last output byte
+            while (L.active) {
+                Tok tk;
+                if (L.rd.pos >= L.end && L.kind == T_EXIT) { L.active = false; break; }
+                next_tok(L.rd, rb, S.t, ed, L.end, tk);
+                if (tk.kind == K_LIT) {
+                    wputb(L, gout, L.dst0 + L.n, tk.val & 0xFFu);
+                    L.n++;
+                    if (tk.n == 2) { wputb(L, gout, L.dst0 + L.n, tk.val >> 8); L.n++; }
+                    if (L.rd.qw != L.lastqw) { wq_flush(L, gout); L.lastqw = L.rd.qw; }
+                    L.lastb = tk.val >> (tk.n == 2 ? 8 : 0);
+                    lastsrc = L.dst0 + L.n - 1;
+                    continue;
                 }
-                // progress = bytes issued to memory; a reader drains the wave's vmcnt before using
-                // them.  A lane that stopped on an error releases its waiters: what follows an error is
-                // never reported, so they may read anything
-                E_prog[lane] = (!L.active && L.kind == T_ERR) ? 0xFFFFFFFFu
-                                                              : (uint32_t)min(L.n - L.wcn - 4 * L.qn, (uint64_t)0xFFFFFFFFu);
-                __syncthreads();
-                if (__all(!L.active || waiting)) { if (++idle > 2) __builtin_amdgcn_s_sleep(2); }
-                else idle = 0;
+                if (tk.kind != K_LEN) { L.active = false; break; }     // EOB or error (as verified)
+                if ((uint64_t)tk.dist > L.dst0 + L.n) {
+                    L.kind = T_ERR; L.reason = R_COPY_BEFORE; L.end = L.rd.pos; L.active = false; break;
+                }
+                const uint32_t len = tk.val, dist = tk.dist;
+                const uint64_t dst = L.dst0 + L.n;
+                const uint64_t src = dst - dist;
+                const uint64_t src_end = src + min(len, dist);          // the copy's bytes before dst
+                if (src >= L.dst0 && src_end <= dfr) {
+                    wcopy(L, gout, dst, src, len, dist);                // sources final and our own
+                    lastsrc = dst + len - 1;
+                } else {
+                    // deferred: back-references (a dist-1 run points at the byte its value comes
+                    // from), pending bits; the bytes are written by the resolve rounds
+                    wflush(L, gout, dst);
+                    const uint64_t anchor = dist == 1 ? (L.n > 0 ? lastsrc : src) : 0;
+                    for (uint32_t k = 0; k < len; k++)
+                        ref[dst + k] = dist == 1 ? (uint32_t)(dst + k - anchor) : dist;
+                    for (uint64_t q = dst >> 5; q <= (dst + len - 1) >> 5; q++) {
+                        const uint64_t lo = max(dst, q << 5), hi = min(dst + len, (q + 1) << 5);
+                        const uint32_t m = (uint32_t)(((1ull << (hi - lo)) - 1) << (lo & 31));
+                        atomicOr(&pend[q], m);
+                    }
+                    if (dist == 1) lastsrc = anchor; else lastsrc = dst + len - 1;
+                    dfr = min(dfr, dst);
+                }
+                L.n += len;
             }
-            __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
-            __syncthreads();
-            __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup");
-            tainted |= __any(L.tainted);
+            wflush(L, gout, L.dst0 + L.n);
             // the first lane (in stream order) that ended with an error decides
             const uint64_t em = __ballot(live && L.kind == T_ERR);
             if (em) {
@@ -1202,17 +1146,78 @@ ndfl_inflate_emit_wave_kernel(const uint32_t* w, uint64_t nwords, uint64_t nbits
         }
         if (chain_done) break;
     }
-    // publish: output complete -> done flag (release, agent scope)
-    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    __syncthreads();
     if (lane == 0) {
-        if (taint) taint[ci] = tainted ? 1u : 0u;
         ChainRes o;
         o.end_bit = endpos; o.out_count = base - ch.out_off; o.status = status; o.reason = reason;
         res[ci] = o;
-        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
-        __hip_atomic_store(&done[ci], 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     }
+    }
+}
+
+// ---- resolve rounds -------------------------------------------------------------------------------
+// Pending bytes form 32-byte groups (one bitmap word each) listed in `list`.  A wave takes two
+// groups, a lane one byte i: with p = i - ref[i], a final p gives out[i] = out[p]; a pending p makes
+// i jump (ref[i] += ref[p]), so the remaining distance to a final byte halves each round.  Bits and
+// bytes read here were settled by earlier launches; ref[p] may be updated concurrently, but both its
+// old and new values point at a byte of the same value.
+extern "C" __global__ void __launch_bounds__(256)
+ndfl_inflate_resolve_kernel(const uint32_t* list, const uint32_t* nlist, const uint32_t* pend, uint32_t* ref,
+                            uint8_t* out, uint32_t* newbits) {
+    const uint32_t n = *nlist;
+    const uint32_t b = threadIdx.x & 31;
+    for (uint32_t k = (blockIdx.x * 256 + threadIdx.x) >> 5; k < n; k += gridDim.x * 8) {
+        const uint64_t wd = list[k];
+        const uint32_t bits = pend[wd];
+        bool still = false;
+        if ((bits >> b) & 1) {
+            const uint64_t i = wd * 32 + b;
+            const uint32_t d = ref[i];
+            const uint64_t p = i - d;
+            if ((pend[p >> 5] >> (p & 31)) & 1) {
+                ref[i] = d + ref[p];
+                still = true;
+            } else {
+                out[i] = out[p];
+            }
+        }
+        const uint64_t m = __ballot(still);
+        if (b == 0) newbits[k] = (uint32_t)(m >> (threadIdx.x & 32));
+    }
+}
+
+// Apply a round's bits and compact the list of still-pending groups (grid-stride: the grid is sized
+// before the list size is known).
+extern "C" __global__ void __launch_bounds__(256)
+ndfl_inflate_resolve_apply_kernel(const uint32_t* list, const uint32_t* nlist, uint32_t* pend, const uint32_t* newbits,
+                                  uint32_t* list_out, uint32_t* nlist_out) {
+    const uint32_t n = *nlist;
+    for (uint32_t k0 = blockIdx.x * 256; k0 < n; k0 += gridDim.x * 256) {
+        const uint32_t k = k0 + threadIdx.x;
+        const bool live = k < n;
+        uint32_t nb = 0, wd = 0;
+        if (live) { wd = list[k]; nb = newbits[k]; pend[wd] = nb; }
+        const uint64_t m = __ballot(live && nb != 0);
+        if (m) {
+            const int lane = threadIdx.x & 63;
+            uint32_t base = 0;
+            if (lane == 0) base = atomicAdd(nlist_out, (uint32_t)__popcll(m));
+            base = __shfl(base, 0, 64);
+            if (live && nb) list_out[base + __popcll(m & ((1ull << lane) - 1))] = wd;
+        }
+    }
+}
+
+// Initial list: every non-zero bitmap word in [w0, w1).
+extern "C" __global__ void __launch_bounds__(256)
+ndfl_inflate_pending_list_kernel(const uint32_t* pend, uint64_t w0, uint64_t w1, uint32_t* list, uint32_t* nlist) {
+    const uint64_t wd = w0 + (uint64_t)blockIdx.x * 256 + threadIdx.x;
+    const bool nz = wd < w1 && pend[wd] != 0;
+    const uint64_t m = __ballot(nz);
+    if (m) {
+        const int lane = threadIdx.x & 63;
+        uint32_t base = 0;
+        if (lane == 0) base = atomicAdd(nlist, (uint32_t)__popcll(m));
+        base = __shfl(base, 0, 64);
+        if (nz) list[base + __popcll(m & ((1ull << lane) - 1))] = (uint32_t)wd;
     }
 }

@@ -19,7 +19,7 @@ import io
 from . import _lib
 from ._lib import IN_DEVICE, OUT_DEVICE, DICT_DEFERRED, NO_END, STRATEGIES, NdflError, check, load, reason_name
 
-__all__ = ["Context", "Reason", "DataFormatException", "DeflaterOutputStream", "InflaterInputStream",
+__all__ = ["Context", "Reason", "DataFormatException", "Lz77Huffman", "DeflaterOutputStream", "InflaterInputStream",
            "GzipMetadata", "GzipOutputStream", "GzipInputStream", "ZlibMetadata", "ZlibOutputStream",
            "ZlibInputStream", "Strategy", "default_context", "compress", "decompress", "crc32_combine"]
 
@@ -68,6 +68,40 @@ class Strategy(enum.Enum):
     FULL_STATIC = 4
     FULL_DYNAMIC = 5
     UNCOMPRESSED = 6
+
+
+class Lz77Huffman:
+    """The Lz77Huffman record (D/comp/Lz77Huffman.java:20-39): greedy longest-match LZ77 over
+    distances [searchMinimumDistance, searchMaximumDistance] with runs in [searchMinimumRunLength,
+    searchMaximumRunLength], then static or dynamic Huffman codes.  Validation as :28-38
+    (ValueError = IllegalArgumentException).  Presets as class attributes (:298-305)."""
+
+    def __init__(self, useDynamicHuffmanCodes, searchMinimumRunLength, searchMaximumRunLength,
+                 searchMinimumDistance, searchMaximumDistance):
+        p = (searchMinimumRunLength, searchMaximumRunLength, searchMinimumDistance, searchMaximumDistance)
+        mnr, mxr, mnd, mxd = p
+        if not (p == (0, 0, 0, 0) or (3 <= mnr <= mxr <= 258 and 1 <= mnd <= mxd <= 32768)):
+            raise ValueError("Invalid minimum/maximum run-length/distance")
+        self.useDynamicHuffmanCodes = bool(useDynamicHuffmanCodes)
+        self.params = p
+
+    def __eq__(self, other):
+        return isinstance(other, Lz77Huffman) and (self.useDynamicHuffmanCodes, self.params) == \
+            (other.useDynamicHuffmanCodes, other.params)
+
+    def __hash__(self):
+        return hash((self.useDynamicHuffmanCodes, self.params))
+
+    def __repr__(self):
+        return f"Lz77Huffman({self.useDynamicHuffmanCodes}, {', '.join(map(str, self.params))})"
+
+
+Lz77Huffman.LITERAL_STATIC = Lz77Huffman(False, 0, 0, 0, 0)
+Lz77Huffman.LITERAL_DYNAMIC = Lz77Huffman(True, 0, 0, 0, 0)
+Lz77Huffman.RLE_STATIC = Lz77Huffman(False, 3, 258, 1, 1)
+Lz77Huffman.RLE_DYNAMIC = Lz77Huffman(True, 3, 258, 1, 1)
+Lz77Huffman.FULL_STATIC = Lz77Huffman(False, 3, 258, 1, 32768)
+Lz77Huffman.FULL_DYNAMIC = Lz77Huffman(True, 3, 258, 1, 32768)
 
 
 def _ptr(obj):
@@ -122,10 +156,17 @@ class Context:
         L = load()
         endbits = ctypes.c_uint64(0)
         crcv = ctypes.c_uint32(crc if crc is not None else 0)
-        r = L.ndfl_deflate_chunks(self._h, hist_addr, hist_len, hist_limit, data_addr, n, chunk_len, strategy,
-                                  int(final), start_bitpos, out_addr, out_cap, ctypes.byref(endbits),
-                                  ctypes.byref(crcv) if crc is not None else None, flags)
-        check(r, "ndfl_deflate_chunks")
+        crcp = ctypes.byref(crcv) if crc is not None else None
+        if isinstance(strategy, Lz77Huffman):
+            r = L.ndfl_deflate_chunks_lz77(self._h, hist_addr, hist_len, hist_limit, data_addr, n, chunk_len,
+                                           int(strategy.useDynamicHuffmanCodes), *strategy.params, int(final),
+                                           start_bitpos, out_addr, out_cap, ctypes.byref(endbits), crcp, flags)
+            check(r, "ndfl_deflate_chunks_lz77")
+        else:
+            r = L.ndfl_deflate_chunks(self._h, hist_addr, hist_len, hist_limit, data_addr, n, chunk_len,
+                                      _strategy_id(strategy), int(final), start_bitpos, out_addr, out_cap,
+                                      ctypes.byref(endbits), crcp, flags)
+            check(r, "ndfl_deflate_chunks")
         return endbits.value, (crcv.value if crc is not None else None)
 
     def deflate(self, data, strategy=Strategy.RLE_DYNAMIC, chunk_len=65536, hist_limit=32768, with_crc=False):
@@ -136,7 +177,7 @@ class Context:
         out = ctypes.create_string_buffer(cap)
         src = ctypes.create_string_buffer(data, max(1, len(data)))
         endbits, crc = self.deflate_chunks_raw(None, 0, hist_limit, ctypes.addressof(src), len(data), chunk_len,
-                                               _strategy_id(strategy), True, 0, ctypes.addressof(out), cap, 0,
+                                               strategy, True, 0, ctypes.addressof(out), cap, 0,
                                                crc=0 if with_crc else None)
         comp = out.raw[:(endbits + 7) // 8]
         return (comp, crc) if with_crc else comp
@@ -195,6 +236,8 @@ class Context:
 
 
 def _strategy_id(s):
+    if isinstance(s, Lz77Huffman):
+        return s
     if isinstance(s, Strategy):
         return s.value
     if isinstance(s, str):

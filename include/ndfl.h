@@ -85,13 +85,28 @@ int ndfl_ctx_timings(ndfl_ctx* ctx, double* ms, int n);
  *                   begins at that bit of out[0]; bits below it are written as 0 (caller ORs)
  *   out/out_cap     output bytes; on success *out_end_bits = start_bitpos + bits written
  *   crc_inout       optional: java.util.zip.CRC32 value updated with `data` (GzipOutputStream)
- * Returns 0, NDFL_E_UNSUPPORTED (FULL_* and UNCOMPRESSED are CPU-only in the reference-parity
- * sense and not yet on the GPU path), NDFL_E_CAPACITY (*out_end_bits = bits required), ...
+ * Returns 0, NDFL_E_UNSUPPORTED (chunk_len > 65536, or UNCOMPRESSED), NDFL_E_CAPACITY
+ * (*out_end_bits = bits required), ...  FULL_STATIC / FULL_DYNAMIC run ndfl_deflate_chunks_lz77
+ * with (3, 258, 1, 32768).
  */
 int ndfl_deflate_chunks(ndfl_ctx* ctx, const uint8_t* hist, uint32_t hist_len, uint32_t hist_limit,
                         const uint8_t* data, uint64_t len, uint32_t chunk_len, int strategy,
                         int final_flag, uint32_t start_bitpos, uint8_t* out, uint64_t out_cap,
                         uint64_t* out_end_bits, uint32_t* crc_inout, uint32_t flags);
+
+/*
+ * Same as ndfl_deflate_chunks for an explicit Lz77Huffman(useDynamicHuffmanCodes,
+ * searchMinimumRunLength, searchMaximumRunLength, searchMinimumDistance, searchMaximumDistance)
+ * strategy (D/comp/Lz77Huffman.java:20-39 record + validation, :62-130 greedy longest-match parse
+ * with the smallest distance on ties).  (0,0,0,0) is the literal-only form; parameters outside
+ * 3 <= minRun <= maxRun <= 258, 1 <= minDist <= maxDist <= 32768 give NDFL_E_ARG
+ * (IllegalArgumentException, :37-38).  The FULL_* presets are (3, 258, 1, 32768).
+ */
+int ndfl_deflate_chunks_lz77(ndfl_ctx* ctx, const uint8_t* hist, uint32_t hist_len, uint32_t hist_limit,
+                             const uint8_t* data, uint64_t len, uint32_t chunk_len, int dynamic, int min_run,
+                             int max_run, int min_dist, int max_dist, int final_flag, uint32_t start_bitpos,
+                             uint8_t* out, uint64_t out_cap, uint64_t* out_end_bits, uint32_t* crc_inout,
+                             uint32_t flags);
 
 /* Upper bound of output bytes of ndfl_deflate_chunks for `len` bytes. */
 uint64_t ndfl_deflate_bound(uint64_t len, uint32_t chunk_len);
