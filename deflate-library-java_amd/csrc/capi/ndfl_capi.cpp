@@ -342,6 +342,12 @@ int ndfl_deflate_chunks_lz77(ndfl_ctx* c, const uint8_t* hist, uint32_t hist_len
     la.hist_limit = hist_limit; la.min_run = (uint32_t)min_run; la.max_run = (uint32_t)max_run;
     la.min_dist = (uint32_t)min_dist; la.max_dist = (uint32_t)max_dist;
     la.link = c->d_link.as<uint16_t>(); la.match = c->d_match.as<uint32_t>();
+    static const bool lz_stats = getenv("NDFL_LZ_STATS") != nullptr;
+    la.stats = nullptr;
+    if (lz_stats) {
+        HIPCHK(hipMalloc(&la.stats, 64));
+        HIPCHK(hipMemsetAsync(la.stats, 0, 64, s));
+    }
     LzEncArgs ea;
     ea.match = c->d_match.as<uint32_t>(); ea.n = len; ea.chunk_len = chunk_len; ea.nchunks = nch;
     ea.final_last = final_flag ? 1 : 0; ea.dynamic = dynamic ? 1 : 0; ea.base_bit = start_bitpos;
@@ -368,6 +374,15 @@ int ndfl_deflate_chunks_lz77(ndfl_ctx* c, const uint8_t* hist, uint32_t hist_len
         HIPCHK(hipGetLastError());
     }
     HIPCHK(hipEventRecord(c->ev1, s));
+    if (la.stats) {
+        unsigned long long st[4];
+        HIPCHK(hipMemcpyAsync(st, la.stats, 32, hipMemcpyDeviceToHost, s));
+        HIPCHK(hipStreamSynchronize(s));
+        hipFree(la.stats);
+        fprintf(stderr, "[ndfl] lz match: %llu searched positions, %.2f hops/pos, %.2f trigram hits/pos, %.2f compare words/pos\n",
+                st[0], (double)st[1] / std::max(1ull, st[0]), (double)st[2] / std::max(1ull, st[0]),
+                (double)st[3] / std::max(1ull, st[0]));
+    }
     const uint32_t ne = 2 * nch;
     hipLaunchKernelGGL(ndfl_edge_fixup_kernel, dim3((ne + 255) / 256), dim3(256), 0, s,
                        (const uint64_t*)ea.edge_w, (const uint32_t*)ea.edge_v, ne, d_out);

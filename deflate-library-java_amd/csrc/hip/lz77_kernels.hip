@@ -42,6 +42,7 @@ struct LzArgs {
     uint64_t L0;
     uint64_t p_begin, p_end;  // searched positions (buffer index) of this launch
     uint32_t* match;          // match[q - p_begin]
+    unsigned long long* stats;  // optional: [0] searched positions, [1] chain hops, [2] trigram hits, [3] compare words
 };
 
 }  // namespace
@@ -54,37 +55,56 @@ struct LzArgs {
 extern "C" __global__ void __launch_bounds__(64)
 ndfl_lz_links_kernel(const uint8_t* buf, uint64_t total, uint64_t vstart, uint64_t L0, uint64_t L1, uint16_t* link) {
     __shared__ __attribute__((aligned(16))) uint16_t head[1 << LZ_HBITS];
+    __shared__ __attribute__((aligned(16))) uint32_t bb[(1024 + 16) / 4];    // one 1 KiB block + lookahead
     const int lane = threadIdx.x;
     const uint64_t s0 = L0 + (uint64_t)blockIdx.x * LZ_SEG;
     const uint64_t s1 = min(s0 + LZ_SEG, L1);
     const uint64_t seed0 = max(vstart, s0 >= (uint64_t)LZ_SEG ? s0 - LZ_SEG : 0ull);
     for (int k = lane; k < (1 << LZ_HBITS) / 8; k += 64) ((u32x4*)head)[k] = u32x4{~0u, ~0u, ~0u, ~0u};
-    __syncthreads();
-    for (uint64_t q0 = seed0; q0 < s1; q0 += 64) {
-        const uint64_t q = q0 + lane;
-        const bool valid = q < s1 && q + 2 < total;
-        uint32_t h = 0x10000u + (uint32_t)lane;   // distinct non-bucket for invalid lanes
-        if (valid) h = lz_hash((uint32_t)buf[q] | (uint32_t)buf[q + 1] << 8 | (uint32_t)buf[q + 2] << 16);
-        int prevLane = -1;
-        bool last = true;
+    // bytes are staged 1 KiB at a time, the next block's loads in flight while this one is linked
+    // (the staging buffer has 64 zero bytes after `total`)
+    auto load16 = [&](uint64_t g) -> u32x4 {
+        return g + 16 <= total + 64 ? *(const u32x4*)(buf + g) : u32x4{0u, 0u, 0u, 0u};
+    };
+    const uint64_t a0 = seed0 & ~15ull;
+    u32x4 nx = load16(a0 + 16 * (uint64_t)lane);
+    u32x4 nx2 = lane == 0 ? load16(a0 + 1024) : u32x4{0u, 0u, 0u, 0u};
+    for (uint64_t q0 = a0; q0 < s1; q0 += 1024) {
+        __syncthreads();
+        ((u32x4*)bb)[lane] = nx;
+        if (lane == 0) ((u32x4*)bb)[64] = nx2;
+        __syncthreads();
+        if (q0 + 1024 < s1) {
+            nx = load16(q0 + 1024 + 16 * (uint64_t)lane);
+            if (lane == 0) nx2 = load16(q0 + 2048);
+        }
+        for (int it = 0; it < 16; it++) {
+            const uint32_t r = (uint32_t)(it * 64 + lane);
+            const uint64_t q = q0 + r;
+            const bool valid = q >= seed0 && q < s1 && q + 2 < total;
+            uint32_t h = 0x10000u + (uint32_t)lane;   // distinct non-bucket for invalid lanes
+            if (valid) h = lz_hash(__builtin_amdgcn_alignbyte(bb[(r >> 2) + 1], bb[r >> 2], r & 3) & 0xFFFFFFu);
+            int prevLane = -1;
+            bool last = true;
 #pragma unroll 8
-        for (int k = 0; k < 64; k++) {
-            const uint32_t hk = __builtin_amdgcn_readlane(h, k);
-            const bool eq = hk == h;
-            if (eq && k < lane) prevLane = k;
-            if (eq && k > lane) last = false;
-        }
-        const uint32_t off = (uint32_t)(q - seed0);   // < 65536; 0xFFFF is written only by the
-        uint32_t d = 0;                               // segment's last position and never read
-        if (valid) {
-            if (prevLane >= 0) d = (uint32_t)(lane - prevLane);
-            else {
-                const uint32_t hv = head[h];
-                if (hv != 0xFFFFu) { d = off - hv; if (d > (uint32_t)LZ_SEG) d = 0; }
+            for (int k = 0; k < 64; k++) {
+                const uint32_t hk = __builtin_amdgcn_readlane(h, k);
+                const bool eq = hk == h;
+                if (eq && k < lane) prevLane = k;
+                if (eq && k > lane) last = false;
             }
+            const uint32_t off = (uint32_t)(q - seed0);   // < 65536; 0xFFFF is written only by the
+            uint32_t d = 0;                               // segment's last position and never read
+            if (valid) {
+                if (prevLane >= 0) d = (uint32_t)(lane - prevLane);
+                else {
+                    const uint32_t hv = head[h];
+                    if (hv != 0xFFFFu) { d = off - hv; if (d > (uint32_t)LZ_SEG) d = 0; }
+                }
+            }
+            if (valid && last) head[h] = (uint16_t)off;   // one wave: LDS ops stay in program order
+            if (q >= s0 && q < s1) link[q - L0] = (uint16_t)d;
         }
-        if (valid && last) head[h] = (uint16_t)off;   // one wave: LDS ops stay in program order
-        if (q >= s0 && q < s1) link[q - L0] = (uint16_t)d;
     }
 }
 
@@ -102,7 +122,9 @@ extern "C" __global__ void __launch_bounds__(1024)
 ndfl_lz_match_kernel(LzArgs a) {
     __shared__ __attribute__((aligned(16))) uint32_t wb[LZ_WWORDS + 4];
     __shared__ __attribute__((aligned(16))) uint16_t lk[LZ_WIN + LZ_TILE];
+    __shared__ uint32_t s_next;
     const int tid = threadIdx.x;
+    if (tid == 0) s_next = 1024;
     const uint64_t p0 = a.p_begin + (uint64_t)blockIdx.x * LZ_TILE;
     const uint64_t p1 = min(p0 + LZ_TILE, a.p_end);
     const int64_t wb0 = (int64_t)p0 - LZ_WIN;         // window base (buffer index); p0 >= LZ_DS
@@ -121,30 +143,52 @@ ndfl_lz_match_kernel(LzArgs a) {
     }
     __syncthreads();
     const uint32_t minRun = a.min_run, maxRun = a.max_run;
-    for (uint64_t i = p0 + tid; i < p1; i += 1024) {
-        const uint64_t x = i - LZ_DS;                  // data index
-        const uint64_t c = x / a.chunk_len;
-        const uint64_t cs = LZ_DS + c * a.chunk_len;
-        const uint64_t e = min(cs + a.chunk_len, a.total);
-        const uint32_t maxlen = (uint32_t)min((uint64_t)maxRun, e - i);
-        const uint64_t avail = cs - a.vstart;           // history bytes before the chunk
-        const uint64_t off = cs - min((uint64_t)a.hist_limit, avail);
-        const int64_t lo = max((int64_t)i - (int64_t)a.max_dist, (int64_t)off);
-        const int64_t hi = (int64_t)i - (int64_t)a.min_dist;
-        const uint32_t ri = (uint32_t)((int64_t)i - wb0);
-        uint32_t best = 0, bestd = 0;
-        if (maxlen >= minRun && hi >= lo) {
-            const uint32_t wi0 = lz_word(wb, ri);
-            const uint32_t rlo = (uint32_t)(lo - wb0), rhi = (uint32_t)(hi - wb0);
-            uint32_t rj = ri;
-            for (;;) {
-                const uint32_t d = lk[rj];
-                if (d == 0 || d > rj - rlo) break;     // chain ends, or next candidate below lo
-                rj -= d;
-                if (rj > rhi) continue;
-                const uint32_t x0 = lz_word(wb, rj) ^ wi0;
-                if (x0 & 0xFFFFFFu) continue;           // run < 3: can never be chosen
-                if (best >= 3 && lz_byte(wb, rj + best) != lz_byte(wb, ri + best)) continue;   // not longer
+    uint32_t st_pos = 0, st_hop = 0, st_hit = 0, st_cmp = 0;
+    // Each lane searches positions one hop per iteration and takes the tile's next unclaimed position
+    // (LDS counter) as soon as it finishes one: chain lengths vary by orders of magnitude, so static
+    // assignment would leave the tile waiting on its unluckiest lanes.  The next link is read
+    // together with the candidate.
+    uint64_t i = p0 + tid;
+    bool have = false;
+    uint32_t ri = 0, rlo = 0, rhi = 0, maxlen = 0, wi0 = 0, best = 0, bestd = 0, rj = 0, d = 0, want = 0;
+    for (;;) {
+        if (!have) {
+            while (i < p1) {
+                const uint64_t x = i - LZ_DS;                  // data index
+                const uint64_t c = x / a.chunk_len;
+                const uint64_t cs = LZ_DS + c * a.chunk_len;
+                const uint64_t e = min(cs + a.chunk_len, a.total);
+                maxlen = (uint32_t)min((uint64_t)maxRun, e - i);
+                const uint64_t avail = cs - a.vstart;           // history bytes before the chunk
+                const uint64_t off = cs - min((uint64_t)a.hist_limit, avail);
+                const int64_t lo = max((int64_t)i - (int64_t)a.max_dist, (int64_t)off);
+                const int64_t hi = (int64_t)i - (int64_t)a.min_dist;
+                ri = (uint32_t)((int64_t)i - wb0);
+                if (maxlen >= minRun && hi >= lo) {
+                    st_pos++;
+                    wi0 = lz_word(wb, ri);
+                    rlo = (uint32_t)(lo - wb0);
+                    rhi = (uint32_t)(hi - wb0);
+                    rj = ri; d = lk[ri];
+                    best = 0; bestd = 0; want = 0;
+                    have = true;
+                    break;
+                }
+                a.match[i - a.p_begin] = lz_byte(wb, ri);
+                i = p0 + atomicAdd(&s_next, 1u);
+            }
+            if (!have) break;
+        }
+        // one hop
+        bool fin = d == 0 || d > rj - rlo;                      // chain ends, or next candidate below lo
+        if (!fin) {
+            rj -= d;
+            st_hop++;
+            d = lk[rj];
+            const uint32_t x0 = lz_word(wb, rj) ^ wi0;
+            const uint32_t sb = lz_byte(wb, rj + best);
+            if (rj <= rhi && (x0 & 0xFFFFFFu) == 0 && (best < 3 || sb == want)) {   // can be longer
+                st_hit++;
                 uint32_t run;
                 if (x0) run = 3;
                 else {
@@ -152,6 +196,7 @@ ndfl_lz_match_kernel(LzArgs a) {
                     for (;;) {
                         if (k >= maxlen) { run = maxlen; break; }
                         const uint32_t y = lz_word(wb, rj + k) ^ lz_word(wb, ri + k);
+                        st_cmp++;
                         if (y) { run = k + (__builtin_ctz(y) >> 3); break; }
                         k += 4;
                     }
@@ -160,11 +205,20 @@ ndfl_lz_match_kernel(LzArgs a) {
                 if (run > best) {
                     best = run;
                     bestd = ri - rj;
-                    if (best >= maxlen) break;
+                    fin = best >= maxlen;
+                    if (!fin) want = lz_byte(wb, ri + best);
                 }
             }
         }
-        a.match[i - a.p_begin] = best >= minRun ? (best << 16 | (bestd - 1)) : lz_byte(wb, ri);
+        if (fin) {
+            a.match[i - a.p_begin] = best >= minRun ? (best << 16 | (bestd - 1)) : lz_byte(wb, ri);
+            have = false;
+            i = p0 + atomicAdd(&s_next, 1u);
+        }
+    }
+    if (a.stats) {
+        atomicAdd(&a.stats[0], (unsigned long long)st_pos); atomicAdd(&a.stats[1], (unsigned long long)st_hop);
+        atomicAdd(&a.stats[2], (unsigned long long)st_hit); atomicAdd(&a.stats[3], (unsigned long long)st_cmp);
     }
 }
 
