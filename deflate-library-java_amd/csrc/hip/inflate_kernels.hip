@@ -692,22 +692,26 @@ static int resolve_rounds(InflateScratch& S, hipStream_t s, uint8_t* d_out, uint
     int cur = 0;
     uint32_t n = 0;
     for (int round = 0;; round++) {
-        if ((round & 3) == 0) {
+        static const bool rstats = getenv("NDFL_STATS") != nullptr;
+        if ((round & 3) == 0 || rstats) {
             INF_CHK(hipMemcpyAsync(h, cnt + cur, 4, hipMemcpyDeviceToHost, s));
+            if (rstats) INF_CHK(hipMemcpyAsync(h + 1, cnt + 2 + cur, 4, hipMemcpyDeviceToHost, s));
             INF_CHK(hipStreamSynchronize(s));
             n = *h;
+            if (rstats) fprintf(stderr, "[ndfl] resolve round %d: %u pending groups, %u bytes\n", round, n, h[1]);
             if (round == 0) *groups = n;
             if (n == 0) return 0;
             if (round >= 48) return R_INTERNAL;              // distances double each round: unreachable
         }
         INF_CHK(hipMemsetAsync(cnt + (cur ^ 1), 0, 4, s));
+        if (rstats) INF_CHK(hipMemsetAsync(cnt + 2 + (cur ^ 1), 0, 4, s));
         const uint32_t gb = (uint32_t)std::min<uint64_t>(4096, ((uint64_t)n * 32 + 255) / 256);
         hipLaunchKernelGGL(ndfl_inflate_resolve_kernel, dim3(gb), dim3(256), 0, s,
                            (const uint32_t*)lst[cur], (const uint32_t*)(cnt + cur), (const uint32_t*)pend, ref, d_out, nb);
         INF_CHK(hipGetLastError());
         hipLaunchKernelGGL(ndfl_inflate_resolve_apply_kernel, dim3((uint32_t)std::min<uint64_t>(1024, (n + 255) / 256)),
                            dim3(256), 0, s, (const uint32_t*)lst[cur], (const uint32_t*)(cnt + cur), pend,
-                           (const uint32_t*)nb, lst[cur ^ 1], cnt + (cur ^ 1));
+                           (const uint32_t*)nb, lst[cur ^ 1], cnt + (cur ^ 1), rstats ? cnt + 2 + (cur ^ 1) : (uint32_t*)nullptr);
         INF_CHK(hipGetLastError());
         cur ^= 1;
     }

@@ -993,7 +993,7 @@ ndfl_inflate_count_wave_kernel(const uint32_t* w, uint64_t nwords, uint64_t nbit
 
 // Emit pass: persistent waves claiming the linked chains through `ticket`.  No lane and no chain
 // ever waits on another: a copy whose source lies before the lane's own output (an earlier lane,
-// an earlier chain, the window), or reaches the lane's first deferred byte, is not executed but
+// an earlier chain, the window), or covers one of the lane's own deferred bytes, is not executed but
 // deferred -- its bytes get a back-reference (ref[i] = distance to a byte holding the same value)
 // and a pending bit, and ndfl_inflate_resolve_kernel rounds resolve them afterwards by pointer
 // jumping.  So every chain decodes in parallel whatever the LZ77 distances.
@@ -1103,7 +1103,18 @@ ndfl_inflate_emit_wave_kernel(const uint32_t* w, uint64_t nwords, uint64_t nbits
                 const uint64_t dst = L.dst0 + L.n;
                 const uint64_t src = dst - dist;
                 const uint64_t src_end = src + min(len, dist);          // the copy's bytes before dst
-                if (src >= L.dst0 && src_end <= dfr) {
+                bool defer = src < L.dst0;
+                if (!defer && src_end > dfr) {
+                    // a source at or past our first deferred byte: pending only if its bit is set
+                    // (bits of our own range are set by this lane alone, atomically, so an agent-
+                    // scope load sees them)
+                    for (uint64_t q = src >> 5; q <= (src_end - 1) >> 5 && !defer; q++) {
+                        const uint64_t lo = max(src, q << 5), hi = min(src_end, (q + 1) << 5);
+                        const uint32_t m = (uint32_t)(((1ull << (hi - lo)) - 1) << (lo & 31));
+                        defer = (__hip_atomic_load(&pend[q], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) & m) != 0;
+                    }
+                }
+                if (!defer) {
                     wcopy(L, gout, dst, src, len, dist);                // sources final and our own
                     lastsrc = dst + len - 1;
                 } else {
@@ -1187,23 +1198,38 @@ ndfl_inflate_resolve_kernel(const uint32_t* list, const uint32_t* nlist, const u
 
 // Apply a round's bits and compact the list of still-pending groups (grid-stride: the grid is sized
 // before the list size is known).
+// Block-wide append of the flagged lanes' values to list[*n ...] (one global atomic per block).
+__device__ __forceinline__ void block_append(bool flag, uint32_t v, uint32_t* list, uint32_t* n) {
+    __shared__ uint32_t wc[4], wbase;
+    const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
+    const uint64_t m = __ballot(flag);
+    if (lane == 0) wc[wid] = (uint32_t)__popcll(m);
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        const uint32_t t = wc[0] + wc[1] + wc[2] + wc[3];
+        wbase = t ? atomicAdd(n, t) : 0u;
+    }
+    __syncthreads();
+    uint32_t off = wbase;
+    for (int k = 0; k < wid; k++) off += wc[k];
+    if (flag) list[off + __popcll(m & ((1ull << lane) - 1))] = v;
+    __syncthreads();
+}
+
 extern "C" __global__ void __launch_bounds__(256)
 ndfl_inflate_resolve_apply_kernel(const uint32_t* list, const uint32_t* nlist, uint32_t* pend, const uint32_t* newbits,
-                                  uint32_t* list_out, uint32_t* nlist_out) {
+                                  uint32_t* list_out, uint32_t* nlist_out, uint32_t* nbytes_out) {
     const uint32_t n = *nlist;
     for (uint32_t k0 = blockIdx.x * 256; k0 < n; k0 += gridDim.x * 256) {
         const uint32_t k = k0 + threadIdx.x;
         const bool live = k < n;
         uint32_t nb = 0, wd = 0;
         if (live) { wd = list[k]; nb = newbits[k]; pend[wd] = nb; }
-        const uint64_t m = __ballot(live && nb != 0);
-        if (m) {
-            const int lane = threadIdx.x & 63;
-            uint32_t base = 0;
-            if (lane == 0) base = atomicAdd(nlist_out, (uint32_t)__popcll(m));
-            base = __shfl(base, 0, 64);
-            if (live && nb) list_out[base + __popcll(m & ((1ull << lane) - 1))] = wd;
+        if (nbytes_out) {
+            const uint32_t c = wave_sum((uint32_t)__popc(nb));
+            if ((threadIdx.x & 63) == 0 && c) atomicAdd(nbytes_out, c);
         }
+        block_append(live && nb != 0, wd, list_out, nlist_out);
     }
 }
 
@@ -1211,13 +1237,5 @@ ndfl_inflate_resolve_apply_kernel(const uint32_t* list, const uint32_t* nlist, u
 extern "C" __global__ void __launch_bounds__(256)
 ndfl_inflate_pending_list_kernel(const uint32_t* pend, uint64_t w0, uint64_t w1, uint32_t* list, uint32_t* nlist) {
     const uint64_t wd = w0 + (uint64_t)blockIdx.x * 256 + threadIdx.x;
-    const bool nz = wd < w1 && pend[wd] != 0;
-    const uint64_t m = __ballot(nz);
-    if (m) {
-        const int lane = threadIdx.x & 63;
-        uint32_t base = 0;
-        if (lane == 0) base = atomicAdd(nlist, (uint32_t)__popcll(m));
-        base = __shfl(base, 0, 64);
-        if (nz) list[base + __popcll(m & ((1ull << lane) - 1))] = (uint32_t)wd;
-    }
+    block_append(wd < w1 && pend[wd] != 0, (uint32_t)wd, list, nlist);
 }
