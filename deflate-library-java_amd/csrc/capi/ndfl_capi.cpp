@@ -3,6 +3,7 @@
 #include "../../../include/ndfl.h"
 #include "../hip/deflate_kernels.hip"
 #include "../hip/lz77_kernels.hip"
+#include "../hip/strategy_kernels.hip"
 #include "../hip/inflate_kernels.hip"
 
 #include <hip/hip_runtime.h>
@@ -61,6 +62,8 @@ struct ndfl_ctx {
     double deflate_ms = 0;
     DevBuf d_in, d_out, d_status, d_ticket, d_edge_w, d_edge_v, d_crc, d_crc1, d_tabs, d_hostio;
     DevBuf d_lz, d_link, d_match;   // LZ77 path: staging [pad|hist|data], hash links, per-position matches
+    DevBuf d_mdata, d_mstreams[8], d_mbits[8], d_masm;   // strategy composition
+    uint64_t* cb_out = nullptr;     // internal: when set, encoders also write per-chunk block bits here
     InflateScratch inf;
     uint32_t* h_pinned = nullptr;   // small pinned area for results
 };
@@ -120,8 +123,10 @@ int ndfl_ctx_destroy(ndfl_ctx* c) {
     hipSetDevice(c->device);
     hipStreamSynchronize(c->stream);
     DevBuf* bufs[] = {&c->d_in, &c->d_out, &c->d_status, &c->d_ticket, &c->d_edge_w, &c->d_edge_v,
-                      &c->d_crc, &c->d_crc1, &c->d_tabs, &c->d_hostio, &c->d_lz, &c->d_link, &c->d_match};
+                      &c->d_crc, &c->d_crc1, &c->d_tabs, &c->d_hostio, &c->d_lz, &c->d_link, &c->d_match,
+                      &c->d_mdata, &c->d_masm};
     for (DevBuf* b : bufs) b->release();
+    for (int k = 0; k < 8; k++) { c->d_mstreams[k].release(); c->d_mbits[k].release(); }
     c->inf.release();
     if (c->h_pinned) hipHostFree(c->h_pinned);
     if (c->ev0) hipEventDestroy(c->ev0);
@@ -175,7 +180,11 @@ int ndfl_deflate_chunks(ndfl_ctx* c, const uint8_t* hist, uint32_t hist_len, uin
             return ndfl_deflate_chunks_lz77(c, hist, hist_len, hist_limit, data, len, chunk_len,
                                             strategy == NDFL_FULL_DYNAMIC, 3, 258, 1, 32768, final_flag,
                                             start_bitpos, out, out_cap, out_end_bits, crc_inout, flags);
-        case NDFL_UNCOMPRESSED: return NDFL_E_UNSUPPORTED;
+        case NDFL_UNCOMPRESSED: {
+            ndfl_strategy_desc u = {NDFL_KIND_UNCOMPRESSED, 0, 0, 0, 0, 0};
+            return ndfl_deflate_chunks_multi(c, hist, hist_len, hist_limit, data, len, chunk_len, &u, 1, final_flag,
+                                             start_bitpos, out, out_cap, out_end_bits, crc_inout, flags);
+        }
         default: return NDFL_E_ARG;
     }
     if (chunk_len > (uint32_t)MAX_CHUNK) return NDFL_E_UNSUPPORTED;
@@ -224,7 +233,7 @@ int ndfl_deflate_chunks(ndfl_ctx* c, const uint8_t* hist, uint32_t hist_len, uin
     a.rle = rle; a.dynamic = dyn; a.base_bit = start_bitpos;
     a.out = d_out; a.status = c->d_status.as<uint64_t>(); a.ticket = c->d_ticket.as<uint32_t>();
     a.edge_w = c->d_edge_w.as<uint64_t>(); a.edge_v = c->d_edge_v.as<uint32_t>();
-    a.chunk_bits = nullptr;
+    a.chunk_bits = c->cb_out;
     a.crc_raw = crc_inout ? c->d_crc.as<uint32_t>() : nullptr;
     a.crc_tab = c->d_tabs.as<uint32_t>();
     a.crc_x = c->d_tabs.as<uint32_t>() + 1024;
@@ -353,6 +362,7 @@ int ndfl_deflate_chunks_lz77(ndfl_ctx* c, const uint8_t* hist, uint32_t hist_len
     ea.final_last = final_flag ? 1 : 0; ea.dynamic = dynamic ? 1 : 0; ea.base_bit = start_bitpos;
     ea.out = d_out; ea.status = c->d_status.as<uint64_t>(); ea.ticket = c->d_ticket.as<uint32_t>();
     ea.edge_w = c->d_edge_w.as<uint64_t>(); ea.edge_v = c->d_edge_v.as<uint32_t>();
+    ea.chunk_bits = c->cb_out;
 
     HIPCHK(hipEventRecord(c->ev0, s));
     for (uint32_t cb = 0; cb < nch; cb += batch_ch) {
@@ -405,6 +415,143 @@ int ndfl_deflate_chunks_lz77(ndfl_ctx* c, const uint8_t* hist, uint32_t hist_len
         *crc_inout = cr;
         c->last_ms = ms;
     }
+    if (!direct) {
+        if (nbytes > out_cap) return NDFL_E_CAPACITY;
+        HIPCHK(hipMemcpyAsync(out, d_out, nbytes,
+                              (flags & NDFL_OUT_DEVICE) ? hipMemcpyDeviceToDevice : hipMemcpyDeviceToHost, s));
+        HIPCHK(hipStreamSynchronize(s));
+    }
+    return NDFL_OK;
+}
+
+// MultiStrategy over Lz77Huffman / Uncompressed substrategies (D/comp/MultiStrategy.java:31-57,
+// D/comp/Uncompressed.java:19-51): every Lz77Huffman substrategy encodes all chunks into its own
+// stream; the host walks the chunks with the bit position mod 8 and keeps, per chunk, the first
+// substrategy with the fewest bits at that position; ndfl_assemble_kernel writes the result.
+int ndfl_deflate_chunks_multi(ndfl_ctx* c, const uint8_t* hist, uint32_t hist_len, uint32_t hist_limit,
+                              const uint8_t* data, uint64_t len, uint32_t chunk_len, const ndfl_strategy_desc* strats,
+                              uint32_t n_strats, int final_flag, uint32_t start_bitpos, uint8_t* out, uint64_t out_cap,
+                              uint64_t* out_end_bits, uint32_t* crc_inout, uint32_t flags) {
+    if (!c || !out_end_bits || (!data && len) || (!hist && hist_len) || !out || !strats) return NDFL_E_ARG;
+    if (n_strats == 0 || n_strats > 8) return n_strats == 0 ? NDFL_E_ARG : NDFL_E_UNSUPPORTED;
+    if (start_bitpos > 7 || hist_limit > 32768 || hist_len > hist_limit || chunk_len == 0) return NDFL_E_ARG;
+    if (!final_flag && (len == 0 || len % chunk_len != 0)) return NDFL_E_ARG;
+    if (chunk_len > (uint32_t)MAX_CHUNK) return NDFL_E_UNSUPPORTED;
+    for (uint32_t k = 0; k < n_strats; k++) {
+        const ndfl_strategy_desc& d = strats[k];
+        if (d.kind == NDFL_KIND_UNCOMPRESSED) continue;
+        if (d.kind != NDFL_KIND_LZ77) return NDFL_E_ARG;
+        const bool lit = d.min_run == 0 && d.max_run == 0 && d.min_dist == 0 && d.max_dist == 0;
+        if (!lit && !(3 <= d.min_run && d.min_run <= d.max_run && d.max_run <= 258 && 1 <= d.min_dist &&
+                      d.min_dist <= d.max_dist && d.max_dist <= 32768))
+            return NDFL_E_ARG;
+    }
+    HIPCHK(hipSetDevice(c->device));
+    hipStream_t s = c->stream;
+    const uint64_t nch64 = final_flag ? (len == 0 ? 1 : (len + chunk_len - 1) / chunk_len) : len / chunk_len;
+    if (nch64 > 0xFFFFFFFFull) return NDFL_E_UNSUPPORTED;
+    const uint32_t nch = (uint32_t)nch64;
+    // device copies of the inputs (the substrategy calls below take device pointers)
+    const uint8_t* d_data = data;
+    const uint8_t* d_hist = hist;
+    if (!(flags & NDFL_IN_DEVICE)) {
+        HIPCHK(c->d_mdata.ensure(len + hist_len + 16));
+        if (hist_len) HIPCHK(hipMemcpyAsync(c->d_mdata.p, hist, hist_len, hipMemcpyHostToDevice, s));
+        if (len) HIPCHK(hipMemcpyAsync(c->d_mdata.as<uint8_t>() + hist_len, data, len, hipMemcpyHostToDevice, s));
+        d_hist = c->d_mdata.as<uint8_t>();
+        d_data = d_hist + hist_len;
+    }
+    const uint64_t bound = ndfl_deflate_bound(len, chunk_len);
+    const uint64_t bound_words = (bound + 3) / 4 + 2;
+    std::vector<std::vector<uint64_t>> bits(n_strats);
+    std::vector<const uint32_t*> streams(n_strats, nullptr);
+    for (uint32_t k = 0; k < n_strats; k++) {
+        const ndfl_strategy_desc& d = strats[k];
+        if (d.kind == NDFL_KIND_UNCOMPRESSED) continue;
+        HIPCHK(c->d_mstreams[k].ensure(bound_words * 4 + 64));
+        HIPCHK(c->d_mbits[k].ensure(nch * 8ull));
+        c->cb_out = c->d_mbits[k].as<uint64_t>();
+        uint64_t eb = 0;
+        const int rc = ndfl_deflate_chunks_lz77(c, d_hist, hist_len, hist_limit, d_data, len, chunk_len, d.dynamic,
+                                                d.min_run, d.max_run, d.min_dist, d.max_dist, final_flag, 0,
+                                                c->d_mstreams[k].as<uint8_t>(), bound_words * 4 + 64, &eb, nullptr,
+                                                NDFL_IN_DEVICE | NDFL_OUT_DEVICE);
+        c->cb_out = nullptr;
+        if (rc) return rc;
+        bits[k].resize(nch);
+        HIPCHK(hipMemcpyAsync(bits[k].data(), c->d_mbits[k].p, nch * 8ull, hipMemcpyDeviceToHost, s));
+        streams[k] = c->d_mstreams[k].as<uint32_t>();
+    }
+    HIPCHK(hipStreamSynchronize(s));
+    // choose (D/comp/MultiStrategy.java:35-44: strictly fewer bits wins, so ties keep the earlier one)
+    std::vector<uint8_t> choice(nch);
+    std::vector<uint64_t> src_bit(nch), dst_bit(nch), nb(nch), soff(n_strats, 0);
+    uint64_t pos = start_bitpos;
+    for (uint32_t ci = 0; ci < nch; ci++) {
+        const uint64_t cl = std::min<uint64_t>(chunk_len, len - (uint64_t)ci * chunk_len);
+        const uint32_t p8 = (uint32_t)(pos & 7);
+        uint64_t best = UINT64_MAX;
+        uint32_t bk = 0;
+        for (uint32_t k = 0; k < n_strats; k++) {
+            uint64_t b;
+            if (strats[k].kind == NDFL_KIND_UNCOMPRESSED) {
+                const uint64_t nblk = std::max<uint64_t>((cl + 65534) / 65535, 1);   // (:23-25)
+                b = cl * 8 + nblk * 40 + (uint64_t)((int)((13 - p8) % 8) - 5);
+            } else {
+                b = bits[k][ci];
+            }
+            if (b < best) { best = b; bk = k; }
+        }
+        choice[ci] = (uint8_t)bk;
+        dst_bit[ci] = pos;
+        nb[ci] = best;
+        for (uint32_t k = 0; k < n_strats; k++)
+            if (strats[k].kind != NDFL_KIND_UNCOMPRESSED) {
+                if (k == bk) src_bit[ci] = soff[k];
+                soff[k] += bits[k][ci];
+            }
+        pos += best;
+    }
+    const uint64_t end_bits = pos;
+    const uint64_t need_words = (end_bits + 31) / 32 + 2;
+    uint32_t* d_out;
+    const bool direct = (flags & NDFL_OUT_DEVICE) && (((uintptr_t)out & 3) == 0) && out_cap >= need_words * 4;
+    if (direct) d_out = (uint32_t*)out;
+    else { HIPCHK(c->d_out.ensure(need_words * 4)); d_out = c->d_out.as<uint32_t>(); }
+    HIPCHK(hipMemsetAsync(d_out, 0, need_words * 4, s));
+    // per-chunk tables + stream pointers in one device block
+    const size_t tb = nch * (3 * 8ull) + nch + 8 * n_strats + 64;
+    HIPCHK(c->d_masm.ensure(tb));
+    char* base = (char*)c->d_masm.p;
+    uint64_t* d_src = (uint64_t*)base;
+    uint64_t* d_dst = d_src + nch;
+    uint64_t* d_nb = d_dst + nch;
+    const uint32_t** d_streams = (const uint32_t**)(d_nb + nch);
+    uint8_t* d_choice = (uint8_t*)(d_streams + n_strats);
+    std::vector<char> host(tb);
+    memcpy(host.data(), src_bit.data(), nch * 8ull);
+    memcpy(host.data() + nch * 8ull, dst_bit.data(), nch * 8ull);
+    memcpy(host.data() + nch * 16ull, nb.data(), nch * 8ull);
+    memcpy(host.data() + nch * 24ull, streams.data(), 8ull * n_strats);
+    memcpy(host.data() + nch * 24ull + 8ull * n_strats, choice.data(), nch);
+    HIPCHK(hipMemcpyAsync(base, host.data(), tb, hipMemcpyHostToDevice, s));
+    AsmArgs aa;
+    aa.streams = d_streams; aa.data = d_data; aa.n = len; aa.chunk_len = chunk_len; aa.nchunks = nch;
+    aa.final_last = final_flag ? 1 : 0; aa.choice = d_choice; aa.src_bit = d_src; aa.dst_bit = d_dst; aa.nbits = d_nb;
+    aa.out = d_out;
+    HIPCHK(hipEventRecord(c->ev0, s));
+    hipLaunchKernelGGL(ndfl_assemble_kernel, dim3(nch), dim3(256), 0, s, aa);
+    HIPCHK(hipGetLastError());
+    HIPCHK(hipEventRecord(c->ev1, s));
+    HIPCHK(hipStreamSynchronize(s));
+    *out_end_bits = end_bits;
+    if (crc_inout && len) {
+        uint32_t cr = *crc_inout;
+        const int rc = ndfl_crc32(c, &cr, d_data, len, NDFL_IN_DEVICE);
+        if (rc) return rc;
+        *crc_inout = cr;
+    }
+    const uint64_t nbytes = (end_bits + 7) / 8;
     if (!direct) {
         if (nbytes > out_cap) return NDFL_E_CAPACITY;
         HIPCHK(hipMemcpyAsync(out, d_out, nbytes,

@@ -240,6 +240,7 @@ struct LzEncArgs {
     uint32_t* ticket;
     uint64_t* edge_w;
     uint32_t* edge_v;
+    uint64_t* chunk_bits;     // optional [nchunks]: block bits
 };
 
 // Length symbol / extra of a run (D/comp/Lz77Huffman.java:92-111) and distance symbol / extra of
@@ -355,6 +356,7 @@ ndfl_lz_encode_kernel(LzEncArgs a) {
     if (tid == 0) {
         if (c == 0) st_agent(&a.status[0], ST_PRE | (a.base_bit + S));
         else st_agent(&a.status[c], ST_AGG | S);
+        if (a.chunk_bits) a.chunk_bits[c] = S;
     }
     const uint32_t nwl = (uint32_t)((S + 31) >> 5) + 1;
     __syncthreads();

@@ -19,7 +19,7 @@ import io
 from . import _lib
 from ._lib import IN_DEVICE, OUT_DEVICE, DICT_DEFERRED, NO_END, STRATEGIES, NdflError, check, load, reason_name
 
-__all__ = ["Context", "Reason", "DataFormatException", "Lz77Huffman", "DeflaterOutputStream", "InflaterInputStream",
+__all__ = ["Context", "Reason", "DataFormatException", "Lz77Huffman", "Uncompressed", "MultiStrategy", "DeflaterOutputStream", "InflaterInputStream",
            "GzipMetadata", "GzipOutputStream", "GzipInputStream", "ZlibMetadata", "ZlibOutputStream",
            "ZlibInputStream", "Strategy", "default_context", "compress", "decompress", "crc32_combine"]
 
@@ -104,6 +104,44 @@ Lz77Huffman.FULL_STATIC = Lz77Huffman(False, 3, 258, 1, 32768)
 Lz77Huffman.FULL_DYNAMIC = Lz77Huffman(True, 3, 258, 1, 32768)
 
 
+class _UncompressedType:
+    """Uncompressed.SINGLETON (D/comp/Uncompressed.java:14-54): stored blocks of <= 65535 bytes."""
+
+    def __repr__(self):
+        return "Uncompressed.SINGLETON"
+
+
+class Uncompressed:
+    SINGLETON = _UncompressedType()
+
+
+class MultiStrategy:
+    """MultiStrategy(strats...) (D/comp/MultiStrategy.java:19-57): per chunk and output bit position,
+    the first substrategy giving the fewest bits.  Substrategies: Lz77Huffman or Uncompressed
+    (at most 8 on the GPU path)."""
+
+    def __init__(self, *strats):
+        if strats is None or any(s is None for s in strats):
+            raise TypeError("strategy")
+        if len(strats) == 0:
+            raise ValueError("Empty list of strategies")
+        for st in strats:
+            if not isinstance(st, (Lz77Huffman, _UncompressedType)):
+                raise TypeError(f"unsupported substrategy {st!r}")
+        self.substrategies = tuple(strats)
+
+
+def _desc(st):
+    d = _lib.StrategyDesc()
+    if isinstance(st, _UncompressedType):
+        d.kind = _lib.KIND_UNCOMPRESSED
+    else:
+        d.kind = _lib.KIND_LZ77
+        d.dynamic = int(st.useDynamicHuffmanCodes)
+        d.min_run, d.max_run, d.min_dist, d.max_dist = st.params
+    return d
+
+
 def _ptr(obj):
     """(address, keepalive) of bytes-like / torch tensor."""
     if hasattr(obj, "data_ptr"):
@@ -157,7 +195,14 @@ class Context:
         endbits = ctypes.c_uint64(0)
         crcv = ctypes.c_uint32(crc if crc is not None else 0)
         crcp = ctypes.byref(crcv) if crc is not None else None
-        if isinstance(strategy, Lz77Huffman):
+        if isinstance(strategy, (MultiStrategy, _UncompressedType)):
+            subs = strategy.substrategies if isinstance(strategy, MultiStrategy) else (strategy,)
+            arr = (_lib.StrategyDesc * len(subs))(*[_desc(x) for x in subs])
+            r = L.ndfl_deflate_chunks_multi(self._h, hist_addr, hist_len, hist_limit, data_addr, n, chunk_len, arr,
+                                            len(subs), int(final), start_bitpos, out_addr, out_cap,
+                                            ctypes.byref(endbits), crcp, flags)
+            check(r, "ndfl_deflate_chunks_multi")
+        elif isinstance(strategy, Lz77Huffman):
             r = L.ndfl_deflate_chunks_lz77(self._h, hist_addr, hist_len, hist_limit, data_addr, n, chunk_len,
                                            int(strategy.useDynamicHuffmanCodes), *strategy.params, int(final),
                                            start_bitpos, out_addr, out_cap, ctypes.byref(endbits), crcp, flags)
@@ -236,7 +281,7 @@ class Context:
 
 
 def _strategy_id(s):
-    if isinstance(s, Lz77Huffman):
+    if isinstance(s, (Lz77Huffman, MultiStrategy, _UncompressedType)):
         return s
     if isinstance(s, Strategy):
         return s.value

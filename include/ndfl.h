@@ -85,7 +85,7 @@ int ndfl_ctx_timings(ndfl_ctx* ctx, double* ms, int n);
  *                   begins at that bit of out[0]; bits below it are written as 0 (caller ORs)
  *   out/out_cap     output bytes; on success *out_end_bits = start_bitpos + bits written
  *   crc_inout       optional: java.util.zip.CRC32 value updated with `data` (GzipOutputStream)
- * Returns 0, NDFL_E_UNSUPPORTED (chunk_len > 65536, or UNCOMPRESSED), NDFL_E_CAPACITY
+ * Returns 0, NDFL_E_UNSUPPORTED (chunk_len > 65536), NDFL_E_CAPACITY
  * (*out_end_bits = bits required), ...  FULL_STATIC / FULL_DYNAMIC run ndfl_deflate_chunks_lz77
  * with (3, 258, 1, 32768).
  */
@@ -107,6 +107,27 @@ int ndfl_deflate_chunks_lz77(ndfl_ctx* ctx, const uint8_t* hist, uint32_t hist_l
                              int max_run, int min_dist, int max_dist, int final_flag, uint32_t start_bitpos,
                              uint8_t* out, uint64_t out_cap, uint64_t* out_end_bits, uint32_t* crc_inout,
                              uint32_t flags);
+
+/* A substrategy of ndfl_deflate_chunks_multi: an Lz77Huffman record or Uncompressed.SINGLETON. */
+#define NDFL_KIND_LZ77          0
+#define NDFL_KIND_UNCOMPRESSED  1
+typedef struct {
+    int32_t kind;                                     /* NDFL_KIND_* */
+    int32_t dynamic, min_run, max_run, min_dist, max_dist;   /* Lz77Huffman components (kind LZ77) */
+} ndfl_strategy_desc;
+
+/*
+ * Same as ndfl_deflate_chunks for a MultiStrategy(strats...) (D/comp/MultiStrategy.java:31-57)
+ * over up to 8 Lz77Huffman / Uncompressed substrategies (n_strats = 1 gives that strategy alone):
+ * per chunk, the first substrategy with the fewest bits at the current output bit position
+ * (Decision.getBitLengths, D/comp/Decision.java:16-19; Uncompressed's depend on the position,
+ * D/comp/Uncompressed.java:22-26).  NDFL_UNCOMPRESSED in ndfl_deflate_chunks runs this with the
+ * single Uncompressed substrategy.
+ */
+int ndfl_deflate_chunks_multi(ndfl_ctx* ctx, const uint8_t* hist, uint32_t hist_len, uint32_t hist_limit,
+                              const uint8_t* data, uint64_t len, uint32_t chunk_len, const ndfl_strategy_desc* strats,
+                              uint32_t n_strats, int final_flag, uint32_t start_bitpos, uint8_t* out,
+                              uint64_t out_cap, uint64_t* out_end_bits, uint32_t* crc_inout, uint32_t flags);
 
 /* Upper bound of output bytes of ndfl_deflate_chunks for `len` bytes. */
 uint64_t ndfl_deflate_bound(uint64_t len, uint32_t chunk_len);

@@ -496,6 +496,59 @@ int64_t or_deflate_mixed(const uint8_t* data, uint64_t len, uint32_t chunk_len, 
     return (int64_t)w.n;
 }
 
+/* MultiStrategy(subs...).decide/compressTo (D/comp/MultiStrategy.java:31-57) over Lz77Huffman /
+ * Uncompressed substrategies, driven like DeflaterOutputStream (D/DeflaterOutputStream.java:119-137).
+ * desc: n x {kind (0 Lz77Huffman, 1 Uncompressed), dynamic, minRun, maxRun, minDist, maxDist}. */
+int64_t or_deflate_multi(const uint8_t* data, uint64_t len, uint32_t chunk_len, uint32_t hist_limit,
+                         const int32_t* desc, uint32_t n, uint8_t* out, uint64_t out_cap) {
+    if (chunk_len < 1 || hist_limit > 32768 || n == 0 || n > 64) return OR_ERR_ARG;
+    lz_params P[64];
+    for (uint32_t k = 0; k < n; k++) {
+        const int32_t* d = desc + 6 * k;
+        if (d[0] == 1) continue;
+        if (d[0] != 0) return OR_ERR_ARG;
+        if (!(d[2] == 0 && d[3] == 0 && d[4] == 0 && d[5] == 0) &&
+            !(3 <= d[2] && d[2] <= d[3] && d[3] <= 258 && 1 <= d[4] && d[4] <= d[5] && d[5] <= 32768))
+            return OR_ERR_ARG;
+        lz_params q = {d[1] ? 1 : 0, d[2], d[3], d[4], d[5]};
+        P[k] = q;
+    }
+    bw_t w = {out, out_cap, 0, 0, 0, 0};
+    uint64_t pos = 0;
+    for (;;) {
+        uint64_t dlen = len - pos; int fin = 1;
+        if (dlen > chunk_len) { dlen = chunk_len; fin = 0; }
+        else if (dlen == chunk_len && pos + dlen < len) fin = 0;
+        uint64_t hlen = pos < hist_limit ? pos : hist_limit;
+        const uint8_t* base = data + (pos - hlen);
+        /* decide: bitLengths of every substrategy (:35-44) */
+        int64_t best[8]; int pick[8];
+        for (int i = 0; i < 8; i++) { best[i] = INT64_MAX; pick[i] = -1; }
+        for (uint32_t k = 0; k < n; k++) {
+            int64_t bl[8];
+            if (desc[6 * k] == 1) {                  /* Uncompressed (:22-26) */
+                int64_t nblk = ((int64_t)dlen + 65534) / 65535; if (nblk < 1) nblk = 1;
+                for (int i = 0; i < 8; i++) bl[i] = (int64_t)dlen * 8 + nblk * 40 + ((13 - i) % 8 - 5);
+            } else {                                 /* Lz77Huffman: a counting pass (:45-53) */
+                sink_t cnt = { NULL, 0 };
+                if (lz_compress(base, 0, (int64_t)hlen, (int64_t)dlen, &P[k], 0, &cnt, 0) != 0) return OR_ERR_ARG;
+                for (int i = 0; i < 8; i++) bl[i] = (int64_t)cnt.count;
+            }
+            for (int i = 0; i < 8; i++) if (bl[i] < best[i]) { best[i] = bl[i]; pick[i] = (int)k; }
+        }
+        /* compressTo: the decision for the current bit position (:51-53) */
+        sink_t sk = { &w, 0 };
+        const int k = pick[sk_pos(&sk)];
+        if (desc[6 * k] == 1) unc_compress(base, 0, (int64_t)hlen, (int64_t)dlen, fin, &sk);
+        else if (lz_compress(base, 0, (int64_t)hlen, (int64_t)dlen, &P[k], fin, &sk, 0) != 0) return OR_ERR_ARG;
+        pos += dlen;
+        if (fin) break;
+    }
+    bw_finish(&w);
+    if (w.overflow) return OR_ERR_CAPACITY;
+    return (int64_t)w.n;
+}
+
 int64_t or_deflate_block_bits(const uint8_t* data, uint64_t len, uint32_t chunk_len, uint32_t hist_limit,
                               int strategy, uint64_t* bits, uint64_t cap) {
     if (strategy < 0 || strategy > 6) return OR_ERR_ARG;

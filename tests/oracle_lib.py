@@ -56,6 +56,9 @@ def lib():
         L.or_deflate_lz.argtypes = [u8p, ctypes.c_uint64, ctypes.c_uint32, ctypes.c_uint32, ctypes.c_int,
                                     ctypes.c_int, ctypes.c_int, ctypes.c_int, ctypes.c_int, ctypes.c_int,
                                     u8p, ctypes.c_uint64]
+        L.or_deflate_multi.restype = ctypes.c_int64
+        L.or_deflate_multi.argtypes = [u8p, ctypes.c_uint64, ctypes.c_uint32, ctypes.c_uint32, ctypes.c_void_p,
+                                       ctypes.c_uint32, u8p, ctypes.c_uint64]
         L.or_deflate_block_bits.restype = ctypes.c_int64
         L.or_deflate_block_bits.argtypes = [u8p, ctypes.c_uint64, ctypes.c_uint32, ctypes.c_uint32,
                                             ctypes.c_int, ctypes.POINTER(ctypes.c_uint64), ctypes.c_uint64]
@@ -116,6 +119,21 @@ def deflate_lz(data, dynamic, min_run, max_run, min_dist, max_dist, chunk_len=65
                             int(brute), out, cap)
     if r < 0:
         raise ValueError(f"or_deflate_lz failed: {r}")
+    return out.raw[:r]
+
+
+def deflate_multi(data, subs, chunk_len=65536, hist_limit=32768):
+    """MultiStrategy(subs...): each sub is "UNCOMPRESSED" or (dynamic, minRun, maxRun, minDist, maxDist)."""
+    src, n = _buf(data)
+    flat = []
+    for st in subs:
+        flat += [1, 0, 0, 0, 0, 0] if st == "UNCOMPRESSED" else [0] + [int(x) for x in st]
+    arr = (ctypes.c_int32 * len(flat))(*flat)
+    cap = deflate_bound(n, chunk_len) * 2
+    out = ctypes.create_string_buffer(cap)
+    r = lib().or_deflate_multi(src, n, chunk_len, hist_limit, arr, len(subs), out, cap)
+    if r < 0:
+        raise ValueError(f"or_deflate_multi failed: {r}")
     return out.raw[:r]
 
 

@@ -266,3 +266,53 @@ def deflate(data, strategy="RLE_DYNAMIC", chunk_len=65536, hist_limit=32768, par
         if final:
             break
     return w.getbytes()
+
+
+def stored_blocks(w, data, final):
+    """Uncompressed (D/comp/Uncompressed.java:33-46), restated from RFC 1951 §3.2.4: blocks of at
+    most 65535 bytes, each byte-aligned after its 3 header bits."""
+    i = 0
+    while True:
+        n = min(len(data) - i, 65535)
+        w.bits(1 if final and i + n == len(data) else 0, 1)
+        w.bits(0, 2)
+        w.bits(0, (8 - w.n % 8) % 8)
+        w.bits(n, 16)
+        w.bits(n ^ 0xFFFF, 16)
+        for b in data[i:i + n]:
+            w.bits(b, 8)
+        i += n
+        if i >= len(data):
+            break
+
+
+def deflate_multi(data, subs, chunk_len=65536, hist_limit=32768):
+    """MultiStrategy(subs...) (D/comp/MultiStrategy.java): per chunk, the first substrategy giving the
+    fewest bits from the writer's current bit position.  Lengths are measured by writing each
+    candidate into a scratch writer at that position (no closed form)."""
+    w = BitWriter()
+    pos = 0
+    n = len(data)
+    while True:
+        dlen = min(n - pos, chunk_len)
+        final = pos + dlen >= n
+        hlen = min(pos, hist_limit)
+        buf = data[pos - hlen: pos + dlen]
+        best = None
+        for st in subs:
+            t = BitWriter()
+            t.n = w.n % 8
+            if st == "UNCOMPRESSED":
+                stored_blocks(t, buf[hlen:], False)
+            else:
+                compress_block(t, buf, hlen, dlen, tuple(st), False)
+            if best is None or t.n < best[0]:
+                best = (t.n, st)
+        if best[1] == "UNCOMPRESSED":
+            stored_blocks(w, buf[hlen:], final)
+        else:
+            compress_block(w, buf, hlen, dlen, tuple(best[1]), final)
+        pos += dlen
+        if final:
+            break
+    return w.getbytes()

@@ -121,3 +121,34 @@ def test_gzip_config1_fixture():
     reason, out, hd, end = O.gunzip(gz + b"trailing")
     assert reason is None and out == data and end == len(gz)
     assert hd["mtime"] == 1700000000 and hd["os"] == 3 and hd["has_header_crc"]
+
+
+MULTI_SETS = [
+    ["UNCOMPRESSED"],
+    [P.PRESETS["RLE_DYNAMIC"], "UNCOMPRESSED"],
+    ["UNCOMPRESSED", P.PRESETS["LITERAL_STATIC"]],
+    [P.PRESETS["LITERAL_DYNAMIC"], P.PRESETS["RLE_STATIC"], "UNCOMPRESSED", P.PRESETS["FULL_DYNAMIC"]],
+    [P.PRESETS["FULL_STATIC"], P.PRESETS["FULL_DYNAMIC"]],
+]
+
+
+@pytest.mark.parametrize("k", range(len(MULTI_SETS)))
+def test_nversion_multistrategy(k):
+    """MultiStrategy / Uncompressed: the oracle (closed-form Uncompressed lengths, D/comp/
+    Uncompressed.java:22-26) against pyref (lengths measured by writing) and round trips."""
+    subs = MULTI_SETS[k]
+    rng = random.Random(40 + k)
+    for data in samples(3)[:12] + [bytes(rng.randrange(256) for _ in range(70000)), b"\x05" * 70000]:
+        for chunk_len, hist in [(65536, 32768), (700, 32768), (97, 1), (65535, 0)]:
+            if any(s != "UNCOMPRESSED" and s[4] > 1 for s in subs) and len(data) > 5000:
+                continue
+            a = O.deflate_multi(data, subs, chunk_len, hist)
+            b = P.deflate_multi(data, subs, chunk_len, hist)
+            assert a == b, (k, len(data), chunk_len, hist)
+            assert zlib.decompress(a, -15) == data
+
+
+def test_uncompressed_preset_equals_single_multistrategy():
+    for data in samples(4)[:10]:
+        assert O.deflate(data, "UNCOMPRESSED") == O.deflate_multi(data, ["UNCOMPRESSED"])
+        assert O.deflate(data, "RLE_DYNAMIC") == O.deflate_multi(data, [P.PRESETS["RLE_DYNAMIC"]])
