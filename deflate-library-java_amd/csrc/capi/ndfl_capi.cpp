@@ -595,6 +595,39 @@ int ndfl_crc32(ndfl_ctx* c, uint32_t* crc_inout, const uint8_t* data, uint64_t l
     return NDFL_OK;
 }
 
+int ndfl_adler32(ndfl_ctx* c, uint32_t* adler_inout, const uint8_t* data, uint64_t len, uint32_t flags) {
+    if (!c || !adler_inout || (!data && len)) return NDFL_E_ARG;
+    if (len == 0) return NDFL_OK;
+    HIPCHK(hipSetDevice(c->device));
+    hipStream_t s = c->stream;
+    const uint8_t* d = data;
+    if (!(flags & NDFL_IN_DEVICE)) {
+        HIPCHK(c->d_in.ensure(len));
+        HIPCHK(hipMemcpyAsync(c->d_in.p, data, len, hipMemcpyHostToDevice, s));
+        d = c->d_in.as<uint8_t>();
+    }
+    const uint64_t nseg = (len + 65535) / 65536;
+    HIPCHK(c->d_crc.ensure(nseg * 8));
+    HIPCHK(hipEventRecord(c->ev0, s));
+    hipLaunchKernelGGL(ndfl_adler_segments_kernel, dim3((uint32_t)nseg), dim3(1024), 0, s, d, len, c->d_crc.as<uint32_t>());
+    HIPCHK(hipGetLastError());
+    HIPCHK(hipEventRecord(c->ev1, s));
+    std::vector<uint32_t> st(nseg * 2);
+    HIPCHK(hipMemcpyAsync(st.data(), c->d_crc.p, nseg * 8, hipMemcpyDeviceToHost, s));
+    HIPCHK(hipStreamSynchronize(s));
+    float ms = 0;
+    hipEventElapsedTime(&ms, c->ev0, c->ev1);
+    c->last_ms = ms;
+    uint64_t a = *adler_inout & 0xFFFF, b = *adler_inout >> 16;
+    for (uint64_t k = 0; k < nseg; k++) {
+        const uint64_t sl = std::min<uint64_t>(65536, len - k * 65536);
+        b = (b + sl % 65521 * a + st[2 * k + 1]) % 65521;
+        a = (a + st[2 * k]) % 65521;
+    }
+    *adler_inout = (uint32_t)(b << 16 | a);
+    return NDFL_OK;
+}
+
 int ndfl_inflate(ndfl_ctx* c, const uint8_t* in, uint64_t in_len, uint8_t* out, uint64_t out_cap,
                  uint64_t* out_len, uint64_t* consumed_bits, uint32_t flags) {
     if (!c || !out_len || !consumed_bits || (!in && in_len)) return NDFL_E_ARG;

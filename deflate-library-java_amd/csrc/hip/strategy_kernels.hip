@@ -31,9 +31,6 @@ struct AsmArgs {
     uint32_t* out;                   // zeroed, word-aligned
 };
 
-__device__ __forceinline__ void or_byte(uint32_t* out, uint64_t byte, uint32_t v) {
-    atomicOr(&out[byte >> 2], v << (8 * (uint32_t)(byte & 3)));
-}
 }  // namespace
 
 extern "C" __global__ void __launch_bounds__(256)
@@ -92,5 +89,50 @@ ndfl_assemble_kernel(AsmArgs a) {
         v &= m;
         if (m == 0xFFFFFFFFu && w != w0 && w != w1) a.out[w] = v;
         else atomicOr(&a.out[w], v);
+    }
+}
+
+// ---- Adler-32 (java.util.zip.Adler32, the zlib container's checksum: D/ZlibOutputStream.java:22,
+// D/ZlibInputStream.java:25) -------------------------------------------------------------------
+// One 1024-thread workgroup per 64 KiB segment: S = sum of bytes, T = sum of (len - i) * byte_i
+// (i from 0), both mod 65521; the host folds the segments in order: b += len*a + T, a += S.
+extern "C" __global__ void __launch_bounds__(1024)
+ndfl_adler_segments_kernel(const uint8_t* in, uint64_t n, uint32_t* seg_st) {
+    __shared__ unsigned long long rs[16], rt[16];
+    const uint32_t seg = blockIdx.x;
+    const uint64_t s0 = (uint64_t)seg * 65536;
+    const uint32_t len = (uint32_t)min((uint64_t)65536, n - s0);
+    const uint32_t t0 = threadIdx.x * 64;
+    const uint32_t cnt = len > t0 ? min(64u, len - t0) : 0u;
+    const uint8_t* p = in + s0 + t0;
+    uint32_t ss = 0, tt = 0;                         // sums over this thread's bytes, weights cnt - k
+    if (cnt == 64 && (((uintptr_t)p) & 15) == 0) {
+        const u32x4* q = (const u32x4*)p;
+#pragma unroll
+        for (int k = 0; k < 4; k++) {
+            const u32x4 v = __builtin_nontemporal_load(q + k);
+            const uint32_t w4[4] = {v.x, v.y, v.z, v.w};
+#pragma unroll
+            for (int j = 0; j < 16; j++) {
+                const uint32_t b = (w4[j >> 2] >> (8 * (j & 3))) & 0xFF;
+                ss += b;
+                tt += (uint32_t)(64 - (16 * k + j)) * b;
+            }
+        }
+    } else {
+        for (uint32_t k = 0; k < cnt; k++) { const uint32_t b = p[k]; ss += b; tt += (cnt - k) * b; }
+    }
+    // weight of this thread's bytes relative to the segment end: + bytes after them
+    const unsigned long long after = (unsigned long long)(len - t0 - cnt);
+    unsigned long long S = ss, T = tt + (cnt ? after * ss : 0ull);
+    S = wave_sum(S);
+    T = wave_sum(T);
+    if ((threadIdx.x & 63) == 0) { rs[threadIdx.x >> 6] = S; rt[threadIdx.x >> 6] = T; }
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        unsigned long long a = 0, b = 0;
+        for (int k = 0; k < 16; k++) { a += rs[k]; b += rt[k]; }
+        seg_st[2 * seg] = (uint32_t)(a % 65521u);
+        seg_st[2 * seg + 1] = (uint32_t)(b % 65521u);
     }
 }

@@ -280,6 +280,14 @@ class Context:
         return v.value
 
 
+    def adler32(self, data, adler=1, flags=0):
+        addr, keep = _ptr(data)
+        n = data.numel() * data.element_size() if hasattr(data, "numel") else len(data)
+        v = ctypes.c_uint32(adler)
+        check(load().ndfl_adler32(self._h, ctypes.byref(v), addr, n, flags), "ndfl_adler32")
+        return v.value
+
+
 def _strategy_id(s):
     if isinstance(s, (Lz77Huffman, MultiStrategy, _UncompressedType)):
         return s

@@ -31,7 +31,7 @@ E_ARG, E_UNSUPPORTED, E_CAPACITY, E_DEVICE, E_STATE, E_INTERNAL = -1, -2, -3, -4
 EXPORTS = ["ndfl_abi_version", "ndfl_error_string", "ndfl_ctx_create", "ndfl_ctx_destroy",
            "ndfl_ctx_set_stream", "ndfl_ctx_last_kernel_ms", "ndfl_ctx_timings", "ndfl_deflate_chunks",
            "ndfl_deflate_chunks_lz77", "ndfl_deflate_chunks_multi", "ndfl_deflate_bound",
-           "ndfl_inflate", "ndfl_inflate_range", "ndfl_inflate_resolve", "ndfl_bits_shift", "ndfl_crc32",
+           "ndfl_inflate", "ndfl_inflate_range", "ndfl_inflate_resolve", "ndfl_bits_shift", "ndfl_crc32", "ndfl_adler32",
            "ndfl_crc32_combine"]
 
 KIND_LZ77, KIND_UNCOMPRESSED = 0, 1
@@ -77,6 +77,7 @@ def load():
     L.ndfl_inflate_resolve.argtypes = [vp, ctypes.POINTER(u64)]
     L.ndfl_bits_shift.argtypes = [vp, vp, u64, u32, vp, u64, u32]
     L.ndfl_crc32.argtypes = [vp, ctypes.POINTER(u32), vp, u64, u32]
+    L.ndfl_adler32.argtypes = [vp, ctypes.POINTER(u32), vp, u64, u32]
     L.ndfl_crc32_combine.restype = u32
     L.ndfl_crc32_combine.argtypes = [u32, u32, u64]
     _lib = L

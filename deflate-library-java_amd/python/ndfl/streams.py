@@ -4,6 +4,7 @@ Java exception mapping: IllegalArgumentException -> ValueError, IllegalStateExce
 RuntimeError, IOException -> OSError, DataFormatException -> ndfl.DataFormatException.
 """
 import ctypes
+import enum
 import dataclasses
 import os
 from typing import Optional
@@ -44,6 +45,7 @@ class DeflaterOutputStream:
         self._bitlen = 0          # 0..7
         self._ended = False
         self._crc = None          # GzipOutputStream asks for a CRC pass fused into the encoder
+        self._adler = None        # ZlibOutputStream: Adler-32 over each batch, on the GPU
 
     def getUnderlyingStream(self):
         if self._out is None:
@@ -86,6 +88,8 @@ class DeflaterOutputStream:
             ctypes.addressof(out), cap, 0, crc=self._crc)
         if self._crc is not None:
             self._crc = crc
+        if self._adler is not None and data:
+            self._adler = self._ctx.adler32(data, self._adler)
         nbytes = (endbits + 7) // 8
         raw = bytearray(out.raw[:nbytes])
         if raw:
@@ -416,14 +420,169 @@ class GzipInputStream:
 
 
 class ZlibMetadata:
-    pass
+    """D/ZlibMetadata.java:19-127 (record of compressionMethod, compressionInfo, presetDictionary,
+    compressionLevel).  presetDictionary is None or the 32-bit DICTID."""
+
+    class CompressionMethod(enum.Enum):
+        DEFLATE = 0
+        RESERVED = 1
+
+    class CompressionLevel(enum.Enum):
+        FASTEST = 0
+        FAST = 1
+        DEFAULT = 2
+        MAXIMUM = 3
+
+    CHECKSUM_MODULUS = 31
+
+    def __init__(self, compressionMethod, compressionInfo, presetDictionary, compressionLevel):
+        if compressionMethod is None or compressionLevel is None:
+            raise TypeError("null")
+        if compressionInfo >> 4 != 0 or (compressionMethod == ZlibMetadata.CompressionMethod.DEFLATE
+                                         and compressionInfo > 7):
+            raise ValueError("Invalid compression info value")           # (:37-38)
+        self.compressionMethod = compressionMethod
+        self.compressionInfo = compressionInfo
+        self.presetDictionary = presetDictionary
+        self.compressionLevel = compressionLevel
+
+    def __eq__(self, o):
+        return isinstance(o, ZlibMetadata) and (self.compressionMethod, self.compressionInfo, self.presetDictionary,
+                                                  self.compressionLevel) == (o.compressionMethod, o.compressionInfo,
+                                                                             o.presetDictionary, o.compressionLevel)
+
+    @staticmethod
+    def read(inp):
+        """(:52-83): header checksum, method, DICTID (big-endian), level."""
+        from . import DataFormatException, Reason
+        hb = inp.read(2)
+        if hb is None or len(hb) < 2:
+            raise DataFormatException(Reason.UNEXPECTED_END_OF_STREAM)
+        cmf, flg = hb[0], hb[1]
+        if (cmf << 8 | flg) % ZlibMetadata.CHECKSUM_MODULUS != 0:
+            raise DataFormatException(Reason.HEADER_CHECKSUM_MISMATCH, "Header checksum mismatch")
+        cm = cmf & 0xF
+        if cm == 8:
+            method = ZlibMetadata.CompressionMethod.DEFLATE
+        elif cm == 15:
+            method = ZlibMetadata.CompressionMethod.RESERVED
+        else:
+            raise DataFormatException(Reason.UNSUPPORTED_COMPRESSION_METHOD, f"Unsupported compression method: {cm}")
+        dictid = None
+        if (flg >> 5) & 1:
+            d = inp.read(4)
+            if d is None or len(d) < 4:
+                raise DataFormatException(Reason.UNEXPECTED_END_OF_STREAM)
+            dictid = int.from_bytes(d, "big")
+        return ZlibMetadata(method, cmf >> 4, dictid, ZlibMetadata.CompressionLevel(flg >> 6))
+
+    def header_bytes(self):
+        """(:90-108)."""
+        cm = 8 if self.compressionMethod == ZlibMetadata.CompressionMethod.DEFLATE else 15
+        cmf = cm | self.compressionInfo << 4
+        flg = (1 if self.presetDictionary is not None else 0) << 5 | self.compressionLevel.value << 6
+        flg |= (31 - (cmf << 8 | flg) % 31) % 31
+        out = bytes([cmf, flg])
+        if self.presetDictionary is not None:
+            out += (self.presetDictionary & 0xFFFFFFFF).to_bytes(4, "big")
+        return out
+
+    def write(self, out):
+        out.write(self.header_bytes())
+
+
+ZlibMetadata.DEFAULT = ZlibMetadata(ZlibMetadata.CompressionMethod.DEFLATE, 7, None,
+                                    ZlibMetadata.CompressionLevel.DEFAULT)
 
 
 class ZlibOutputStream:
-    def __init__(self, *a, **k):
-        raise NotImplementedError("zlib container: SURVEY §8f row 3 (not yet on the GPU path)")
+    """D/ZlibOutputStream.java:19-91.  Adler-32 on the GPU over each batch the encoder takes."""
+
+    def __init__(self, out, meta, context=None):
+        dout = out if isinstance(out, DeflaterOutputStream) else DeflaterOutputStream(out, context=context)
+        if meta is None:
+            raise TypeError("meta")
+        meta.write(dout.getUnderlyingStream())
+        self._d = dout
+        self._d._adler = 1
+        self._ended = False
+
+    def write(self, b, off=0, length=None):
+        if self._ended:
+            raise RuntimeError("Stream already ended")
+        if isinstance(b, int):
+            b = bytes([b & 0xFF])
+        mv = memoryview(bytes(b))
+        if length is None:
+            length = len(mv) - off
+        self._d.write(mv, off, length)
+
+    def finish(self):
+        if self._ended:
+            raise RuntimeError("Stream already ended")
+        self._d.finish()
+        self._d.getUnderlyingStream().write(self._d._adler.to_bytes(4, "big"))     # (:70-71)
+        self._ended = True
+
+    def close(self):
+        if not self._ended:
+            self.finish()
+        self._d.close()
+
+    def __enter__(self):
+        return self
+
+    def __exit__(self, *exc):
+        self.close()
 
 
 class ZlibInputStream:
-    def __init__(self, *a, **k):
-        raise NotImplementedError("zlib container: SURVEY §8f row 3 (not yet on the GPU path)")
+    """D/ZlibInputStream.java:22-100: header, inflate with exact end, big-endian Adler-32 trailer
+    (EOF -> UNEXPECTED_END_OF_STREAM, mismatch -> DECOMPRESSED_CHECKSUM_MISMATCH).  A preset
+    dictionary is recorded but not applied, as in the reference."""
+
+    def __init__(self, inp, context=None):
+        if inp is None:
+            raise TypeError("in")
+        self._ctx = _ctx(context)
+        self.metadata = ZlibMetadata.read(inp)
+        self._raw = inp
+        self._inf = InflaterInputStream(inp, True, context=self._ctx)
+        self._done = False
+        self._adler = 1
+
+    def getMetadata(self):
+        return self.metadata
+
+    def _trailer(self):
+        from . import DataFormatException, Reason
+        t = self._raw.read(4)
+        if t is None or len(t) < 4:
+            raise DataFormatException(Reason.UNEXPECTED_END_OF_STREAM)
+        if int.from_bytes(t, "big") != self._adler:
+            raise DataFormatException(Reason.DECOMPRESSED_CHECKSUM_MISMATCH, "Decompression Adler-32 mismatch")
+
+    def readall(self):
+        if self._done:
+            return b""
+        out = self._inf.readall()
+        self._adler = self._ctx.adler32(out) if out else 1
+        self._done = True
+        self._trailer()
+        return out
+
+    def read(self, b=None, off=0, length=None):
+        if self._done:
+            return -1
+        if self._inf._buf is None:
+            self._inf._decode()
+            if self._inf._error is None:
+                self._adler = self._ctx.adler32(self._inf._buf) if self._inf._buf else 1
+        r = self._inf.read(b, off, length)
+        if r == -1:
+            self._done = True
+            self._trailer()
+        return r
+
+    def close(self):
+        self._raw.close()

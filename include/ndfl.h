@@ -179,6 +179,10 @@ int ndfl_bits_shift(ndfl_ctx* ctx, const uint8_t* in, uint64_t nbits, uint32_t s
 
 /* java.util.zip.CRC32.update over a buffer, on the GPU (flags: NDFL_IN_DEVICE). */
 int ndfl_crc32(ndfl_ctx* ctx, uint32_t* crc_inout, const uint8_t* data, uint64_t len, uint32_t flags);
+/* java.util.zip.Adler32.update over a buffer, on the GPU (flags: NDFL_IN_DEVICE): the zlib
+ * container's checksum (D/ZlibOutputStream.java:22,48, D/ZlibInputStream.java:25,57-69).
+ * *adler_inout = (b << 16) | a, 1 for a fresh checksum. */
+int ndfl_adler32(ndfl_ctx* ctx, uint32_t* adler_inout, const uint8_t* data, uint64_t len, uint32_t flags);
 /* crc of A||B from crc(A), crc(B), |B| (host arithmetic). */
 uint32_t ndfl_crc32_combine(uint32_t crc_a, uint32_t crc_b, uint64_t len_b);
 
