@@ -30,6 +30,7 @@
 #include <vector>
 #include <algorithm>
 #include <unordered_map>
+#include <chrono>
 #include <string.h>
 #include <stdio.h>
 #include <stdlib.h>
@@ -582,6 +583,8 @@ struct ChainRes {
     uint64_t out_count;   // output bytes (before the error, if any)
     uint32_t status;      // ST_*
     uint32_t reason;      // for ST_ERROR
+    uint32_t next;        // count pass, ST_BOUNDARY at a candidate: its index in the candidate list
+    uint32_t pad;
 };
 
 struct EmitChain {
@@ -683,7 +686,7 @@ static int resolve_rounds(InflateScratch& S, hipStream_t s, uint8_t* d_out, uint
     uint32_t* pend = (uint32_t*)S.d_pend;
     uint32_t* ref = (uint32_t*)S.d_ref;
     INF_CHK(hipMemsetAsync(cnt, 0, 8, s));
-    hipLaunchKernelGGL(ndfl_inflate_pending_list_kernel, dim3((uint32_t)((npw + 255) / 256)), dim3(256), 0, s,
+    hipLaunchKernelGGL(ndfl_inflate_pending_list_kernel, dim3((uint32_t)((npw + 4095) / 4096)), dim3(256), 0, s,
                        (const uint32_t*)pend, (uint64_t)0, npw, lst[0], cnt);
     INF_CHK(hipGetLastError());
     uint32_t* h = (uint32_t*)S.h_cnt;
@@ -729,6 +732,9 @@ static int inflate_run(InflateScratch& S, hipStream_t s, const uint8_t* in, uint
     *out_len = 0;
     *consumed_bits = 0;
     S.pending = false;
+    static const bool htime = getenv("NDFL_HOST_TIMES") != nullptr;
+    auto hnow = []() { return std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now().time_since_epoch()).count(); };
+    double ht[8] = {hnow(), 0, 0, 0, 0, 0, 0, 0};
     const uint64_t nbits = in_len * 8;
     const uint64_t nwords = (in_len + 3) / 4;
     if (start_bit > nbits) return -1;
@@ -752,7 +758,9 @@ static int inflate_run(InflateScratch& S, hipStream_t s, const uint8_t* in, uint
         // boundaries that are not candidates); every window holds a block start unless blocks
         // are longer than the gap, in which case chains just get longer
         const uint64_t nw32 = (nbits + 31) / 32;
-        const uint32_t period = FIND_PERIOD_WORDS, win = FIND_WIN_WORDS;
+        static const uint32_t env_win = getenv("NDFL_FIND_WIN") ? (uint32_t)atoi(getenv("NDFL_FIND_WIN")) : 0;
+        static const uint32_t env_per = getenv("NDFL_FIND_PERIOD") ? (uint32_t)atoi(getenv("NDFL_FIND_PERIOD")) : 0;
+        const uint32_t period = env_per ? env_per : FIND_PERIOD_WORDS, win = env_win ? env_win : FIND_WIN_WORDS;
         const uint64_t nwin = (nw32 + period - 1) / period;
         const uint64_t nthr = nw32 <= (uint64_t)period ? nw32 : (nwin - 1) * win + std::min<uint64_t>(win, nw32 - (nwin - 1) * period);
         const uint32_t qcap = (uint32_t)std::min<uint64_t>(0x7FFFFFFFull, nbits / 256 + 65536);
@@ -873,6 +881,7 @@ static int inflate_run(InflateScratch& S, hipStream_t s, const uint8_t* in, uint
         INF_CHK(hipStreamSynchronize(s));
         return 0;
     };
+    ht[1] = hnow();
     S.repairs = 0;
     S.count_first = true;
     int rc = run_count(starts, res);
@@ -887,14 +896,23 @@ static int inflate_run(InflateScratch& S, hipStream_t s, const uint8_t* in, uint
     // link from the range start.  A boundary that is no candidate (fixed-Huffman block, header
     // rejected by the finder) is repaired: every such boundary of every chain is decoded on in
     // parallel rounds; a final serial fallback guarantees progress.
-    std::unordered_map<uint64_t, size_t> at;
-    at.reserve(starts.size() * 2);
-    for (size_t k = 0; k < starts.size(); k++) at[starts[k]] = k;
+    // chain starts: the sorted candidate prefix (binary search) plus repaired boundaries
+    const size_t n0 = starts.size();
+    std::unordered_map<uint64_t, size_t> extra;
+    auto find_at = [&](uint64_t b, size_t& idx) -> bool {
+        auto it = std::lower_bound(starts.begin(), starts.begin() + n0, b);
+        if (it != starts.begin() + n0 && *it == b) { idx = (size_t)(it - starts.begin()); return true; }
+        auto e = extra.find(b);
+        if (e != extra.end()) { idx = e->second; return true; }
+        return false;
+    };
     for (int round = 0; round < 8; round++) {
         std::vector<uint64_t> todo;
+        size_t dummy;
         for (size_t k = 0; k < res.size(); k++)
-            if (res[k].status == ST_BOUNDARY && res[k].end_bit < end_bit && !at.count(res[k].end_bit)) {
-                at[res[k].end_bit] = NONE;          // placeholder, filled below
+            if (res[k].status == ST_BOUNDARY && res[k].end_bit < end_bit &&
+                !(res[k].next < n0 && starts[res[k].next] == res[k].end_bit) && !find_at(res[k].end_bit, dummy)) {
+                extra[res[k].end_bit] = NONE;       // placeholder, filled below
                 todo.push_back(res[k].end_bit);
             }
         if (todo.empty()) break;
@@ -904,10 +922,11 @@ static int inflate_run(InflateScratch& S, hipStream_t s, const uint8_t* in, uint
         for (size_t k = 0; k < todo.size(); k++) {
             starts.push_back(todo[k]);
             res.push_back(r2[k]);
-            at[todo[k]] = starts.size() - 1;
+            extra[todo[k]] = starts.size() - 1;
         }
         S.repairs += todo.size();
     }
+    ht[2] = hnow();
     std::vector<EmitChain> chains;
     std::vector<uint64_t> offs;
     uint64_t off = dict_len;
@@ -928,8 +947,9 @@ static int inflate_run(InflateScratch& S, hipStream_t s, const uint8_t* in, uint
         if (r.status == ST_ERROR) break;
         if (r.end_bit == end_bit) { stop_bit = end_bit; break; }
         if (r.end_bit > end_bit) return -1;          // the range end is no block boundary
-        auto it = at.find(r.end_bit);
-        if (it != at.end() && it->second != (size_t)NONE) { cur = it->second; continue; }
+        size_t nxt;
+        if (r.next < n0 && starts[r.next] == r.end_bit) { cur = r.next; continue; }
+        if (find_at(r.end_bit, nxt) && nxt != (size_t)NONE) { cur = nxt; continue; }
         // serial fallback (beyond the parallel rounds)
         std::vector<uint64_t> st1{r.end_bit};
         std::vector<ChainRes> r1;
@@ -937,7 +957,7 @@ static int inflate_run(InflateScratch& S, hipStream_t s, const uint8_t* in, uint
         if (rc) return rc;
         starts.push_back(r.end_bit);
         res.push_back(r1[0]);
-        at[r.end_bit] = starts.size() - 1;
+        extra[r.end_bit] = starts.size() - 1;
         cur = starts.size() - 1;
         S.repairs++;
     }
@@ -956,6 +976,7 @@ static int inflate_run(InflateScratch& S, hipStream_t s, const uint8_t* in, uint
                 t64[4] * 1e-5, t64[5] * 1e-5, t64[6] * 1e-5);
     }
     const uint64_t total = off - dict_len;
+    ht[3] = hnow();
     if (total > out_cap) { *out_len = total; return -3; }
 
     // emit pass
@@ -992,6 +1013,7 @@ static int inflate_run(InflateScratch& S, hipStream_t s, const uint8_t* in, uint
     std::vector<ChainRes> er(nch);
     INF_CHK(hipMemcpyAsync(er.data(), S.d_res, nch * sizeof(ChainRes), hipMemcpyDeviceToHost, s));
     INF_CHK(hipStreamSynchronize(s));
+    ht[4] = hnow();
     float ms = 0;
     hipEventElapsedTime(&ms, e2, e3);
     S.last_ms_emit = ms;
@@ -1011,6 +1033,9 @@ static int inflate_run(InflateScratch& S, hipStream_t s, const uint8_t* in, uint
     S.last_ms_wall = ms2;
     hipEventElapsedTime(&ms2, e2, e3);
     *last_ms = ms2;
+    ht[5] = hnow();
+    if (htime) fprintf(stderr, "[ndfl] inflate host ms: finder+starts %.2f count+repairs %.2f link %.2f emit %.2f resolve %.2f\n",
+                       ht[1] - ht[0], ht[2] - ht[1], ht[3] - ht[2], ht[4] - ht[3], ht[5] - ht[4]);
     // first error in stream order (the emit pass also checks the dictionary bound exactly)
     for (uint32_t k = 0; k < nch; k++) {
         if (er[k].status == ST_ERROR) {

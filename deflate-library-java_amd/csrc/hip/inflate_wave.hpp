@@ -746,9 +746,10 @@ __device__ __forceinline__ uint64_t wave_excl_u64(uint64_t v, int lane) {
 }
 
 // Is b one of the header candidates (sorted list)?
-__device__ __forceinline__ bool is_cand(const uint64_t* cands, uint32_t ncand, uint64_t b) {
+__device__ __forceinline__ bool is_cand(const uint64_t* cands, uint32_t ncand, uint64_t b, uint32_t* idx = nullptr) {
     uint32_t lo = 0, hi = ncand;
     while (lo < hi) { const uint32_t mid = (lo + hi) >> 1; if (cands[mid] < b) lo = mid + 1; else hi = mid; }
+    if (idx) *idx = lo;
     return lo < ncand && cands[lo] == b;
 }
 
@@ -870,7 +871,7 @@ ndfl_inflate_count_wave_kernel(const uint32_t* w, uint64_t nwords, uint64_t nbit
     const uint32_t c = order[s_ticket];
     const uint64_t start = starts[c], stop = stops[c];
     uint64_t cur = start, total = 0, endpos = start;
-    uint32_t status = ST_BOUNDARY, reason = 0, nslow = 0, nfix = 0, nround = 0;
+    uint32_t status = ST_BOUNDARY, reason = 0, nslow = 0, nfix = 0, nround = 0, next_idx = 0xFFFFFFFFu;
     bool recording = slot_base + c < pool.nslot;
     uint32_t prev_rec = NOREC;
     uint64_t span_est = 1ull << 18;             // round span: the previous block's size once known
@@ -884,7 +885,7 @@ ndfl_inflate_count_wave_kernel(const uint32_t* w, uint64_t nwords, uint64_t nbit
     for (int blk = 0;; blk++) {
         // a chain ends at the first later block boundary that is itself a header candidate (its own
         // chain links on from there) or at the range end; false candidates are passed over
-        if (blk > 0 && (cur >= stop || is_cand(cands, ncand, cur))) { status = ST_BOUNDARY; endpos = cur; break; }
+        if (blk > 0 && (cur >= stop || is_cand(cands, ncand, cur, &next_idx))) { status = ST_BOUNDARY; endpos = cur; break; }
         for (uint32_t s = (uint32_t)lane; s < 320; s += 64) S.lens[s] = 0;
         __syncthreads();
         if (lane == 0) parse_hdr(in, cur, S);
@@ -979,6 +980,7 @@ ndfl_inflate_count_wave_kernel(const uint32_t* w, uint64_t nwords, uint64_t nbit
     if (lane == 0) {
         ChainRes o;
         o.end_bit = endpos; o.out_count = total; o.status = status; o.reason = reason;
+        o.next = next_idx; o.pad = 0;
         res[c] = o;
         if (stats) {
             atomicAdd(&stats[0], nslow); atomicAdd(&stats[1], nfix); atomicAdd(&stats[2], nround);
@@ -1160,6 +1162,7 @@ ndfl_inflate_emit_wave_kernel(const uint32_t* w, uint64_t nwords, uint64_t nbits
     if (lane == 0) {
         ChainRes o;
         o.end_bit = endpos; o.out_count = base - ch.out_off; o.status = status; o.reason = reason;
+        o.next = 0xFFFFFFFFu; o.pad = 0;
         res[ci] = o;
     }
     }
@@ -1236,6 +1239,22 @@ ndfl_inflate_resolve_apply_kernel(const uint32_t* list, const uint32_t* nlist, u
 // Initial list: every non-zero bitmap word in [w0, w1).
 extern "C" __global__ void __launch_bounds__(256)
 ndfl_inflate_pending_list_kernel(const uint32_t* pend, uint64_t w0, uint64_t w1, uint32_t* list, uint32_t* nlist) {
-    const uint64_t wd = w0 + (uint64_t)blockIdx.x * 256 + threadIdx.x;
-    block_append(wd < w1 && pend[wd] != 0, (uint32_t)wd, list, nlist);
+    // 16 words per thread (four 16-byte loads); sparse bitmaps are the common case, so the block
+    // only appends when some word is non-zero
+    const uint64_t base = w0 + ((uint64_t)blockIdx.x * 256 + threadIdx.x) * 16;
+    uint32_t v[16];
+    if (base + 16 <= w1 && (base & 3) == 0) {
+        const u32x4* q = (const u32x4*)(pend + base);
+#pragma unroll
+        for (int k = 0; k < 4; k++) { const u32x4 x = q[k]; v[4 * k] = x.x; v[4 * k + 1] = x.y; v[4 * k + 2] = x.z; v[4 * k + 3] = x.w; }
+    } else {
+#pragma unroll
+        for (int k = 0; k < 16; k++) v[k] = base + k < w1 ? pend[base + k] : 0u;
+    }
+    bool any = false;
+#pragma unroll
+    for (int k = 0; k < 16; k++) any |= v[k] != 0;
+    if (!__syncthreads_or(any)) return;
+#pragma unroll
+    for (int k = 0; k < 16; k++) block_append(v[k] != 0, (uint32_t)(base + k), list, nlist);
 }
