@@ -133,13 +133,15 @@ def main():
     total_in = world * n + c_total       # bytes fed to compress + bytes fed to decompress
     value = total_in / per / MIB
 
-    # roofline of the dominant kernel: algorithmic bytes = N + C per launch
+    # roofline of the dominant kernel (longest average launch): algorithmic bytes per launch are
+    # N + C for the encoder and the decoder's write pass, C for the decoder's read-only passes
+    # (header finder + strict stage, count pass) -- SURVEY §8d
     kd, ke = state["t_deflate"], state["t_emit"]
-    alg = n + state["cbytes"]
-    if ke >= kd:
-        dom, kms = "ndfl_inflate_emit_wave_kernel", ke
-    else:
-        dom, kms = "ndfl_deflate_chunks_kernel", kd
+    cands = [("ndfl_deflate_chunks_kernel", kd, n + state["cbytes"]),
+             ("ndfl_inflate_count_wave_kernel", state["t_count"], state["cbytes"]),
+             ("ndfl_inflate_find_kernel+ndfl_inflate_strict_kernel", state["t_find"], state["cbytes"]),
+             ("ndfl_inflate_emit_wave_kernel", ke, n + state["cbytes"])]
+    dom, kms, alg = max(cands, key=lambda x: x[1])
     achieved = alg / (kms / 1e3)
     traffic, traffic_src = pmc_traffic(dom, n)
 

@@ -12,6 +12,8 @@
 #include <algorithm>
 #include <stdlib.h>
 #include <vector>
+#include <functional>
+#include <map>
 
 namespace {
 
@@ -62,8 +64,9 @@ struct ndfl_ctx {
     double deflate_ms = 0;
     DevBuf d_in, d_out, d_status, d_ticket, d_edge_w, d_edge_v, d_crc, d_crc1, d_tabs, d_hostio;
     DevBuf d_lz, d_link, d_match;   // LZ77 path: staging [pad|hist|data], hash links, per-position matches
-    DevBuf d_mdata, d_mstreams[8], d_mbits[8], d_masm;   // strategy composition
+    DevBuf d_mdata, d_mstreams[16], d_mbits[16], d_masm;   // strategy composition
     uint64_t* cb_out = nullptr;     // internal: when set, encoders also write per-chunk block bits here
+    uint32_t parent_len = 0;        // internal: history rule of BinarySplit sub-blocks (0: chunk_len)
     InflateScratch inf;
     uint32_t* h_pinned = nullptr;   // small pinned area for results
 };
@@ -126,7 +129,7 @@ int ndfl_ctx_destroy(ndfl_ctx* c) {
                       &c->d_crc, &c->d_crc1, &c->d_tabs, &c->d_hostio, &c->d_lz, &c->d_link, &c->d_match,
                       &c->d_mdata, &c->d_masm};
     for (DevBuf* b : bufs) b->release();
-    for (int k = 0; k < 8; k++) { c->d_mstreams[k].release(); c->d_mbits[k].release(); }
+    for (int k = 0; k < 16; k++) { c->d_mstreams[k].release(); c->d_mbits[k].release(); }
     c->inf.release();
     if (c->h_pinned) hipHostFree(c->h_pinned);
     if (c->ev0) hipEventDestroy(c->ev0);
@@ -231,6 +234,7 @@ int ndfl_deflate_chunks(ndfl_ctx* c, const uint8_t* hist, uint32_t hist_len, uin
     a.in = d_data; a.n = len; a.chunk_len = chunk_len; a.nchunks = nch;
     a.prev_byte = prev_byte; a.hist_enabled = hist_limit > 0; a.final_last = final_flag ? 1 : 0;
     a.rle = rle; a.dynamic = dyn; a.base_bit = start_bitpos;
+    a.parent_len = c->parent_len ? c->parent_len : chunk_len;
     a.out = d_out; a.status = c->d_status.as<uint64_t>(); a.ticket = c->d_ticket.as<uint32_t>();
     a.edge_w = c->d_edge_w.as<uint64_t>(); a.edge_v = c->d_edge_v.as<uint32_t>();
     a.chunk_bits = c->cb_out;
@@ -348,6 +352,7 @@ int ndfl_deflate_chunks_lz77(ndfl_ctx* c, const uint8_t* hist, uint32_t hist_len
 
     LzArgs la;
     la.buf = buf; la.total = total; la.vstart = LZ_DS - hist_len; la.chunk_len = chunk_len;
+    la.parent_len = c->parent_len ? c->parent_len : chunk_len;
     la.hist_limit = hist_limit; la.min_run = (uint32_t)min_run; la.max_run = (uint32_t)max_run;
     la.min_dist = (uint32_t)min_dist; la.max_dist = (uint32_t)max_dist;
     la.link = c->d_link.as<uint16_t>(); la.match = c->d_match.as<uint32_t>();
@@ -538,7 +543,7 @@ int ndfl_deflate_chunks_multi(ndfl_ctx* c, const uint8_t* hist, uint32_t hist_le
     AsmArgs aa;
     aa.streams = d_streams; aa.data = d_data; aa.n = len; aa.chunk_len = chunk_len; aa.nchunks = nch;
     aa.final_last = final_flag ? 1 : 0; aa.choice = d_choice; aa.src_bit = d_src; aa.dst_bit = d_dst; aa.nbits = d_nb;
-    aa.out = d_out;
+    aa.setfin = nullptr; aa.per_entry_stream = 0; aa.out = d_out;
     HIPCHK(hipEventRecord(c->ev0, s));
     hipLaunchKernelGGL(ndfl_assemble_kernel, dim3(nch), dim3(256), 0, s, aa);
     HIPCHK(hipGetLastError());
@@ -548,6 +553,238 @@ int ndfl_deflate_chunks_multi(ndfl_ctx* c, const uint8_t* hist, uint32_t hist_le
     if (crc_inout && len) {
         uint32_t cr = *crc_inout;
         const int rc = ndfl_crc32(c, &cr, d_data, len, NDFL_IN_DEVICE);
+        if (rc) return rc;
+        *crc_inout = cr;
+    }
+    const uint64_t nbytes = (end_bits + 7) / 8;
+    if (!direct) {
+        if (nbytes > out_cap) return NDFL_E_CAPACITY;
+        HIPCHK(hipMemcpyAsync(out, d_out, nbytes,
+                              (flags & NDFL_OUT_DEVICE) ? hipMemcpyDeviceToDevice : hipMemcpyDeviceToHost, s));
+        HIPCHK(hipStreamSynchronize(s));
+    }
+    return NDFL_OK;
+}
+
+// BinarySplit(sub, minBlockLen) over an Lz77Huffman substrategy (D/comp/BinarySplit.java:21-82):
+// each chunk is halved recursively while both halves are longer than minBlockLen, and a split is
+// kept when the halves' decisions take fewer bits.  Every halving level of the full chunks is
+// encoded by one call (block length L/2^k, history from the parent chunk -- the sub-decide keeps
+// `off`, :44-45), a partial final chunk node by node; the host runs the reference's recursion on
+// the bit counts and ndfl_assemble_kernel copies the chosen blocks (bfinal set on the last one).
+int ndfl_deflate_chunks_binsplit(ndfl_ctx* c, const uint8_t* hist, uint32_t hist_len, uint32_t hist_limit,
+                                 const uint8_t* data, uint64_t len, uint32_t chunk_len, const ndfl_strategy_desc* sub,
+                                 int32_t min_block_len, int final_flag, uint32_t start_bitpos, uint8_t* out,
+                                 uint64_t out_cap, uint64_t* out_end_bits, uint32_t* crc_inout, uint32_t flags) {
+    if (!c || !out_end_bits || (!data && len) || (!hist && hist_len) || !out || !sub) return NDFL_E_ARG;
+    if (min_block_len < 1) return NDFL_E_ARG;                                      // (:23-24)
+    if (start_bitpos > 7 || hist_limit > 32768 || hist_len > hist_limit || chunk_len == 0) return NDFL_E_ARG;
+    if (!final_flag && (len == 0 || len % chunk_len != 0)) return NDFL_E_ARG;
+    if (chunk_len > (uint32_t)MAX_CHUNK) return NDFL_E_UNSUPPORTED;
+    if (sub->kind != NDFL_KIND_LZ77) return NDFL_E_UNSUPPORTED;     // position-independent substrategies only
+    {
+        const ndfl_strategy_desc& d = *sub;
+        const bool lit = d.min_run == 0 && d.max_run == 0 && d.min_dist == 0 && d.max_dist == 0;
+        if (!lit && !(3 <= d.min_run && d.min_run <= d.max_run && d.max_run <= 258 && 1 <= d.min_dist &&
+                      d.min_dist <= d.max_dist && d.max_dist <= 32768))
+            return NDFL_E_ARG;
+    }
+    HIPCHK(hipSetDevice(c->device));
+    hipStream_t s = c->stream;
+    const uint32_t M = (uint32_t)min_block_len;
+    // device copy [hist | data]
+    HIPCHK(c->d_mdata.ensure(len + hist_len + 16));
+    const hipMemcpyKind kin = (flags & NDFL_IN_DEVICE) ? hipMemcpyDeviceToDevice : hipMemcpyHostToDevice;
+    if (hist_len) HIPCHK(hipMemcpyAsync(c->d_mdata.p, hist, hist_len, kin, s));
+    if (len) HIPCHK(hipMemcpyAsync(c->d_mdata.as<uint8_t>() + hist_len, data, len, kin, s));
+    const uint8_t* base = c->d_mdata.as<uint8_t>();            // base[hist_len + x] = data[x]
+    // uniform halving levels of a full chunk
+    std::vector<uint32_t> lv{chunk_len};
+    while (true) {
+        const uint32_t sz = lv.back();
+        if (!(sz / 2 > M)) break;                               // min((n+1)/2, n/2) > minBlockLen (:41-42)
+        if (sz & 1) return NDFL_E_UNSUPPORTED;                  // uneven halves: not on the GPU path
+        lv.push_back(sz / 2);
+    }
+    const uint32_t nlev = (uint32_t)lv.size();
+    if (nlev > 16) return NDFL_E_UNSUPPORTED;
+    const bool partial = final_flag && (len == 0 || len % chunk_len != 0);
+    const uint64_t nfull = len / chunk_len;
+    const uint64_t bound = ndfl_deflate_bound(len, chunk_len) + 64;
+    const uint64_t need_words = (bound + 3) / 4 + 4;
+    uint32_t* d_out;
+    const bool direct = (flags & NDFL_OUT_DEVICE) && (((uintptr_t)out & 3) == 0) && out_cap >= need_words * 4;
+    if (direct) d_out = (uint32_t*)out;
+    else { HIPCHK(c->d_out.ensure(need_words * 4)); d_out = c->d_out.as<uint32_t>(); }
+    HIPCHK(hipMemsetAsync(d_out, 0, need_words * 4, s));
+
+    // encode data [a, a + n) as blocks of `blk` into dst (device), block bits to `bits`.  `level`:
+    // a is a chunk boundary and the blocks' history starts at their chunk's (parent_len = chunk_len);
+    // otherwise one block whose history is that of the partial chunk starting at `pstart`
+    auto encode = [&](uint64_t a, uint64_t n, uint32_t blk, bool level, uint64_t pstart, bool fin, uint8_t* dst,
+                      uint64_t cap, uint64_t* d_bits, std::vector<uint64_t>& bits) -> int {
+        uint64_t hl, hlim;
+        if (level) {
+            hl = std::min<uint64_t>(hist_limit, hist_len + a);
+            hlim = hist_limit;
+            c->parent_len = chunk_len;
+        } else {
+            const uint64_t off = hist_len + pstart - std::min<uint64_t>(hist_limit, hist_len + pstart);   // in base
+            hl = std::min<uint64_t>(32768, hist_len + a - off);
+            hlim = hl;
+            c->parent_len = 0;
+        }
+        c->cb_out = d_bits;
+        uint64_t eb = 0;
+        const int rc = ndfl_deflate_chunks_lz77(c, base + hist_len + a - hl, (uint32_t)hl, (uint32_t)hlim,
+                                                base + hist_len + a, n, blk, sub->dynamic, sub->min_run,
+                                                sub->max_run, sub->min_dist, sub->max_dist, fin ? 1 : 0, 0, dst, cap,
+                                                &eb, nullptr, NDFL_IN_DEVICE | NDFL_OUT_DEVICE);
+        c->cb_out = nullptr;
+        c->parent_len = 0;
+        if (rc) return rc;
+        const uint64_t nb = n ? n / blk : 1;
+        bits.resize(nb);
+        HIPCHK(hipMemcpyAsync(bits.data(), d_bits, nb * 8, hipMemcpyDeviceToHost, s));
+        HIPCHK(hipStreamSynchronize(s));
+        return 0;
+    };
+    struct Ent { const uint32_t* st; uint64_t src, nb; uint8_t fin; };
+    uint64_t pos = start_bitpos;
+    // write a group of entries at pos (one assemble launch)
+    auto assemble = [&](std::vector<Ent>& ents) -> int {
+        const uint32_t ne = (uint32_t)ents.size();
+        if (ne == 0) return 0;
+        std::vector<uint64_t> src(ne), dst(ne), nb(ne);
+        std::vector<const uint32_t*> st(ne);
+        std::vector<uint8_t> fin(ne), ch(ne);
+        for (uint32_t k = 0; k < ne; k++) {
+            src[k] = ents[k].src; dst[k] = pos; nb[k] = ents[k].nb; st[k] = ents[k].st; fin[k] = ents[k].fin;
+            ch[k] = 0;
+            pos += ents[k].nb;
+        }
+        // per-entry stream pointers: one "substrategy" per entry (choice = 0 and streams + k)
+        const size_t tb = ne * 32ull + 2 * ne + 64;
+        HIPCHK(c->d_masm.ensure(tb));
+        char* bp = (char*)c->d_masm.p;
+        std::vector<char> host(tb);
+        memcpy(host.data(), src.data(), ne * 8ull);
+        memcpy(host.data() + ne * 8ull, dst.data(), ne * 8ull);
+        memcpy(host.data() + ne * 16ull, nb.data(), ne * 8ull);
+        memcpy(host.data() + ne * 24ull, st.data(), ne * 8ull);
+        memcpy(host.data() + ne * 32ull, fin.data(), ne);
+        memcpy(host.data() + ne * 32ull + ne, ch.data(), ne);
+        HIPCHK(hipMemcpyAsync(bp, host.data(), tb, hipMemcpyHostToDevice, s));
+        AsmArgs aa;
+        aa.data = nullptr; aa.n = 0; aa.chunk_len = 1; aa.nchunks = ne; aa.final_last = 0;
+        aa.src_bit = (const uint64_t*)bp; aa.dst_bit = (const uint64_t*)(bp + ne * 8ull);
+        aa.nbits = (const uint64_t*)(bp + ne * 16ull); aa.streams = (const uint32_t* const*)(bp + ne * 24ull);
+        aa.setfin = (const uint8_t*)(bp + ne * 32ull); aa.choice = (const uint8_t*)(bp + ne * 32ull + ne);
+        aa.per_entry_stream = 1;
+        aa.out = d_out;
+        hipLaunchKernelGGL(ndfl_assemble_kernel, dim3(ne), dim3(256), 0, s, aa);
+        HIPCHK(hipGetLastError());
+        HIPCHK(hipStreamSynchronize(s));
+        return 0;
+    };
+    // recursion of BinarySplit.decide (:33-66) on bit counts (position-independent substrategy)
+    std::vector<std::vector<uint64_t>> lb(nlev);
+    std::function<uint64_t(uint32_t, uint64_t, std::vector<std::pair<uint32_t, uint64_t>>&)> decide_lv =
+        [&](uint32_t k, uint64_t idx, std::vector<std::pair<uint32_t, uint64_t>>& leaves) -> uint64_t {
+            const uint64_t cur = lb[k][idx];
+            if (k + 1 < nlev) {
+                const uint64_t d0 = lb[k + 1][2 * idx], d1 = lb[k + 1][2 * idx + 1];
+                if (d0 + d1 < cur) {                            // improved: recurse into both halves
+                    std::vector<std::pair<uint32_t, uint64_t>> l2;
+                    const uint64_t t = decide_lv(k + 1, 2 * idx, l2) + decide_lv(k + 1, 2 * idx + 1, l2);
+                    if (t < cur) { leaves.insert(leaves.end(), l2.begin(), l2.end()); return t; }
+                }
+            }
+            leaves.push_back({k, idx});
+            return cur;
+        };
+    const uint32_t BCH = std::max<uint32_t>(1, (uint32_t)((64ull << 20) / chunk_len));
+    const bool last_is_full = !partial;
+    for (uint64_t cb = 0; cb < nfull; cb += BCH) {
+        const uint64_t ce = std::min<uint64_t>(nfull, cb + BCH);
+        const uint64_t a = cb * chunk_len, n = (ce - cb) * chunk_len;
+        std::vector<uint64_t> soff[16];
+        for (uint32_t k = 0; k < nlev; k++) {
+            const uint64_t capk = (ndfl_deflate_bound(n, lv[k]) + 3) / 4 * 4 + 64;
+            HIPCHK(c->d_mstreams[k].ensure(capk));
+            HIPCHK(c->d_mbits[k].ensure((n / lv[k]) * 8 + 64));
+            const int rc = encode(a, n, lv[k], true, 0, false, c->d_mstreams[k].as<uint8_t>(), capk,
+                                  c->d_mbits[k].as<uint64_t>(), lb[k]);
+            if (rc) return rc;
+            soff[k].resize(lb[k].size() + 1);
+            soff[k][0] = 0;
+            for (size_t q = 0; q < lb[k].size(); q++) soff[k][q + 1] = soff[k][q] + lb[k][q];
+        }
+        std::vector<Ent> ents;
+        for (uint64_t j = 0; j < ce - cb; j++) {
+            std::vector<std::pair<uint32_t, uint64_t>> leaves;
+            decide_lv(0, j, leaves);
+            for (auto& lf : leaves)
+                ents.push_back({c->d_mstreams[lf.first].as<uint32_t>(), soff[lf.first][lf.second], lb[lf.first][lf.second], 0});
+        }
+        if (ce == nfull && last_is_full && final_flag && !ents.empty()) ents.back().fin = 1;
+        const int rc = assemble(ents);
+        if (rc) return rc;
+    }
+    if (partial) {
+        const uint64_t P = nfull * chunk_len, lp = len - P;
+        std::vector<DevBuf> bufs;
+        int nenc = 0, err = 0;
+        std::vector<uint64_t> tmpbits;
+        HIPCHK(c->d_mbits[0].ensure(64));
+        // node [a, a+n): bits and the buffer holding its block (encoded once, kept for assembly)
+        std::map<std::pair<uint64_t, uint64_t>, std::pair<size_t, uint64_t>> memo;
+        auto node = [&](uint64_t a2, uint64_t n2) -> std::pair<size_t, uint64_t> {
+            auto it = memo.find({a2, n2});
+            if (it != memo.end()) return it->second;
+            if (++nenc > 8192) { err = NDFL_E_UNSUPPORTED; return {0, 0}; }
+            bufs.emplace_back();
+            const uint64_t capn = (ndfl_deflate_bound(n2, (uint32_t)std::max<uint64_t>(n2, 1)) + 3) / 4 * 4 + 64;
+            if (bufs.back().ensure(capn) != hipSuccess) { err = NDFL_E_DEVICE; return {0, 0}; }
+            const int rc = encode(P + (a2 - P), n2, (uint32_t)std::max<uint64_t>(n2, 1), false, P, n2 == 0,
+                                  bufs.back().as<uint8_t>(), capn, c->d_mbits[0].as<uint64_t>(), tmpbits);
+            if (rc) { err = rc; return {0, 0}; }
+            auto r = std::make_pair(bufs.size() - 1, tmpbits[0]);
+            memo[{a2, n2}] = r;
+            return r;
+        };
+        std::vector<std::pair<uint64_t, uint64_t>> leaves;     // (a, n)
+        std::function<uint64_t(uint64_t, uint64_t, std::vector<std::pair<uint64_t, uint64_t>>&)> decide_node =
+            [&](uint64_t a2, uint64_t n2, std::vector<std::pair<uint64_t, uint64_t>>& out_l) -> uint64_t {
+                const uint64_t cur = node(a2, n2).second;
+                const uint64_t h1 = (n2 + 1) / 2, h2 = n2 - h1;
+                if (!err && std::min(h1, h2) > M) {
+                    const uint64_t d0 = node(a2, h1).second, d1 = node(a2 + h1, h2).second;
+                    if (!err && d0 + d1 < cur) {
+                        std::vector<std::pair<uint64_t, uint64_t>> l2;
+                        const uint64_t t = decide_node(a2, h1, l2) + decide_node(a2 + h1, h2, l2);
+                        if (t < cur) { out_l.insert(out_l.end(), l2.begin(), l2.end()); return t; }
+                    }
+                }
+                out_l.push_back({a2, n2});
+                return cur;
+            };
+        decide_node(P, lp, leaves);
+        if (err) return err;
+        std::vector<Ent> ents;
+        for (auto& lf : leaves) {
+            auto nd = memo[lf];
+            ents.push_back({bufs[nd.first].as<uint32_t>(), 0, nd.second, 0});
+        }
+        if (!ents.empty() && lp > 0) ents.back().fin = 1;     // (an empty final block was encoded final)
+        const int rc = assemble(ents);
+        if (rc) return rc;
+    }
+    const uint64_t end_bits = pos;
+    *out_end_bits = end_bits;
+    if (crc_inout && len) {
+        uint32_t cr = *crc_inout;
+        const int rc = ndfl_crc32(c, &cr, base + hist_len, len, NDFL_IN_DEVICE);
         if (rc) return rc;
         *crc_inout = cr;
     }

@@ -53,7 +53,7 @@ constexpr int SCR_MASK = SCR_NXC + 16 * 4;          // u32[16][10] symbols-by-le
 constexpr int SCR_CLH = SCR_MASK + 16 * 10 * 4;     // u32[20] code-length histogram
 constexpr int SCR_MISC = SCR_CLH + 20 * 4;          // u32[16]
 constexpr int SCR_END = SCR_MISC + 16 * 4;
-static_assert(SCR_END <= OUTW * 4, "scratch must fit in the bit buffer");
+static_assert(2 * SCR_END <= OUTW * 4, "scratch (two package-merge problems) must fit in the bit buffer");
 
 struct Persist {
     uint32_t litCode[288];    // rev(code) | len << 16
@@ -82,6 +82,8 @@ struct Args {
     int32_t final_last;       // last chunk is bfinal
     int32_t rle;              // 1: RLE preset (dist 1, runs 3..258); 0: LITERAL preset
     int32_t dynamic;
+    uint32_t parent_len;      // history start rule: the chunk of this length containing the block
+                              // (BinarySplit sub-blocks, D/comp/BinarySplit.java:44-45); = chunk_len otherwise
     uint32_t base_bit;        // bit offset of chunk 0 in `out` (0..7)
     uint32_t* out;            // word-aligned output, words [0, ...)
     uint64_t* status;         // [nchunks], zeroed
@@ -108,8 +110,11 @@ __device__ __forceinline__ void run_sym(uint32_t run, uint32_t& sym, uint32_t& n
 }
 
 // ---- Package-merge code lengths (D/comp/Lz77Huffman.java:309-335) ---------------------------
-// hist: n entries (LDS).  Writes lens[0..n) (LDS, u8).  All threads must call.
-__device__ void pm_lengths(const uint32_t* hist, int n, int L, uint8_t* lens, char* s) {
+// hist: n entries (LDS).  Writes lens[0..n) (LDS, u8).  Every thread of the block must call (the
+// barriers are shared); thread `t` of the calling group works on this problem when `active`, so two
+// independent problems (literal/length and distance codes) run side by side on disjoint thread
+// ranges with their own scratch `s`.
+__device__ void pm_lengths(const uint32_t* hist, int n, int L, uint8_t* lens, char* s, int t, bool active) {
     uint32_t* key = (uint32_t*)(s + SCR_KEY);
     uint32_t* lf = (uint32_t*)(s + SCR_LF);
     uint32_t* ls = (uint32_t*)(s + SCR_LS);
@@ -118,45 +123,43 @@ __device__ void pm_lengths(const uint32_t* hist, int n, int L, uint8_t* lens, ch
     uint32_t* mf = (uint32_t*)(s + SCR_MF);
     uint32_t* mpk = (uint32_t*)(s + SCR_MPK);
     uint32_t* lvl = (uint32_t*)(s + SCR_LVL);
-    uint32_t* misc = (uint32_t*)(s + SCR_MISC);
-    const int tid = threadIdx.x;
-    if (tid < n) {
-        uint32_t f = hist[tid];
-        key[tid] = f ? (f << 9 | (uint32_t)tid) : 0xFFFFFFFFu;
+    if (active && t < n) {
+        uint32_t f = hist[t];
+        key[t] = f ? (f << 9 | (uint32_t)t) : 0xFFFFFFFFu;
     }
-    if (tid < 15 * 20) mpk[tid] = 0;
+    if (active && t < 15 * 20) mpk[t] = 0;
     __syncthreads();
     // leaves sorted by (freq, symbol): rank by counting (n <= 288, broadcast LDS reads)
     uint32_t nl = 0;
-    for (int j = 0; j < n; j++) nl += key[j] != 0xFFFFFFFFu;   // uniform
-    if (tid < n) {
-        uint32_t k = key[tid];
+    if (active) for (int j = 0; j < n; j++) nl += key[j] != 0xFFFFFFFFu;   // uniform per problem
+    if (active && t < n) {
+        uint32_t k = key[t];
         if (k != 0xFFFFFFFFu) {
             uint32_t r = 0;
             for (int j = 0; j < n; j++) r += key[j] < k;
             lf[r] = k >> 9;
-            ls[r] = (uint32_t)tid;
+            ls[r] = (uint32_t)t;
         }
-        lens[tid] = 0;
+        lens[t] = 0;
     }
     __syncthreads();
-    if (nl < 2) return;   // all zero lengths (callers never reach this for litlen/dist)
+    const bool work = active && nl >= 2;   // otherwise all zero lengths (callers never need this for litlen/dist)
     uint32_t np = 0;
     uint32_t* pf = pfA;
     uint32_t* pfn = pfB;
     for (int it = 0; it < L; it++) {
         const uint32_t m = np + nl;
-        if ((uint32_t)tid < m) {
+        if (work && (uint32_t)t < m) {
             uint32_t f, pos;
-            bool isp = (uint32_t)tid < np;
+            bool isp = (uint32_t)t < np;
             if (isp) {
-                f = pf[tid];
+                f = pf[t];
                 // # leaves with freq < f
                 uint32_t lo = 0, hi = nl;
                 while (lo < hi) { uint32_t mid = (lo + hi) >> 1; if (lf[mid] < f) lo = mid + 1; else hi = mid; }
-                pos = (uint32_t)tid + lo;
+                pos = (uint32_t)t + lo;
             } else {
-                uint32_t r = (uint32_t)tid - np;
+                uint32_t r = (uint32_t)t - np;
                 f = lf[r];
                 // # packages with freq <= f
                 uint32_t lo = 0, hi = np;
@@ -168,35 +171,37 @@ __device__ void pm_lengths(const uint32_t* hist, int n, int L, uint8_t* lens, ch
         }
         __syncthreads();
         const uint32_t np2 = m >> 1;
-        if ((uint32_t)tid < np2) pfn[tid] = mf[2 * tid] + mf[2 * tid + 1];
+        if (work && (uint32_t)t < np2) pfn[t] = mf[2 * t] + mf[2 * t + 1];
         __syncthreads();
         np = np2;
-        uint32_t* t = pf; pf = pfn; pfn = t;
+        uint32_t* tmp = pf; pf = pfn; pfn = tmp;
     }
     // backtrack: prefix of 2(nl-1) items at the last level; leaves in the prefix of each level.
-    if (tid < 64) {
+    if (work && t < 64) {
         uint32_t m = 2 * (nl - 1);
         for (int it = L - 1; it >= 0; it--) {
             uint32_t cnt = 0;
-            if (tid < 20) {
-                uint32_t w = mpk[it * 20 + tid];
-                uint32_t lo = (uint32_t)tid * 32;
+            if (t < 20) {
+                uint32_t w = mpk[it * 20 + t];
+                uint32_t lo = (uint32_t)t * 32;
                 if (lo + 32 <= m) cnt = __popc(w);
                 else if (lo < m) cnt = __popc(w & ((1u << (m - lo)) - 1));
             }
             cnt = wave_sum(cnt);
-            if (tid == 0) lvl[it] = m - cnt;
+            if (t == 0) lvl[it] = m - cnt;
             m = 2 * cnt;
         }
     }
     __syncthreads();
-    if ((uint32_t)tid < nl) {
+    if (work && (uint32_t)t < nl) {
         uint32_t c = 0;
-        for (int it = 0; it < L; it++) c += (uint32_t)tid < lvl[it];
-        lens[ls[tid]] = (uint8_t)c;
+        for (int it = 0; it < L; it++) c += (uint32_t)t < lvl[it];
+        lens[ls[t]] = (uint8_t)c;
     }
-    (void)misc;
     __syncthreads();
+}
+__device__ __forceinline__ void pm_lengths(const uint32_t* hist, int n, int L, uint8_t* lens, char* s) {
+    pm_lengths(hist, n, L, lens, s, (int)threadIdx.x, true);
 }
 
 // Canonical codes (D/comp/Lz77Huffman.java:368-391): rev(code) | len << 16.
@@ -302,9 +307,13 @@ __device__ __forceinline__ void build_block_codes(bool dynamic, char* scr, Persi
         __syncthreads();
         const int ln = (int)misc[0], dn = (int)misc[1];
         const bool emptyDist = misc[2] != 0;
-        pm_lengths(hlit, ln, 15, lens, scr);
-        if (emptyDist) { if (tid == 0) lens[ln] = 0; __syncthreads(); }
-        else pm_lengths(hdist, dn, 15, lens + ln, scr);
+        // literal/length and distance lengths side by side: threads [0, 640) and [640, 1024)
+        if (emptyDist && tid == 0) lens[ln] = 0;
+        {
+            const bool isLit = tid < 640;
+            pm_lengths(isLit ? hlit : hdist, isLit ? ln : dn, 15, isLit ? lens : lens + ln,
+                       isLit ? scr : scr + SCR_END, isLit ? tid : tid - 640, isLit || !emptyDist);
+        }
         canon_codes(lens, ln, ps.litCode, scr);
         canon_codes(lens + ln, dn, ps.distCode, scr);
         // code-length sequence RLE (:187-223) as maximal-run decomposition
@@ -571,7 +580,8 @@ ndfl_deflate_chunks_kernel(Args a) {
 
     const uint64_t tp1 = wall_clock64();
     // ---- 2. run pieces ------------------------------------------------------------------------
-    const bool has_prev0 = (c > 0) ? (a.hist_enabled != 0) : (a.prev_byte >= 0);
+    // a block inside its parent chunk always has the parent's earlier bytes as history
+    const bool has_prev0 = (cs % a.parent_len != 0) ? true : (c > 0) ? (a.hist_enabled != 0) : (a.prev_byte >= 0);
     const uint32_t prev0 = (c > 0) ? (uint32_t)src[-1] : (uint32_t)(a.prev_byte & 0xFF);
     uint64_t F = 0;
     if (vcnt > 0) {

@@ -36,6 +36,7 @@ struct LzArgs {
     uint64_t total;           // LZ_DS + n
     uint64_t vstart;          // LZ_DS - H: first valid history byte
     uint32_t chunk_len;
+    uint32_t parent_len;      // history start from the chunk of this length (BinarySplit sub-blocks)
     uint32_t hist_limit;
     uint32_t min_run, max_run, min_dist, max_dist;
     const uint16_t* link;     // link[q - L0]
@@ -159,8 +160,8 @@ ndfl_lz_match_kernel(LzArgs a) {
                 const uint64_t cs = LZ_DS + c * a.chunk_len;
                 const uint64_t e = min(cs + a.chunk_len, a.total);
                 maxlen = (uint32_t)min((uint64_t)maxRun, e - i);
-                const uint64_t avail = cs - a.vstart;           // history bytes before the chunk
-                const uint64_t off = cs - min((uint64_t)a.hist_limit, avail);
+                const uint64_t ps = LZ_DS + (x / a.parent_len) * a.parent_len;   // parent chunk start
+                const uint64_t off = ps - min((uint64_t)a.hist_limit, ps - a.vstart);
                 const int64_t lo = max((int64_t)i - (int64_t)a.max_dist, (int64_t)off);
                 const int64_t hi = (int64_t)i - (int64_t)a.min_dist;
                 ri = (uint32_t)((int64_t)i - wb0);

@@ -25,9 +25,11 @@ struct AsmArgs {
     uint32_t nchunks;
     int32_t final_last;
     const uint8_t* choice;           // per chunk: substrategy index
-    const uint64_t* src_bit;         // per chunk: bit offset of its block in the chosen stream
+    const uint64_t* src_bit;         // per chunk (entry): bit offset of its block in the chosen stream
     const uint64_t* dst_bit;         // per chunk: global output bit offset
     const uint64_t* nbits;           // per chunk: bits
+    const uint8_t* setfin;           // optional per entry: set the block's bfinal bit (its first bit)
+    int32_t per_entry_stream;        // 1: streams[] has one pointer per entry (choice ignored)
     uint32_t* out;                   // zeroed, word-aligned
 };
 
@@ -37,7 +39,7 @@ extern "C" __global__ void __launch_bounds__(256)
 ndfl_assemble_kernel(AsmArgs a) {
     const uint32_t c = blockIdx.x;
     const uint64_t d = a.dst_bit[c], L = a.nbits[c];
-    const uint32_t* src = a.streams[a.choice[c]];
+    const uint32_t* src = a.per_entry_stream ? a.streams[c] : a.streams[a.choice[c]];
     if (src == nullptr) {
         // stored blocks (D/comp/Uncompressed.java:33-46): bfinal, btype 00, zero pad to a byte,
         // LEN, NLEN, bytes; only the first block can start inside a byte
@@ -72,6 +74,7 @@ ndfl_assemble_kernel(AsmArgs a) {
     const uint64_t s = a.src_bit[c];
     const uint64_t w0 = d >> 5, w1 = (d + L - 1) >> 5;
     if (L == 0) return;
+    if (a.setfin && a.setfin[c] && threadIdx.x == 0) atomicOr(&a.out[d >> 5], 1u << (d & 31));
     for (uint64_t w = w0 + threadIdx.x; w <= w1; w += 256) {
         // dst bits [32w, 32w+32) <- src bits from q = s + (32w - d)
         const int64_t q = (int64_t)s + (int64_t)(32 * w) - (int64_t)d;

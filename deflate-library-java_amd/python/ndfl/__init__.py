@@ -19,7 +19,7 @@ import io
 from . import _lib
 from ._lib import IN_DEVICE, OUT_DEVICE, DICT_DEFERRED, NO_END, STRATEGIES, NdflError, check, load, reason_name
 
-__all__ = ["Context", "Reason", "DataFormatException", "Lz77Huffman", "Uncompressed", "MultiStrategy", "DeflaterOutputStream", "InflaterInputStream",
+__all__ = ["Context", "Reason", "DataFormatException", "Lz77Huffman", "Uncompressed", "MultiStrategy", "BinarySplit", "DeflaterOutputStream", "InflaterInputStream",
            "GzipMetadata", "GzipOutputStream", "GzipInputStream", "ZlibMetadata", "ZlibOutputStream",
            "ZlibInputStream", "Strategy", "default_context", "compress", "decompress", "crc32_combine"]
 
@@ -131,6 +131,20 @@ class MultiStrategy:
         self.substrategies = tuple(strats)
 
 
+class BinarySplit:
+    """BinarySplit(strat, minBlockLen) (D/comp/BinarySplit.java:15-82): halve each chunk recursively
+    while both halves exceed minBlockLen, keeping a split when it takes fewer bits.  On the GPU path
+    the substrategy must be an Lz77Huffman."""
+
+    def __init__(self, strat, minBlockLen):
+        if strat is None:
+            raise TypeError("strat")
+        if minBlockLen < 1:
+            raise ValueError("Non-positive minimum block length")
+        self.substrategy = strat
+        self.minimumBlockLength = int(minBlockLen)
+
+
 def _desc(st):
     d = _lib.StrategyDesc()
     if isinstance(st, _UncompressedType):
@@ -195,7 +209,13 @@ class Context:
         endbits = ctypes.c_uint64(0)
         crcv = ctypes.c_uint32(crc if crc is not None else 0)
         crcp = ctypes.byref(crcv) if crc is not None else None
-        if isinstance(strategy, (MultiStrategy, _UncompressedType)):
+        if isinstance(strategy, BinarySplit):
+            d = _desc(strategy.substrategy)
+            r = L.ndfl_deflate_chunks_binsplit(self._h, hist_addr, hist_len, hist_limit, data_addr, n, chunk_len,
+                                               ctypes.byref(d), strategy.minimumBlockLength, int(final), start_bitpos,
+                                               out_addr, out_cap, ctypes.byref(endbits), crcp, flags)
+            check(r, "ndfl_deflate_chunks_binsplit")
+        elif isinstance(strategy, (MultiStrategy, _UncompressedType)):
             subs = strategy.substrategies if isinstance(strategy, MultiStrategy) else (strategy,)
             arr = (_lib.StrategyDesc * len(subs))(*[_desc(x) for x in subs])
             r = L.ndfl_deflate_chunks_multi(self._h, hist_addr, hist_len, hist_limit, data_addr, n, chunk_len, arr,
@@ -289,7 +309,7 @@ class Context:
 
 
 def _strategy_id(s):
-    if isinstance(s, (Lz77Huffman, MultiStrategy, _UncompressedType)):
+    if isinstance(s, (Lz77Huffman, MultiStrategy, _UncompressedType, BinarySplit)):
         return s
     if isinstance(s, Strategy):
         return s.value

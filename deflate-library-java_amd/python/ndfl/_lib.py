@@ -30,7 +30,8 @@ E_ARG, E_UNSUPPORTED, E_CAPACITY, E_DEVICE, E_STATE, E_INTERNAL = -1, -2, -3, -4
 # Every symbol include/ndfl.h declares (checked by tests/test_capi_symbols.py).
 EXPORTS = ["ndfl_abi_version", "ndfl_error_string", "ndfl_ctx_create", "ndfl_ctx_destroy",
            "ndfl_ctx_set_stream", "ndfl_ctx_last_kernel_ms", "ndfl_ctx_timings", "ndfl_deflate_chunks",
-           "ndfl_deflate_chunks_lz77", "ndfl_deflate_chunks_multi", "ndfl_deflate_bound",
+           "ndfl_deflate_chunks_lz77", "ndfl_deflate_chunks_multi", "ndfl_deflate_chunks_binsplit",
+           "ndfl_deflate_bound",
            "ndfl_inflate", "ndfl_inflate_range", "ndfl_inflate_resolve", "ndfl_bits_shift", "ndfl_crc32", "ndfl_adler32",
            "ndfl_crc32_combine"]
 
@@ -69,6 +70,8 @@ def load():
                                            u64, ctypes.POINTER(u64), ctypes.POINTER(u32), u32]
     L.ndfl_deflate_chunks_multi.argtypes = [vp, vp, u32, u32, vp, u64, u32, ctypes.POINTER(StrategyDesc), u32, i32,
                                             u32, vp, u64, ctypes.POINTER(u64), ctypes.POINTER(u32), u32]
+    L.ndfl_deflate_chunks_binsplit.argtypes = [vp, vp, u32, u32, vp, u64, u32, ctypes.POINTER(StrategyDesc), i32,
+                                               i32, u32, vp, u64, ctypes.POINTER(u64), ctypes.POINTER(u32), u32]
     L.ndfl_deflate_bound.restype = u64
     L.ndfl_deflate_bound.argtypes = [u64, u32]
     L.ndfl_inflate.argtypes = [vp, vp, u64, vp, u64, ctypes.POINTER(u64), ctypes.POINTER(u64), u32]

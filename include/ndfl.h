@@ -129,6 +129,18 @@ int ndfl_deflate_chunks_multi(ndfl_ctx* ctx, const uint8_t* hist, uint32_t hist_
                               uint32_t n_strats, int final_flag, uint32_t start_bitpos, uint8_t* out,
                               uint64_t out_cap, uint64_t* out_end_bits, uint32_t* crc_inout, uint32_t flags);
 
+/*
+ * Same as ndfl_deflate_chunks for BinarySplit(sub, minBlockLen) (D/comp/BinarySplit.java:21-82) over
+ * an Lz77Huffman substrategy: each chunk halves recursively while both halves exceed
+ * min_block_len (>= 1, else NDFL_E_ARG), keeping a split when it takes fewer bits; the sub-blocks'
+ * history starts at their chunk's.  NDFL_E_UNSUPPORTED for other substrategies, for halvings of
+ * an odd length inside full chunks, or for more than 8192 node encodes in a partial final chunk.
+ */
+int ndfl_deflate_chunks_binsplit(ndfl_ctx* ctx, const uint8_t* hist, uint32_t hist_len, uint32_t hist_limit,
+                                 const uint8_t* data, uint64_t len, uint32_t chunk_len, const ndfl_strategy_desc* sub,
+                                 int32_t min_block_len, int final_flag, uint32_t start_bitpos, uint8_t* out,
+                                 uint64_t out_cap, uint64_t* out_end_bits, uint32_t* crc_inout, uint32_t flags);
+
 /* Upper bound of output bytes of ndfl_deflate_chunks for `len` bytes. */
 uint64_t ndfl_deflate_bound(uint64_t len, uint32_t chunk_len);
 

@@ -549,6 +549,107 @@ int64_t or_deflate_multi(const uint8_t* data, uint64_t len, uint32_t chunk_len, 
     return (int64_t)w.n;
 }
 
+/* BinarySplit(sub, minBlockLen).decide/compressTo (D/comp/BinarySplit.java:21-82), with the
+ * reference's loop as written: the split's bit length is accumulated from position 0 whatever the
+ * starting position i (:45-50, :56-63).  sub: {kind, dynamic, minRun, maxRun, minDist, maxDist}. */
+typedef struct bs_dec {
+    int64_t hl, dl;                       /* data = b[hl, hl + dl) relative to the chunk's off */
+    int64_t bits[8];
+    struct bs_dec* pick[8][2];            /* NULL: the substrategy's own decision for the range */
+    struct bs_dec* own[2];                /* children owned by this node */
+} bs_dec;
+
+static void bs_leaf_bits(const uint8_t* b, int64_t hl, int64_t dl, const int32_t* d, const lz_params* P, int64_t out[8]) {
+    if (d[0] == 1) {
+        int64_t nblk = (dl + 65534) / 65535; if (nblk < 1) nblk = 1;
+        for (int i = 0; i < 8; i++) out[i] = dl * 8 + nblk * 40 + ((13 - i) % 8 - 5);
+    } else {
+        sink_t cnt = { NULL, 0 };
+        lz_compress(b, 0, hl, dl, P, 0, &cnt, 0);
+        for (int i = 0; i < 8; i++) out[i] = (int64_t)cnt.count;
+    }
+}
+
+static bs_dec* bs_new_leaf(const uint8_t* b, int64_t hl, int64_t dl, const int32_t* d, const lz_params* P) {
+    bs_dec* x = (bs_dec*)calloc(1, sizeof(bs_dec));
+    x->hl = hl; x->dl = dl;
+    bs_leaf_bits(b, hl, dl, d, P, x->bits);
+    return x;
+}
+
+static void bs_free(bs_dec* x) {
+    if (!x) return;
+    bs_free(x->own[0]); bs_free(x->own[1]);
+    free(x);
+}
+
+/* decide(b, off, historyLen, dataLen, curDec) (:33-66); `cur` becomes the returned node. */
+static bs_dec* bs_decide(const uint8_t* b, bs_dec* cur, const int32_t* d, const lz_params* P, int64_t M) {
+    int64_t first = (cur->dl + 1) / 2, second = cur->dl - first;
+    if ((first < second ? first : second) > M) {
+        bs_dec* sp[2] = { bs_new_leaf(b, cur->hl, first, d, P), bs_new_leaf(b, cur->hl + first, second, d, P) };
+        int improved = 0;
+        for (int i = 0; i < 8; i++) {
+            int64_t bl = 0;
+            for (int k = 0; k < 2; k++) bl += sp[k]->bits[bl % 8];
+            improved |= bl < cur->bits[i];
+        }
+        if (improved) { sp[0] = bs_decide(b, sp[0], d, P, M); sp[1] = bs_decide(b, sp[1], d, P, M); }
+        int used = 0;
+        for (int i = 0; i < 8; i++) {
+            int64_t bl = 0;
+            for (int k = 0; k < 2; k++) bl += sp[k]->bits[bl % 8];
+            if (bl < cur->bits[i]) { cur->bits[i] = bl; cur->pick[i][0] = sp[0]; cur->pick[i][1] = sp[1]; used = 1; }
+        }
+        cur->own[0] = sp[0]; cur->own[1] = sp[1];
+        (void)used;
+    }
+    return cur;
+}
+
+static void bs_emit(const uint8_t* b, const bs_dec* x, const int32_t* d, const lz_params* P, int isFinal, sink_t* sk) {
+    const int pos = sk_pos(sk);
+    if (x->pick[pos][0]) {
+        bs_emit(b, x->pick[pos][0], d, P, 0, sk);
+        bs_emit(b, x->pick[pos][1], d, P, isFinal, sk);
+    } else if (d[0] == 1) {
+        unc_compress(b, 0, x->hl, x->dl, isFinal, sk);
+    } else {
+        lz_compress(b, 0, x->hl, x->dl, P, isFinal, sk, 0);
+    }
+}
+
+int64_t or_deflate_binsplit(const uint8_t* data, uint64_t len, uint32_t chunk_len, uint32_t hist_limit,
+                            const int32_t* desc, int32_t min_block_len, uint8_t* out, uint64_t out_cap) {
+    if (chunk_len < 1 || hist_limit > 32768 || min_block_len < 1) return OR_ERR_ARG;
+    lz_params P = {0, 0, 0, 0, 0};
+    if (desc[0] == 0) {
+        if (!(desc[2] == 0 && desc[3] == 0 && desc[4] == 0 && desc[5] == 0) &&
+            !(3 <= desc[2] && desc[2] <= desc[3] && desc[3] <= 258 && 1 <= desc[4] && desc[4] <= desc[5] && desc[5] <= 32768))
+            return OR_ERR_ARG;
+        lz_params q = {desc[1] ? 1 : 0, desc[2], desc[3], desc[4], desc[5]};
+        P = q;
+    } else if (desc[0] != 1) return OR_ERR_ARG;
+    bw_t w = {out, out_cap, 0, 0, 0, 0};
+    uint64_t pos = 0;
+    for (;;) {
+        uint64_t dlen = len - pos; int fin = 1;
+        if (dlen > chunk_len) { dlen = chunk_len; fin = 0; }
+        else if (dlen == chunk_len && pos + dlen < len) fin = 0;
+        uint64_t hlen = pos < hist_limit ? pos : hist_limit;
+        const uint8_t* base = data + (pos - hlen);
+        bs_dec* root = bs_decide(base, bs_new_leaf(base, (int64_t)hlen, (int64_t)dlen, desc, &P), desc, &P, min_block_len);
+        sink_t sk = { &w, 0 };
+        bs_emit(base, root, desc, &P, fin, &sk);
+        bs_free(root);
+        pos += dlen;
+        if (fin) break;
+    }
+    bw_finish(&w);
+    if (w.overflow) return OR_ERR_CAPACITY;
+    return (int64_t)w.n;
+}
+
 int64_t or_deflate_block_bits(const uint8_t* data, uint64_t len, uint32_t chunk_len, uint32_t hist_limit,
                               int strategy, uint64_t* bits, uint64_t cap) {
     if (strategy < 0 || strategy > 6) return OR_ERR_ARG;

@@ -61,6 +61,11 @@ int64_t or_deflate_lz(const uint8_t* data, uint64_t len, uint32_t chunk_len, uin
 int64_t or_deflate_multi(const uint8_t* data, uint64_t len, uint32_t chunk_len, uint32_t hist_limit,
                          const int32_t* desc, uint32_t n, uint8_t* out, uint64_t out_cap);
 
+/* BinarySplit(sub, minBlockLen) (D/comp/BinarySplit.java:21-82) driven like DeflaterOutputStream;
+ * desc = {kind (0 Lz77Huffman, 1 Uncompressed), dynamic, minRun, maxRun, minDist, maxDist}. */
+int64_t or_deflate_binsplit(const uint8_t* data, uint64_t len, uint32_t chunk_len, uint32_t hist_limit,
+                            const int32_t* desc, int32_t min_block_len, uint8_t* out, uint64_t out_cap);
+
 /* Per-chunk bit sizes of the default encode (for GPU parity of block boundaries).  Writes
  * number of chunks to *nchunks and each chunk's block bit length into bits[] (cap entries). */
 int64_t or_deflate_block_bits(const uint8_t* data, uint64_t len, uint32_t chunk_len, uint32_t hist_limit,

@@ -59,6 +59,9 @@ def lib():
         L.or_deflate_multi.restype = ctypes.c_int64
         L.or_deflate_multi.argtypes = [u8p, ctypes.c_uint64, ctypes.c_uint32, ctypes.c_uint32, ctypes.c_void_p,
                                        ctypes.c_uint32, u8p, ctypes.c_uint64]
+        L.or_deflate_binsplit.restype = ctypes.c_int64
+        L.or_deflate_binsplit.argtypes = [u8p, ctypes.c_uint64, ctypes.c_uint32, ctypes.c_uint32, ctypes.c_void_p,
+                                          ctypes.c_int32, u8p, ctypes.c_uint64]
         L.or_deflate_block_bits.restype = ctypes.c_int64
         L.or_deflate_block_bits.argtypes = [u8p, ctypes.c_uint64, ctypes.c_uint32, ctypes.c_uint32,
                                             ctypes.c_int, ctypes.POINTER(ctypes.c_uint64), ctypes.c_uint64]
@@ -134,6 +137,19 @@ def deflate_multi(data, subs, chunk_len=65536, hist_limit=32768):
     r = lib().or_deflate_multi(src, n, chunk_len, hist_limit, arr, len(subs), out, cap)
     if r < 0:
         raise ValueError(f"or_deflate_multi failed: {r}")
+    return out.raw[:r]
+
+
+def deflate_binsplit(data, sub, min_block_len, chunk_len=65536, hist_limit=32768):
+    """BinarySplit(sub, minBlockLen): sub is "UNCOMPRESSED" or (dynamic, minRun, maxRun, minDist, maxDist)."""
+    src, n = _buf(data)
+    flat = [1, 0, 0, 0, 0, 0] if sub == "UNCOMPRESSED" else [0] + [int(x) for x in sub]
+    arr = (ctypes.c_int32 * 6)(*flat)
+    cap = deflate_bound(n, chunk_len) * 2 + 4096
+    out = ctypes.create_string_buffer(cap)
+    r = lib().or_deflate_binsplit(src, n, chunk_len, hist_limit, arr, min_block_len, out, cap)
+    if r < 0:
+        raise ValueError(f"or_deflate_binsplit failed: {r}")
     return out.raw[:r]
 
 

@@ -316,3 +316,74 @@ def deflate_multi(data, subs, chunk_len=65536, hist_limit=32768):
         if final:
             break
     return w.getbytes()
+
+
+class _Leaf:
+    """The substrategy's own decision over buf[hl, hl + dl); lengths measured by writing."""
+
+    def __init__(self, buf, hl, dl, sub):
+        self.buf, self.hl, self.dl, self.sub = buf, hl, dl, sub
+        self.bits = []
+        for pos in range(8):
+            t = BitWriter()
+            t.n = pos
+            self.emit(t, False)
+            self.bits.append(t.n - pos)
+
+    def emit(self, w, final):
+        if self.sub == "UNCOMPRESSED":
+            stored_blocks(w, self.buf[self.hl:self.hl + self.dl], final)
+        else:
+            compress_block(w, self.buf[:self.hl + self.dl], self.hl, self.dl, tuple(self.sub), final)
+
+
+class _Split:
+    def __init__(self, bits, picks):
+        self.bits, self.picks = bits, picks
+
+    def emit(self, w, final):
+        decs = self.picks[w.n % 8]
+        for j, d in enumerate(decs):
+            d.emit(w, final and j == len(decs) - 1)
+
+
+def _bs_decide(buf, hl, dl, sub, m, cur):
+    """BinarySplit.decide (D/comp/BinarySplit.java:33-66) restated; the split length is accumulated
+    from position 0 for every starting position, as the reference's loops do."""
+    bits = list(cur.bits)
+    picks = [[cur] for _ in range(8)]
+    first = (dl + 1) // 2
+    second = dl - first
+    if min(first, second) > m:
+        sp = [_Leaf(buf, hl, first, sub), _Leaf(buf, hl + first, second, sub)]
+
+        def total(decs):
+            bl = 0
+            for d in decs:
+                bl += d.bits[bl % 8]
+            return bl
+        improved = any(total(sp) < bits[i] for i in range(8))
+        if improved:
+            sp = [_bs_decide(buf, hl, first, sub, m, sp[0]), _bs_decide(buf, hl + first, second, sub, m, sp[1])]
+        t = total(sp)
+        for i in range(8):
+            if t < bits[i]:
+                bits[i] = t
+                picks[i] = sp
+    return _Split(bits, picks)
+
+
+def deflate_binsplit(data, sub, min_block_len, chunk_len=65536, hist_limit=32768):
+    w = BitWriter()
+    pos = 0
+    n = len(data)
+    while True:
+        dlen = min(n - pos, chunk_len)
+        final = pos + dlen >= n
+        hlen = min(pos, hist_limit)
+        buf = data[pos - hlen: pos + dlen]
+        _bs_decide(buf, hlen, dlen, sub, min_block_len, _Leaf(buf, hlen, dlen, sub)).emit(w, final)
+        pos += dlen
+        if final:
+            break
+    return w.getbytes()

@@ -94,3 +94,39 @@ def test_multistrategy_validation(ndfl):
         ndfl.MultiStrategy()
     with pytest.raises(TypeError):
         ndfl.MultiStrategy(None)
+
+
+@pytest.mark.parametrize("name,m", [("RLE_DYNAMIC", 1024), ("FULL_DYNAMIC", 4096), ("LITERAL_STATIC", 64),
+                                    ("RLE_STATIC", 30000)])
+def test_binarysplit_matches_oracle(ndfl, ctx, name, m):
+    strat = ndfl.BinarySplit(ndfl.Lz77Huffman(*PR[name]), m)
+    for data in inputs(24)[::2] + [inputs(25)[-1] * 3]:
+        for chunk_len, hist in [(65536, 32768), (65536, 0), (8192, 100)]:
+            got = ctx.deflate(data, strat, chunk_len=chunk_len, hist_limit=hist)
+            exp = O.deflate_binsplit(data, PR[name], m, chunk_len, hist)
+            assert got == exp, (name, m, len(data), chunk_len, hist)
+            reason, out, _ = ctx.inflate(got)
+            assert reason is None and out == data
+
+
+def test_binarysplit_stream_batches(ndfl, ctx):
+    rng = random.Random(26)
+    strat = ndfl.BinarySplit(ndfl.Lz77Huffman.RLE_DYNAMIC, 2048)
+    for _ in range(4):
+        data = b"".join(inputs(rng.randrange(100))[rng.randrange(8, 24)] for _ in range(3))
+        bout = io.BytesIO()
+        d = ndfl.DeflaterOutputStream(bout, strategy=strat, context=ctx, batch_bytes=rng.choice([1, 65537, 300_000]))
+        off = 0
+        while off < len(data):
+            n = rng.randrange(1, min(90_000, len(data) - off) + 1)
+            d.write(data, off, n)
+            off += n
+        d.finish()
+        assert bout.getvalue() == O.deflate_binsplit(data, PR["RLE_DYNAMIC"], 2048)
+
+
+def test_binarysplit_validation(ndfl):
+    with pytest.raises(ValueError):
+        ndfl.BinarySplit(ndfl.Lz77Huffman.RLE_DYNAMIC, 0)
+    with pytest.raises(TypeError):
+        ndfl.BinarySplit(None, 5)

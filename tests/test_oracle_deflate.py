@@ -152,3 +152,20 @@ def test_uncompressed_preset_equals_single_multistrategy():
     for data in samples(4)[:10]:
         assert O.deflate(data, "UNCOMPRESSED") == O.deflate_multi(data, ["UNCOMPRESSED"])
         assert O.deflate(data, "RLE_DYNAMIC") == O.deflate_multi(data, [P.PRESETS["RLE_DYNAMIC"]])
+
+
+@pytest.mark.parametrize("sub", [P.PRESETS["RLE_DYNAMIC"], P.PRESETS["FULL_STATIC"], P.PRESETS["LITERAL_DYNAMIC"],
+                                 "UNCOMPRESSED"])
+def test_nversion_binarysplit(sub):
+    """BinarySplit: oracle against pyref (lengths measured by writing, the reference's position-0
+    accumulation kept in both) and round trips."""
+    rng = random.Random(60)
+    datas = samples(5)[:14] + [bytes(rng.randrange(256) for _ in range(3000)) + b"\x00" * 3000]
+    for data in datas:
+        for chunk_len, hist, m in [(65536, 32768, 64), (700, 32768, 50), (1024, 0, 100), (300, 10, 1)]:
+            if sub != "UNCOMPRESSED" and sub[4] > 1 and len(data) > 2000:
+                continue
+            a = O.deflate_binsplit(data, sub, m, chunk_len, hist)
+            b = P.deflate_binsplit(data, sub, m, chunk_len, hist)
+            assert a == b, (sub, len(data), chunk_len, hist, m)
+            assert zlib.decompress(a, -15) == data
