@@ -826,11 +826,6 @@ static int inflate_run(InflateScratch& S, hipStream_t s, const uint8_t* in, uint
     S.pool = pool;
     INF_CHK(hipMemsetAsync(pool.head, 0xFF, nslot * 4, s));
 
-    auto next_after = [&](uint64_t b) -> uint64_t {
-        auto ub = std::upper_bound(sorted_cand.begin(), sorted_cand.end(), b);
-        const uint64_t nx = ub != sorted_cand.end() ? *ub : NONE;
-        return std::min(nx, end_bit);
-    };
     static const bool stats_on = getenv("NDFL_STATS") != nullptr;
     std::vector<ChainRes> res;
     auto run_count = [&](const std::vector<uint64_t>& st, std::vector<ChainRes>& r) -> int {

@@ -16,9 +16,9 @@
 //     symbol or an error ends the block; when no lane does (the segment end was a false header
 //     candidate), the next round continues from lane 63's exit.
 //   * count pass: output bytes, end bit, status per chain (the host links chains);
-//     emit pass: a third decode per segment writes the output at its offset.  A copy whose source
-//     lies in an earlier lane's segment waits (per-step progress counters in LDS); a source in an
-//     earlier chain waits on that chain's done flag, as before.
+//     emit pass: a third decode per segment writes the output at its offset.  No lane or chain
+//     waits on another: copies whose source is not yet known there are deferred (back-references
+//     + pending bits) and resolved afterwards by pointer-jumping rounds.
 // Many waves per CU (small LDS footprint) hide the per-token latency chain.
 #pragma once
 
@@ -779,7 +779,7 @@ struct WLane {
     uint32_t q0, q1, q2, q3, qn, lastqw;
     uint64_t qaddr;             // byte address of q0
     uint32_t kind, reason;      // final state (T_ERR also for COPY_BEFORE found here)
-    bool active, tainted;
+    bool active;
 };
 
 __device__ __forceinline__ void wq_flush(WLane& L, gu8* out) {
