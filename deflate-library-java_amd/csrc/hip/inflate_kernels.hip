@@ -704,7 +704,7 @@ static int resolve_rounds(InflateScratch& S, hipStream_t s, uint8_t* d_out, uint
             if (rstats) fprintf(stderr, "[ndfl] resolve round %d: %u pending groups, %u bytes\n", round, n, h[1]);
             if (round == 0) *groups = n;
             if (n == 0) return 0;
-            if (round >= 48) return R_INTERNAL;              // distances double each round: unreachable
+            if (round >= 96) return R_INTERNAL;              // distances double each round: unreachable
         }
         INF_CHK(hipMemsetAsync(cnt + (cur ^ 1), 0, 4, s));
         if (rstats) INF_CHK(hipMemsetAsync(cnt + 2 + (cur ^ 1), 0, 4, s));
@@ -990,7 +990,7 @@ static int inflate_run(InflateScratch& S, hipStream_t s, const uint8_t* in, uint
         if (dict_len) INF_CHK(hipMemcpyAsync(d_out, out, dict_len, hipMemcpyHostToDevice, s));
     }
     const uint64_t nbytes = dict_len + total;
-    if (nbytes > (1ull << 32)) return -2;                    // u32 back-references (indices < 2^32)
+    if ((nbytes + 31) / 32 > 0xFFFFFFFFull) return -2;       // u32 group indices in the resolve lists
     const uint64_t npw = (nbytes + 31) / 32;
     INF_CHK(inf_ensure(&S.d_ref, &S.d_ref_cap, nbytes * 4 + 64));
     INF_CHK(inf_ensure(&S.d_pend, &S.d_pend_cap, npw * 4 + 64));

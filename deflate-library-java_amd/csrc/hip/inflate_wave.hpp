@@ -1124,8 +1124,10 @@ ndfl_inflate_emit_wave_kernel(const uint32_t* w, uint64_t nwords, uint64_t nbits
                     // from), pending bits; the bytes are written by the resolve rounds
                     wflush(L, gout, dst);
                     const uint64_t anchor = dist == 1 ? (L.n > 0 ? lastsrc : src) : 0;
-                    for (uint32_t k = 0; k < len; k++)
-                        ref[dst + k] = dist == 1 ? (uint32_t)(dst + k - anchor) : dist;
+                    for (uint32_t k = 0; k < len; k++) {
+                        const uint64_t back = dst + k - anchor;     // a run > 4 GiB falls back to its previous byte
+                        ref[dst + k] = dist == 1 ? (back < (1ull << 32) ? (uint32_t)back : 1u) : dist;
+                    }
                     for (uint64_t q = dst >> 5; q <= (dst + len - 1) >> 5; q++) {
                         const uint64_t lo = max(dst, q << 5), hi = min(dst + len, (q + 1) << 5);
                         const uint32_t m = (uint32_t)(((1ull << (hi - lo)) - 1) << (lo & 31));
@@ -1188,7 +1190,8 @@ ndfl_inflate_resolve_kernel(const uint32_t* list, const uint32_t* nlist, const u
             const uint32_t d = ref[i];
             const uint64_t p = i - d;
             if ((pend[p >> 5] >> (p & 31)) & 1) {
-                ref[i] = d + ref[p];
+                const uint64_t nd = (uint64_t)d + ref[p];
+                if (nd < (1ull << 32)) ref[i] = (uint32_t)nd;     // else keep d: p still leads to the value
                 still = true;
             } else {
                 out[i] = out[p];
