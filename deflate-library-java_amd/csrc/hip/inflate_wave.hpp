@@ -1242,8 +1242,9 @@ ndfl_inflate_resolve_apply_kernel(const uint32_t* list, const uint32_t* nlist, u
 // Initial list: every non-zero bitmap word in [w0, w1).
 extern "C" __global__ void __launch_bounds__(256)
 ndfl_inflate_pending_list_kernel(const uint32_t* pend, uint64_t w0, uint64_t w1, uint32_t* list, uint32_t* nlist) {
-    // 16 words per thread (four 16-byte loads); sparse bitmaps are the common case, so the block
-    // only appends when some word is non-zero
+    // 16 words per thread (four 16-byte loads), one block scan of the non-zero counts, one global
+    // atomic per block
+    __shared__ uint32_t sh[4], sbase;
     const uint64_t base = w0 + ((uint64_t)blockIdx.x * 256 + threadIdx.x) * 16;
     uint32_t v[16];
     if (base + 16 <= w1 && (base & 3) == 0) {
@@ -1254,10 +1255,15 @@ ndfl_inflate_pending_list_kernel(const uint32_t* pend, uint64_t w0, uint64_t w1,
 #pragma unroll
         for (int k = 0; k < 16; k++) v[k] = base + k < w1 ? pend[base + k] : 0u;
     }
-    bool any = false;
+    uint32_t cnt = 0;
 #pragma unroll
-    for (int k = 0; k < 16; k++) any |= v[k] != 0;
-    if (!__syncthreads_or(any)) return;
+    for (int k = 0; k < 16; k++) cnt += v[k] != 0;
+    uint32_t tot;
+    const uint32_t off = block_excl_scan<uint32_t, 4>(cnt, sh, tot);
+    if (threadIdx.x == 0) sbase = tot ? atomicAdd(nlist, tot) : 0u;
+    __syncthreads();
+    uint32_t o = sbase + off;
 #pragma unroll
-    for (int k = 0; k < 16; k++) block_append(v[k] != 0, (uint32_t)(base + k), list, nlist);
+    for (int k = 0; k < 16; k++)
+        if (v[k]) list[o++] = (uint32_t)(base + k);
 }
