@@ -134,3 +134,24 @@ def test_corrupted_streams_match_oracle_reason(ctx):
             if rng.random() < 0.3:
                 c = c[:rng.randrange(len(c))]
             check_same(ctx, bytes(c))
+
+
+def test_corrupted_lz77_streams_prefix_exact(ctx):
+    """LZ77-heavy streams (FULL_DYNAMIC, zlib -6) across many blocks, corrupted: every byte the GPU
+    reports before the error is produced through deferred copies and the resolve rounds, and must
+    equal the oracle's prefix; the Reason and consumed bits must match too."""
+    import zlib as Z
+    rng = random.Random(19)
+    words = [rng.randbytes(rng.randrange(3, 12)) for _ in range(300)]
+    data = b"".join(rng.choice(words) for _ in range(120_000))[:1 << 20]
+    co = Z.compressobj(6, Z.DEFLATED, -15)
+    streams = [O.deflate(data[:300_000], "FULL_DYNAMIC"), co.compress(data) + co.flush()]
+    for comp in streams:
+        check_same(ctx, comp)
+        for _ in range(25):
+            c = bytearray(comp)
+            for _ in range(rng.randrange(1, 3)):
+                c[rng.randrange(len(c) // 4, len(c))] ^= 1 << rng.randrange(8)
+            if rng.random() < 0.3:
+                c = c[:rng.randrange(len(c) // 2, len(c))]
+            check_same(ctx, bytes(c))
