@@ -67,6 +67,10 @@ constexpr uint32_t FIND_WIN_WORDS = 32768;
 constexpr uint32_t FIND_PERIOD_WORDS = 32768;
 constexpr uint32_t FIND_WPT = 8;                 // finder: input words per thread
 constexpr uint32_t COUNT_WAVES = 256 * 16;       // count pass: persistent waves
+#ifndef NDFL_EMIT_WAVES_PER_SIMD
+#define NDFL_EMIT_WAVES_PER_SIMD 4
+#endif
+constexpr uint32_t EMIT_WAVES = 256 * 4 * NDFL_EMIT_WAVES_PER_SIMD;   // emit pass: persistent waves
 
 struct In {
     const uint32_t* w;
@@ -860,7 +864,7 @@ static int inflate_run(InflateScratch& S, hipStream_t s, const uint8_t* in, uint
         INF_CHK(hipMemcpyAsync(S.d_stops, sp.data(), n * 8, hipMemcpyHostToDevice, s));
         uint32_t* d_order = (uint32_t*)((char*)S.d_stops + n * 8);
         INF_CHK(hipMemcpyAsync(d_order, order.data(), n * 4, hipMemcpyHostToDevice, s));
-        if (!S.d_ph) INF_CHK(hipMalloc(&S.d_ph, (size_t)COUNT_WAVES * sizeof(wv::PhArr)));
+        if (!S.d_ph) INF_CHK(hipMalloc(&S.d_ph, (size_t)std::max(COUNT_WAVES, EMIT_WAVES) * sizeof(wv::PhArr)));
         if (!S.d_cticket) INF_CHK(hipMalloc(&S.d_cticket, 64));
         INF_CHK(hipMemsetAsync(S.d_cticket, 0, 4, s));
         if (S.count_first) INF_CHK(hipEventRecord(S.ev[2], s));
@@ -998,8 +1002,8 @@ static int inflate_run(InflateScratch& S, hipStream_t s, const uint8_t* in, uint
     if (!S.h_cnt) INF_CHK(hipHostMalloc(&S.h_cnt, 64, 0));
     hipEvent_t e2 = S.ev[4], e3 = S.ev[5];
     INF_CHK(hipEventRecord(e2, s));
-    if (!S.d_ph) INF_CHK(hipMalloc(&S.d_ph, (size_t)COUNT_WAVES * sizeof(wv::PhArr)));
-    hipLaunchKernelGGL(ndfl_inflate_emit_wave_kernel, dim3(std::min<uint32_t>(nch, COUNT_WAVES)), dim3(64), 0, s, d_w,
+    if (!S.d_ph) INF_CHK(hipMalloc(&S.d_ph, (size_t)std::max(COUNT_WAVES, EMIT_WAVES) * sizeof(wv::PhArr)));
+    hipLaunchKernelGGL(ndfl_inflate_emit_wave_kernel, dim3(std::min<uint32_t>(nch, EMIT_WAVES)), dim3(64), 0, s, d_w,
                        nwords, nbits, (const EmitChain*)S.d_chains, nch, (uint32_t*)S.d_ticket, d_out,
                        (ChainRes*)S.d_res, (const uint64_t*)S.d_cands, ncand, (uint32_t*)S.d_ref, (uint32_t*)S.d_pend,
                        pool, (wv::PhArr*)S.d_ph);

@@ -999,7 +999,10 @@ ndfl_inflate_count_wave_kernel(const uint32_t* w, uint64_t nwords, uint64_t nbit
 // deferred -- its bytes get a back-reference (ref[i] = distance to a byte holding the same value)
 // and a pending bit, and ndfl_inflate_resolve_kernel rounds resolve them afterwards by pointer
 // jumping.  So every chain decodes in parallel whatever the LZ77 distances.
-extern "C" __global__ void __launch_bounds__(64, 4)
+#ifndef NDFL_EMIT_WAVES_PER_SIMD
+#define NDFL_EMIT_WAVES_PER_SIMD 4
+#endif
+extern "C" __global__ void __launch_bounds__(64, NDFL_EMIT_WAVES_PER_SIMD)
 ndfl_inflate_emit_wave_kernel(const uint32_t* w, uint64_t nwords, uint64_t nbits, const EmitChain* chains,
                               uint32_t nlist, uint32_t* ticket, uint8_t* out, ChainRes* res, const uint64_t* cands,
                               uint32_t ncand, uint32_t* ref, uint32_t* pend, SegPool pool, wv::PhArr* ph_all) {
