@@ -243,7 +243,7 @@ int ndfl_deflate_chunks(ndfl_ctx* c, const uint8_t* hist, uint32_t hist_len, uin
     a.crc_x = c->d_tabs.as<uint32_t>() + 1024;
     a.prof = nullptr;
     const bool prof = getenv("NDFL_DEFLATE_PROFILE") != nullptr;
-    if (prof) HIPCHK(hipMalloc(&a.prof, (size_t)nch * 64));
+    if (prof) { HIPCHK(hipMalloc(&a.prof, (size_t)nch * 128)); HIPCHK(hipMemsetAsync(a.prof, 0, (size_t)nch * 128, s)); }
     HIPCHK(hipEventRecord(c->ev0, s));
     hipLaunchKernelGGL(ndfl_deflate_chunks_kernel, dim3(nch), dim3(1024), 0, s, a);
     HIPCHK(hipGetLastError());
@@ -265,14 +265,25 @@ int ndfl_deflate_chunks(ndfl_ctx* c, const uint8_t* hist, uint32_t hist_len, uin
     c->last_ms = ms;
     c->deflate_ms = ms;
     if (prof) {
-        std::vector<uint64_t> h((size_t)nch * 8);
-        HIPCHK(hipMemcpy(h.data(), a.prof, (size_t)nch * 64, hipMemcpyDeviceToHost));
+        std::vector<uint64_t> h((size_t)nch * 16);
+        HIPCHK(hipMemcpy(h.data(), a.prof, (size_t)nch * 128, hipMemcpyDeviceToHost));
         hipFree(a.prof);
-        double sum[7] = {0}, tmin = 1e300, tmax = 0;
+        double sum[7] = {0}, tmin = 1e300, tmax = 0, sub[6] = {0};
+        uint64_t nsub = 0;
         for (uint32_t k = 0; k < nch; k++) {
-            for (int p = 0; p < 7; p++) sum[p] += (double)(h[k * 8 + p + 1] - h[k * 8 + p]);
-            tmin = std::min(tmin, (double)h[k * 8]); tmax = std::max(tmax, (double)h[k * 8 + 7]);
+            const uint64_t* q = &h[k * 16];
+            for (int p = 0; p < 7; p++) sum[p] += (double)(q[p + 1] - q[p]);
+            tmin = std::min(tmin, (double)q[0]); tmax = std::max(tmax, (double)q[7]);
+            if (q[8]) {   // codes sub-phases: trim, package-merge pair, canonical, cl RLE, cl PM, cl canon/header
+                const uint64_t t[7] = {q[2], q[8], q[9], q[10], q[11], q[12], q[13]};
+                for (int p = 0; p < 6; p++) sub[p] += (double)(t[p + 1] - t[p]);
+                nsub++;
+            }
         }
+        if (nsub)
+            fprintf(stderr, "[ndfl] deflate codes sub-phases (us/chunk): trim %.2f pm(lit,dist) %.2f canon %.2f cl-rle %.2f "
+                    "pm(cl) %.2f canon(cl) %.2f\n", sub[0] / nsub / 100, sub[1] / nsub / 100, sub[2] / nsub / 100,
+                    sub[3] / nsub / 100, sub[4] / nsub / 100, sub[5] / nsub / 100);
         // wall_clock64 runs at 100 MHz
         fprintf(stderr, "[ndfl] deflate phases (us/chunk): load+crc %.2f hist %.2f codes %.2f bits+scan %.2f emit %.2f "
                 "lookback %.2f store %.2f; span %.2f ms\n", sum[0] / nch / 100, sum[1] / nch / 100, sum[2] / nch / 100,

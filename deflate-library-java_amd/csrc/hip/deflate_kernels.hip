@@ -271,7 +271,7 @@ constexpr uint32_t CL_EXTRA_BITS[3] = {2, 3, 7};
 // codes, code-length RLE, code-length code, header sizes); static: the fixed codes of :394-410.
 // Leaves the code tables and header layout in `ps` and the reordered 3-bit code-length-code
 // lengths packed in misc[4..5] of the scratch.  All threads must call.
-__device__ __forceinline__ void build_block_codes(bool dynamic, char* scr, Persist& ps) {
+__device__ __forceinline__ void build_block_codes(bool dynamic, char* scr, Persist& ps, uint64_t* dbg = nullptr) {
     uint32_t* hlit = (uint32_t*)(scr + SCR_HLIT);
     uint32_t* hdist = (uint32_t*)(scr + SCR_HDIST);
     uint8_t* lens = (uint8_t*)(scr + SCR_LEN);
@@ -305,6 +305,7 @@ __device__ __forceinline__ void build_block_codes(bool dynamic, char* scr, Persi
             misc[2] = (dn == 1 && hdist[0] == 0) ? 1u : 0u;   // empty distance code
         }
         __syncthreads();
+        if (dbg && tid == 0) dbg[0] = wall_clock64();
         const int ln = (int)misc[0], dn = (int)misc[1];
         const bool emptyDist = misc[2] != 0;
         // literal/length and distance lengths side by side: threads [0, 640) and [640, 1024)
@@ -314,8 +315,10 @@ __device__ __forceinline__ void build_block_codes(bool dynamic, char* scr, Persi
             pm_lengths(isLit ? hlit : hdist, isLit ? ln : dn, 15, isLit ? lens : lens + ln,
                        isLit ? scr : scr + SCR_END, isLit ? tid : tid - 640, isLit || !emptyDist);
         }
+        if (dbg && tid == 0) dbg[1] = wall_clock64();
         canon_codes(lens, ln, ps.litCode, scr);
         canon_codes(lens + ln, dn, ps.distCode, scr);
+        if (dbg && tid == 0) dbg[2] = wall_clock64();
         // code-length sequence RLE (:187-223) as maximal-run decomposition
         const int nc = ln + dn;
         uint32_t rstart = 0xFFFFFFFFu;
@@ -359,8 +362,11 @@ __device__ __forceinline__ void build_block_codes(bool dynamic, char* scr, Persi
         __syncthreads();
         if ((uint32_t)tid < tot) atomicAdd(&clh[ps.clSym[tid]], 1u);
         __syncthreads();
+        if (dbg && tid == 0) dbg[3] = wall_clock64();
         pm_lengths(clh, 19, 7, clLen, scr);
+        if (dbg && tid == 0) dbg[4] = wall_clock64();
         canon_codes(clLen, 19, ps.clCode, scr);
+        if (dbg && tid == 0) dbg[5] = wall_clock64();
         // per-symbol header bit offsets
         uint32_t sb = 0;
         if ((uint32_t)tid < tot) {
@@ -672,7 +678,7 @@ ndfl_deflate_chunks_kernel(Args a) {
 
     const uint64_t tp2 = wall_clock64();
     // ---- 4. code construction -------------------------------------------------------------------
-    build_block_codes(a.dynamic != 0, scr, ps);
+    build_block_codes(a.dynamic != 0, scr, ps, a.prof ? a.prof + (uint64_t)c * 16 + 8 : nullptr);
     const uint32_t packedLo = misc[4], packedHi = misc[5];
     __syncthreads();
 
@@ -754,7 +760,7 @@ ndfl_deflate_chunks_kernel(Args a) {
     block_store(obuf, P, S, c, a.out, a.edge_w, a.edge_v);
     if (tid == 0) {
         if (a.prof) {
-            uint64_t* q = a.prof + (uint64_t)c * 8;
+            uint64_t* q = a.prof + (uint64_t)c * 16;
             q[0] = tp0; q[1] = tp1; q[2] = tp2; q[3] = tp3; q[4] = tp4; q[5] = tp5e; q[6] = tp5;
             q[7] = wall_clock64();
             (void)tp3a; (void)tp3b;
