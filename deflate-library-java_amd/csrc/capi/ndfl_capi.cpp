@@ -2,6 +2,7 @@
 // Compiled as HIP for gfx950 together with the kernels (single translation unit).
 #include "../../../include/ndfl.h"
 #include "../hip/deflate_kernels.hip"
+#include "../hip/deflate_split.hip"
 #include "../hip/lz77_kernels.hip"
 #include "../hip/strategy_kernels.hip"
 #include "../hip/inflate_kernels.hip"
@@ -34,6 +35,7 @@ struct DevBuf {
 
 uint32_t host_crc_tab[1024];
 uint32_t host_crc_x[64 + 1024];
+uint32_t host_crc_p2[64];          // x^(8 * 2^k)
 bool host_tabs_ready = false;
 
 void init_host_tables() {
@@ -50,6 +52,8 @@ void init_host_tables() {
         }
     for (uint32_t k = 0; k < 64; k++) host_crc_x[k] = crc_x8n(k);
     for (uint32_t k = 0; k < 1024; k++) host_crc_x[64 + k] = crc_x8n((uint64_t)k * 64);
+    host_crc_p2[0] = 1u << 23;
+    for (int k = 1; k < 64; k++) host_crc_p2[k] = crc_multmodp(host_crc_p2[k - 1], host_crc_p2[k - 1]);
     host_tabs_ready = true;
 }
 
@@ -63,6 +67,7 @@ struct ndfl_ctx {
     double last_ms = 0;
     double deflate_ms = 0;
     DevBuf d_in, d_out, d_status, d_ticket, d_edge_w, d_edge_v, d_crc, d_crc1, d_tabs, d_hostio;
+    DevBuf d_hist, d_codes, d_off;  // split RLE/LITERAL pipeline: histograms, code records, offsets
     DevBuf d_lz, d_link, d_match;   // LZ77 path: staging [pad|hist|data], hash links, per-position matches
     DevBuf d_mdata, d_mstreams[16], d_mbits[16], d_masm;   // strategy composition
     uint64_t* cb_out = nullptr;     // internal: when set, encoders also write per-chunk block bits here
@@ -72,6 +77,17 @@ struct ndfl_ctx {
 };
 
 #define HIPCHK(x) do { hipError_t _e = (x); if (_e != hipSuccess) return NDFL_E_DEVICE; } while (0)
+
+// Raw CRC of `len` bytes from the raw CRCs of its consecutive parts of `part_len` bytes into *out.
+static hipError_t launch_crc_combine(ndfl_ctx* c, hipStream_t s, const uint32_t* parts, uint32_t nparts,
+                                     uint32_t part_len, uint64_t len, uint32_t* out) {
+    hipError_t e = hipMemsetAsync(out, 0, 4, s);
+    if (e != hipSuccess) return e;
+    const uint32_t* p2 = c->d_tabs.as<uint32_t>() + 1024 + 64 + 1024;
+    const uint32_t grid = std::max(1u, std::min(1024u, (nparts + 255) / 256));
+    hipLaunchKernelGGL(ndfl_crc_combine_kernel, dim3(grid), dim3(256), 0, s, parts, nparts, part_len, len, p2, out);
+    return hipGetLastError();
+}
 
 extern "C" {
 
@@ -113,9 +129,11 @@ int ndfl_ctx_create(ndfl_ctx** out, int device, uint32_t flags) {
     c->stream = c->own;
     hipEventCreate(&c->ev0);
     hipEventCreate(&c->ev1);
-    if (c->d_tabs.ensure(sizeof(host_crc_tab) + sizeof(host_crc_x)) != hipSuccess) { delete c; return NDFL_E_DEVICE; }
+    if (c->d_tabs.ensure(sizeof(host_crc_tab) + sizeof(host_crc_x) + sizeof(host_crc_p2)) != hipSuccess) { delete c; return NDFL_E_DEVICE; }
     hipMemcpy(c->d_tabs.p, host_crc_tab, sizeof(host_crc_tab), hipMemcpyHostToDevice);
     hipMemcpy((char*)c->d_tabs.p + sizeof(host_crc_tab), host_crc_x, sizeof(host_crc_x), hipMemcpyHostToDevice);
+    hipMemcpy((char*)c->d_tabs.p + sizeof(host_crc_tab) + sizeof(host_crc_x), host_crc_p2, sizeof(host_crc_p2),
+              hipMemcpyHostToDevice);
     if (hipHostMalloc((void**)&c->h_pinned, 4096, 0) != hipSuccess) { delete c; return NDFL_E_DEVICE; }
     *out = c;
     return NDFL_OK;
@@ -127,7 +145,7 @@ int ndfl_ctx_destroy(ndfl_ctx* c) {
     hipStreamSynchronize(c->stream);
     DevBuf* bufs[] = {&c->d_in, &c->d_out, &c->d_status, &c->d_ticket, &c->d_edge_w, &c->d_edge_v,
                       &c->d_crc, &c->d_crc1, &c->d_tabs, &c->d_hostio, &c->d_lz, &c->d_link, &c->d_match,
-                      &c->d_mdata, &c->d_masm};
+                      &c->d_mdata, &c->d_masm, &c->d_hist, &c->d_codes, &c->d_off};
     for (DevBuf* b : bufs) b->release();
     for (int k = 0; k < 16; k++) { c->d_mstreams[k].release(); c->d_mbits[k].release(); }
     c->inf.release();
@@ -244,8 +262,34 @@ int ndfl_deflate_chunks(ndfl_ctx* c, const uint8_t* hist, uint32_t hist_len, uin
     a.prof = nullptr;
     const bool prof = getenv("NDFL_DEFLATE_PROFILE") != nullptr;
     if (prof) { HIPCHK(hipMalloc(&a.prof, (size_t)nch * 128)); HIPCHK(hipMemsetAsync(a.prof, 0, (size_t)nch * 128, s)); }
+    a.hist_out = nullptr; a.codes = nullptr; a.chunk_off = nullptr;
+    a.dbg = getenv("NDFL_DBG") ? atoi(getenv("NDFL_DBG")) : 0;
+    // split pipeline by default (deflate_split.hip); NDFL_DEFLATE_FUSED=1 selects the one-kernel encoder
+    static const bool fused = getenv("NDFL_DEFLATE_FUSED") != nullptr && atoi(getenv("NDFL_DEFLATE_FUSED")) != 0;
+    const bool split = !fused && !prof;
+    uint64_t* d_total = nullptr;
+    if (split) {
+        HIPCHK(c->d_hist.ensure((size_t)nch * HREC * 4));
+        HIPCHK(c->d_codes.ensure((size_t)nch * CREC * 4));
+        HIPCHK(c->d_off.ensure((size_t)nch * 8 + 64));
+        a.hist_out = c->d_hist.as<uint32_t>();
+        a.codes = c->d_codes.as<uint32_t>();
+        a.chunk_off = c->d_off.as<uint64_t>();
+        d_total = c->d_off.as<uint64_t>() + nch;
+    }
     HIPCHK(hipEventRecord(c->ev0, s));
-    hipLaunchKernelGGL(ndfl_deflate_chunks_kernel, dim3(nch), dim3(1024), 0, s, a);
+    if (split) {
+        hipLaunchKernelGGL(ndfl_deflate_hist_kernel, dim3(nch), dim3(1024), 0, s, a);
+        HIPCHK(hipGetLastError());
+        hipLaunchKernelGGL(ndfl_deflate_codes_kernel, dim3(nch), dim3(64), 0, s, a);
+        HIPCHK(hipGetLastError());
+        hipLaunchKernelGGL(ndfl_deflate_offsets_kernel, dim3(1), dim3(1024), 0, s, (const uint64_t*)a.status, nch,
+                           (uint64_t)start_bitpos, c->d_off.as<uint64_t>(), d_total);
+        HIPCHK(hipGetLastError());
+        hipLaunchKernelGGL(ndfl_deflate_emit_kernel, dim3(nch), dim3(1024), 0, s, a);
+    } else {
+        hipLaunchKernelGGL(ndfl_deflate_chunks_kernel, dim3(nch), dim3(1024), 0, s, a);
+    }
     HIPCHK(hipGetLastError());
     HIPCHK(hipEventRecord(c->ev1, s));
     const uint32_t ne = 2 * nch;
@@ -253,12 +297,11 @@ int ndfl_deflate_chunks(ndfl_ctx* c, const uint8_t* hist, uint32_t hist_len, uin
                        (const uint64_t*)a.edge_w, (const uint32_t*)a.edge_v, ne, d_out);
     HIPCHK(hipGetLastError());
     if (crc_inout) {
-        hipLaunchKernelGGL(ndfl_crc_combine_kernel, dim3(1), dim3(1024), 0, s,
-                           (const uint32_t*)a.crc_raw, nch, chunk_len, len, c->d_crc1.as<uint32_t>());
-        HIPCHK(hipGetLastError());
+        HIPCHK(launch_crc_combine(c, s, (const uint32_t*)a.crc_raw, nch, chunk_len, len, c->d_crc1.as<uint32_t>()));
         HIPCHK(hipMemcpyAsync(c->h_pinned + 4, c->d_crc1.p, 4, hipMemcpyDeviceToHost, s));
     }
-    HIPCHK(hipMemcpyAsync(c->h_pinned, a.status + (nch - 1), 8, hipMemcpyDeviceToHost, s));
+    if (split) HIPCHK(hipMemcpyAsync(c->h_pinned, d_total, 8, hipMemcpyDeviceToHost, s));
+    else HIPCHK(hipMemcpyAsync(c->h_pinned, a.status + (nch - 1), 8, hipMemcpyDeviceToHost, s));
     HIPCHK(hipStreamSynchronize(s));
     float ms = 0;
     hipEventElapsedTime(&ms, c->ev0, c->ev1);
@@ -829,9 +872,8 @@ int ndfl_crc32(ndfl_ctx* c, uint32_t* crc_inout, const uint8_t* data, uint64_t l
                        c->d_crc.as<uint32_t>());
     HIPCHK(hipGetLastError());
     HIPCHK(hipEventRecord(c->ev1, s));
-    hipLaunchKernelGGL(ndfl_crc_combine_kernel, dim3(1), dim3(1024), 0, s, (const uint32_t*)c->d_crc.as<uint32_t>(),
-                       (uint32_t)nseg, 65536u, len, c->d_crc1.as<uint32_t>());
-    HIPCHK(hipGetLastError());
+    HIPCHK(launch_crc_combine(c, s, (const uint32_t*)c->d_crc.as<uint32_t>(), (uint32_t)nseg, 65536u, len,
+                              c->d_crc1.as<uint32_t>()));
     HIPCHK(hipMemcpyAsync(c->h_pinned, c->d_crc1.p, 4, hipMemcpyDeviceToHost, s));
     HIPCHK(hipStreamSynchronize(s));
     float ms = 0;

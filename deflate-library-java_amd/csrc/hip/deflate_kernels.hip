@@ -25,7 +25,13 @@ namespace {
 constexpr int DT = 1024;                  // threads per workgroup
 constexpr int NW = DT / 64;               // waves per workgroup
 constexpr int MAX_CHUNK = 65536;
-constexpr int OUTW = 18600;               // LDS bit-buffer words (>= 594,362 bits)
+constexpr int OUTW = 18624;               // LDS bit-buffer words (>= 594,362 bits), a multiple of 64
+
+// Bit-buffer word w lives at LDS word bsw(w): an XOR swizzle inside each 64-word row.  Lane
+// cursors sit about S/1024 words apart (4-16 words), which without it puts the 64 lanes of a wave
+// on 4-16 of the 64 banks; with it, stride-2^k cursors spread over all banks, while 64 consecutive
+// words (zeroing, the coalesced store) still hit 64 distinct banks.
+__device__ __forceinline__ uint32_t bsw(uint32_t w) { return w ^ ((w >> 6) & 63u); }
 
 constexpr uint64_t ST_AGG = 1ull << 62;
 constexpr uint64_t ST_PRE = 2ull << 62;
@@ -95,7 +101,22 @@ struct Args {
     const uint32_t* crc_tab;  // slicing-by-4 tables (1024 u32)
     const uint32_t* crc_x;    // x^(8k) k<64 then x^(8*64k) k<1024
     uint64_t* prof;           // optional [nchunks][8] phase timestamps (wall clock)
+    // split pipeline (hist -> codes -> offsets -> emit), see ndfl_deflate_codes_kernel
+    uint32_t* hist_out;       // [nchunks][HREC] histograms: literal/length [0,288), distance [288,320)
+    const uint32_t* codes;    // [nchunks][CREC] code records
+    const uint64_t* chunk_off;// [nchunks] global bit offset of each chunk
+    int32_t dbg;              // TEMP timing experiments
 };
+
+// Split pipeline record layouts.
+constexpr int HREC = 320;                 // u32 per chunk histogram record
+constexpr int CREC_LIT = 0;               // u32[288] rev(code) | len << 16
+constexpr int CREC_DIST = 288;            // u32[32]
+constexpr int CREC_HDR = 320;             // u32[HDRW] header bits from local bit 0 (bfinal .. code-length symbols)
+constexpr int HDRW = 80;                  // >= 3 + 14 + 57 + 316 * 7 = 2286 bits (every code-length entry costs <= 7 bits)
+constexpr int CREC_META = CREC_HDR + HDRW;  // [0] hdrBits
+constexpr int CREC = CREC_META + 16;
+enum { MODE_FUSED = 0, MODE_HIST = 1, MODE_EMIT = 2 };
 
 // Length symbol / extra bits of a run 3..258 (D/comp/Lz77Huffman.java:92-111).
 __device__ __forceinline__ void run_sym(uint32_t run, uint32_t& sym, uint32_t& ne, uint32_t& ex) {
@@ -253,14 +274,14 @@ struct BitPut {
         acc |= (uint64_t)v << nb;
         nb += n;
         if (nb >= 32) {
-            atomicOr(&buf[wi], (uint32_t)acc);
+            atomicOr(&buf[bsw(wi)], (uint32_t)acc);
             wi++;
             acc >>= 32;
             nb -= 32;
         }
     }
     __device__ __forceinline__ void flush() {
-        if (nb) atomicOr(&buf[wi], (uint32_t)acc);
+        if (nb) atomicOr(&buf[bsw(wi)], (uint32_t)acc);
     }
 };
 
@@ -474,8 +495,8 @@ __device__ __forceinline__ void block_store(const uint32_t* obuf, uint64_t P, ui
     const uint32_t nw = (uint32_t)((sh + S + 31) >> 5);
     const uint64_t W0 = P >> 5;
     auto outw = [&](uint32_t k) -> uint32_t {
-        const uint32_t cur = obuf[k];
-        const uint32_t prv = k ? obuf[k - 1] : 0u;
+        const uint32_t cur = obuf[bsw(k)];
+        const uint32_t prv = k ? obuf[bsw(k - 1)] : 0u;
         return sh ? (cur << sh) | (prv >> (32 - sh)) : cur;
     };
     for (uint32_t k = (uint32_t)tid + 1; k + 1 < nw; k += DT) out[W0 + k] = outw(k);
@@ -489,10 +510,13 @@ __device__ __forceinline__ void block_store(const uint32_t* obuf, uint64_t P, ui
 
 }  // namespace
 
-extern "C" __global__ void __launch_bounds__(DT, 8)
-ndfl_deflate_chunks_kernel(Args a) {
-    __shared__ __attribute__((aligned(16))) uint32_t obuf[OUTW];
-    __shared__ Persist ps;
+// One chunk, one 1024-thread workgroup.  MODE_FUSED does everything (chunk ids from a ticket,
+// look-back for the offset); the split pipeline runs it as MODE_HIST (load, CRC, histograms to
+// hist_out) and, after ndfl_deflate_codes_kernel and ndfl_deflate_offsets_kernel, MODE_EMIT (load,
+// code tables and header from the record, token bits at the precomputed offset).
+template <int MODE>
+__device__ __forceinline__ void deflate_chunk(const Args& a, uint32_t* obuf, Persist& ps, uint32_t* hl4 = nullptr,
+                                              uint32_t* ctab = nullptr) {
     char* scr = (char*)obuf;
     uint32_t* hlit = (uint32_t*)(scr + SCR_HLIT);
     uint32_t* hdist = (uint32_t*)(scr + SCR_HDIST);
@@ -503,9 +527,18 @@ ndfl_deflate_chunks_kernel(Args a) {
     const int lane = tid & 63, wid = tid >> 6;
 
     const uint64_t tp0 = wall_clock64();
-    if (tid == 0) ps.chunk = atomicAdd(a.ticket, 1u);
-    if (tid < 288) hlit[tid] = 0;
-    if (tid < 32) hdist[tid] = 0;
+    if (MODE == MODE_FUSED) {
+        if (tid == 0) ps.chunk = atomicAdd(a.ticket, 1u);
+    } else {
+        if (tid == 0) ps.chunk = blockIdx.x;
+    }
+    if (MODE == MODE_FUSED) {
+        if (tid < 288) hlit[tid] = 0;
+        if (tid < 32) hdist[tid] = 0;
+    } else if (MODE == MODE_HIST) {
+        for (int k = tid; k < 4 * 336; k += DT) hl4[k] = 0;
+        if (a.crc_raw) ctab[tid] = a.crc_tab[tid];          // slicing-by-4 tables to LDS (DT == 1024)
+    }
     __syncthreads();
     const uint32_t c = ps.chunk;
     const uint64_t cs = (uint64_t)c * a.chunk_len;
@@ -546,12 +579,13 @@ ndfl_deflate_chunks_kernel(Args a) {
     }
 
     // ---- CRC-32 (raw, init 0) of this lane's bytes, combined across the chunk ----------------
-    if (a.crc_raw) {
+    if (MODE != MODE_EMIT && a.crc_raw) {
         uint32_t cr = 0;
-        const uint32_t* T0 = a.crc_tab;
-        const uint32_t* T1 = a.crc_tab + 256;
-        const uint32_t* T2 = a.crc_tab + 512;
-        const uint32_t* T3 = a.crc_tab + 768;
+        const uint32_t* tb = MODE == MODE_HIST ? ctab : a.crc_tab;
+        const uint32_t* T0 = tb;
+        const uint32_t* T1 = tb + 256;
+        const uint32_t* T2 = tb + 512;
+        const uint32_t* T3 = tb + 768;
         const int nfull = vcnt >> 2;
 #pragma unroll
         for (int k = 0; k < 16; k++) {
@@ -578,7 +612,7 @@ ndfl_deflate_chunks_kernel(Args a) {
         if (lane == 0) ps.crcAcc[wid] = contrib;
     }
     __syncthreads();
-    if (a.crc_raw && tid == 0) {
+    if (MODE != MODE_EMIT && a.crc_raw && tid == 0) {
         uint32_t x = 0;
         for (int k = 0; k < NW; k++) x ^= ps.crcAcc[k];
         a.crc_raw[c] = x;
@@ -621,7 +655,9 @@ ndfl_deflate_chunks_kernel(Args a) {
         const uint64_t beyond = vcnt >= 64 ? 0ull : (~0ull << (vcnt - 1));
         S1 = F & (nxt | beyond);
     }
-    // visit this lane's pieces in order: BODY sees (gpos, v, pend, single).  Outer loop over 8-byte
+    // visit this lane's pieces in order: BODY sees (gpos, v, pend, single) and pfv = PF_(v), which is
+    // evaluated for all 8 bytes of a group before the per-byte branches (independent LDS reads in
+    // flight instead of one exposed latency per byte).  Outer loop over 8-byte
     // groups (select tree on the uniform group index: a dynamic register index would put w[] in
     // scratch memory), inner loop unrolled: byte extraction is a constant shift.  A macro rather than
     // a lambda: capturing w[] by reference also demotes it to scratch.
@@ -636,10 +672,14 @@ ndfl_deflate_chunks_kernel(Args a) {
         const uint32_t b2_ = o1_ ? w[11] : w[9], b3_ = o1_ ? w[15] : w[13];                            \
         const uint32_t gw0_ = o4_ ? (o2_ ? a3_ : a2_) : (o2_ ? a1_ : a0_);                             \
         const uint32_t gw1_ = o4_ ? (o2_ ? b3_ : b2_) : (o2_ ? b1_ : b0_);                             \
+        uint32_t pf_[8];                                                                               \
+        _Pragma("unroll") for (int j_ = 0; j_ < 8; j_++)                                               \
+            pf_[j_] = PF_(((j_ < 4 ? gw0_ : gw1_) >> (8 * (j_ & 3))) & 0xFFu);                         \
         _Pragma("unroll") for (int j_ = 0; j_ < 8; j_++) {                                             \
             if ((g_ >> j_) & 1) {                                                                      \
                 const int i_ = 8 * o_ + j_;                                                            \
                 const uint32_t v = ((j_ < 4 ? gw0_ : gw1_) >> (8 * (j_ & 3))) & 0xFFu;                 \
+                const uint32_t pfv = pf_[j_];                                                          \
                 const bool single = (S1 >> i_) & 1;                                                    \
                 const uint32_t gpos = t0 + (uint32_t)i_;                                               \
                 uint32_t pend = gpos + 1;                                                              \
@@ -653,33 +693,58 @@ ndfl_deflate_chunks_kernel(Args a) {
     }
 
     // ---- 3. histograms (closed-form greedy parse per piece, App. A.2) -------------------------
+    // MODE_HIST counts into 4 lane-interleaved copies (fewer same-address LDS atomics per
+    // instruction; copy stride 336 words puts a symbol's copies in 4 different banks)
+    uint32_t* hl = hlit;
+    uint32_t* hd = hdist;
+    if (MODE == MODE_HIST && !(a.dbg & 2)) { hl = hl4 + (tid & 3) * 336; hd = hl + 288; }
+    if (MODE == MODE_HIST) { if (tid < 288) hlit[tid] = 0; if (tid < 32) hdist[tid] = 0; __syncthreads(); }
+    if (MODE != MODE_EMIT && !(MODE == MODE_HIST && (a.dbg & 16))) {
+#define PF_(x) 0u
     NDFL_FOR_PIECES({
-        if (single || !a.rle) { atomicAdd(&hlit[v], 1u); continue; }
+        (void)pfv;
+        if (MODE == MODE_HIST && (a.dbg & 1)) continue;
+        if (single || !a.rle) { atomicAdd(&hl[v], 1u); continue; }
         const uint32_t plen = pend - gpos;
         const uint32_t lead = lead_of(gpos, v);
         const uint32_t R = plen - lead;
         const uint32_t n258 = R / 258, m = R % 258;
         uint32_t nlit = lead + (m < 3 ? m : 0);
-        if (nlit) atomicAdd(&hlit[v], nlit);
-        if (n258) atomicAdd(&hlit[285], n258);
+        if (nlit) atomicAdd(&hl[v], nlit);
+        if (n258) atomicAdd(&hl[285], n258);
         uint32_t nd = n258;
         if (m >= 3) {
             uint32_t sym, ne, ex; run_sym(m, sym, ne, ex);
-            atomicAdd(&hlit[sym], 1u);
+            atomicAdd(&hl[sym], 1u);
             nd++;
         }
-        if (nd) atomicAdd(&hdist[0], nd);
+        if (nd) atomicAdd(&hd[0], nd);
     })
+#undef PF_
     if (tid == 0) {
-        atomicAdd(&hlit[256], 1u);                          // end of block (:131-132)
-        if (a.dynamic && len_c == 0) atomicAdd(&hlit[0], 1u);  // (:146-147)
+        atomicAdd(&hl[256], 1u);                          // end of block (:131-132)
+        if (a.dynamic && len_c == 0) atomicAdd(&hl[0], 1u);  // (:146-147)
     }
     __syncthreads();
+    }
+    if (MODE == MODE_HIST) {
+        uint32_t* h = a.hist_out + (uint64_t)c * HREC;
+        if (tid < HREC) h[tid] = hl4[tid] + hl4[336 + tid] + hl4[672 + tid] + hl4[1008 + tid];
+        return;
+    }
 
     const uint64_t tp2 = wall_clock64();
     // ---- 4. code construction -------------------------------------------------------------------
-    build_block_codes(a.dynamic != 0, scr, ps, a.prof ? a.prof + (uint64_t)c * 16 + 8 : nullptr);
-    const uint32_t packedLo = misc[4], packedHi = misc[5];
+    uint32_t packedLo = 0, packedHi = 0;
+    if (MODE == MODE_FUSED) {
+        build_block_codes(a.dynamic != 0, scr, ps, a.prof ? a.prof + (uint64_t)c * 16 + 8 : nullptr);
+        packedLo = misc[4]; packedHi = misc[5];
+    } else {
+        const uint32_t* rec = a.codes + (uint64_t)c * CREC;
+        if (tid < 288) ps.litCode[tid] = rec[CREC_LIT + tid];
+        else if (tid < 320) ps.distCode[tid - 288] = rec[CREC_DIST + tid - 288];
+        if (tid == 0) ps.hdrBits = rec[CREC_META];
+    }
     __syncthreads();
 
     const uint64_t tp3 = wall_clock64();
@@ -687,8 +752,10 @@ ndfl_deflate_chunks_kernel(Args a) {
     const uint32_t d0 = ps.distCode[0];
     const uint32_t c285 = ps.litCode[285];
     uint32_t mybits = 0;
+#define PF_(x) ps.litCode[x]
     NDFL_FOR_PIECES({
-        const uint32_t lv = ps.litCode[v] >> 16;
+        if (MODE == MODE_EMIT && (a.dbg & 8)) continue;
+        const uint32_t lv = pfv >> 16;
         if (single || !a.rle) { mybits += lv; continue; }
         const uint32_t lead = lead_of(gpos, v);
         const uint32_t R = pend - gpos - lead;
@@ -701,6 +768,7 @@ ndfl_deflate_chunks_kernel(Args a) {
             mybits += m * lv;
         }
     })
+#undef PF_
     const uint64_t tp3a = wall_clock64();
     uint32_t tokTotal;
     const uint32_t myoff = block_excl_scan<uint32_t, NW>(mybits, ps.scan32, tokTotal);
@@ -710,7 +778,7 @@ ndfl_deflate_chunks_kernel(Args a) {
     const uint64_t S = (uint64_t)hdrBits + tokTotal + eobLen;
     // publish this chunk's size now; the look-back runs after the chunk is emitted at local bit 0,
     // so predecessors get the emit time to publish theirs
-    if (tid == 0) {
+    if (MODE == MODE_FUSED && tid == 0) {
         if (c == 0) st_agent(&a.status[0], ST_PRE | (a.base_bit + S));
         else st_agent(&a.status[c], ST_AGG | S);
         if (a.chunk_bits) a.chunk_bits[c] = S;
@@ -719,19 +787,34 @@ ndfl_deflate_chunks_kernel(Args a) {
     // zero the bit buffer (scratch is dead from here on); one spare word for the final shift
     const uint32_t nwl = (uint32_t)((S + 31) >> 5) + 1;
     __syncthreads();
-    for (uint32_t k = (uint32_t)tid; k < nwl; k += DT) obuf[k] = 0;
+    if (MODE == MODE_FUSED) {
+        for (uint32_t k = (uint32_t)tid; k < nwl; k += DT) obuf[bsw(k)] = 0;
+    } else {
+        // the record's header words (zero past hdrBits) start the buffer
+        const uint32_t* hdr = a.codes + (uint64_t)c * CREC + CREC_HDR;
+        const uint32_t hw = (hdrBits + 31) >> 5;
+        for (uint32_t k = (uint32_t)tid; k < nwl; k += DT) obuf[bsw(k)] = k < hw ? hdr[k] : 0u;
+    }
     __syncthreads();
     const uint32_t bit0 = 0;
 
     // ---- 6. emit ------------------------------------------------------------------------------
-    emit_block_header(obuf, is_final, a.dynamic != 0, ps, packedLo, packedHi, hdrBits, tokTotal, eobLen);
+    if (MODE == MODE_FUSED) {
+        emit_block_header(obuf, is_final, a.dynamic != 0, ps, packedLo, packedHi, hdrBits, tokTotal, eobLen);
+    } else if (tid == 0) {
+        BitPut be; be.init(obuf, bit0 + hdrBits + tokTotal);
+        be.put(ps.litCode[256] & 0xFFFF, eobLen);
+        be.flush();
+    }
     {
         BitPut bp; bp.init(obuf, bit0 + hdrBits + myoff);
         const uint32_t d0c = d0 & 0xFFFF, d0l = d0 >> 16;
         const uint32_t m258 = (c285 & 0xFFFF) | (d0c << (c285 >> 16));
         const uint32_t m258l = (c285 >> 16) + d0l;
+#define PF_(x) ps.litCode[x]
         NDFL_FOR_PIECES({
-            const uint32_t lc = ps.litCode[v];
+            if (MODE == MODE_EMIT && (a.dbg & 4)) continue;
+            const uint32_t lc = pfv;
             if (single || !a.rle) { bp.put(lc & 0xFFFF, lc >> 16); continue; }
             const uint32_t lead = lead_of(gpos, v);
             const uint32_t R = pend - gpos - lead;
@@ -748,15 +831,16 @@ ndfl_deflate_chunks_kernel(Args a) {
                 for (uint32_t k = 0; k < m; k++) bp.put(lc & 0xFFFF, lc >> 16);
             }
         })
+#undef PF_
         bp.flush();
     }
     __syncthreads();
 
     const uint64_t tp5e = wall_clock64();
     // ---- 7. look-back, then store shifted to the global bit offset ---------------------------
-    block_lookback(c, a.base_bit, S, a.status, ps);
+    if (MODE == MODE_FUSED) block_lookback(c, a.base_bit, S, a.status, ps);
     const uint64_t tp5 = wall_clock64();
-    const uint64_t P = ps.P;
+    const uint64_t P = MODE == MODE_FUSED ? ps.P : a.chunk_off[c];
     block_store(obuf, P, S, c, a.out, a.edge_w, a.edge_v);
     if (tid == 0) {
         if (a.prof) {
@@ -766,6 +850,32 @@ ndfl_deflate_chunks_kernel(Args a) {
             (void)tp3a; (void)tp3b;
         }
     }
+    (void)is_final; (void)packedLo; (void)packedHi;
+}
+
+extern "C" __global__ void __launch_bounds__(DT, 8)
+ndfl_deflate_chunks_kernel(Args a) {
+    __shared__ __attribute__((aligned(16))) uint32_t obuf[OUTW];
+    __shared__ Persist ps;
+    deflate_chunk<MODE_FUSED>(a, obuf, ps);
+}
+
+// Split pipeline pass 1: CRC + histograms only (small LDS).
+extern "C" __global__ void __launch_bounds__(DT, 8)
+ndfl_deflate_hist_kernel(Args a) {
+    __shared__ __attribute__((aligned(16))) uint32_t obuf[(SCR_LAST + 1024) / 4];
+    __shared__ __attribute__((aligned(16))) uint32_t hl4[4 * 336];
+    __shared__ uint32_t ctab[1024];
+    __shared__ Persist ps;
+    deflate_chunk<MODE_HIST>(a, obuf, ps, hl4, ctab);
+}
+
+// Split pipeline pass 4: token bits at the offset from ndfl_deflate_offsets_kernel.
+extern "C" __global__ void __launch_bounds__(DT, 8)
+ndfl_deflate_emit_kernel(Args a) {
+    __shared__ __attribute__((aligned(16))) uint32_t obuf[OUTW];
+    __shared__ Persist ps;
+    deflate_chunk<MODE_EMIT>(a, obuf, ps);
 }
 
 // Merge the boundary words: every word touched by more than one chunk is the OR of all of them.
@@ -780,23 +890,24 @@ extern "C" __global__ void ndfl_edge_fixup_kernel(const uint64_t* edge_w, const 
     out[wv] = v;
 }
 
-// Combine per-chunk raw CRCs into the raw CRC of the call's data (x^(8*after) shifts).
-extern "C" __global__ void ndfl_crc_combine_kernel(const uint32_t* crc_raw, uint32_t nchunks, uint32_t chunk_len,
-                                                   uint64_t n, uint32_t* out_raw) {
-    __shared__ uint32_t red[16];
+// Combine per-chunk raw CRCs into the raw CRC of the call's data: raw = XOR over chunks of
+// crc_c * x^(8 * bytes after chunk c).  Grid-stride over chunks, the shift from a table of
+// x^(8 * 2^k) (one multiply per set bit), partial XORs folded with one atomicXor per wave into
+// *out_raw (zeroed by the caller).
+extern "C" __global__ void __launch_bounds__(256)
+ndfl_crc_combine_kernel(const uint32_t* crc_raw, uint32_t nchunks, uint32_t chunk_len, uint64_t n,
+                        const uint32_t* x8p2, uint32_t* out_raw) {
     uint32_t acc = 0;
-    for (uint32_t c = threadIdx.x; c < nchunks; c += blockDim.x) {
-        uint64_t end = min((uint64_t)(c + 1) * chunk_len, n);
-        acc ^= crc_multmodp(crc_x8n(n - end), crc_raw[c]);
+    for (uint32_t c = blockIdx.x * blockDim.x + threadIdx.x; c < nchunks; c += gridDim.x * blockDim.x) {
+        const uint64_t end = min((uint64_t)(c + 1) * chunk_len, n);
+        uint64_t after = n - end;
+        uint32_t p = 1u << 31;                                   // x^0
+        for (int k = 0; after; k++, after >>= 1)
+            if (after & 1) p = crc_multmodp(x8p2[k], p);
+        acc ^= crc_multmodp(p, crc_raw[c]);
     }
     acc = wave_xor(acc);
-    if ((threadIdx.x & 63) == 0) red[threadIdx.x >> 6] = acc;
-    __syncthreads();
-    if (threadIdx.x == 0) {
-        uint32_t x = 0;
-        for (uint32_t k = 0; k < blockDim.x / 64; k++) x ^= red[k];
-        *out_raw = x;
-    }
+    if ((threadIdx.x & 63) == 0 && acc) atomicXor(out_raw, acc);
 }
 
 // Standalone CRC-32 (raw, init 0) of a device buffer: one 1024-thread workgroup per 64 KiB

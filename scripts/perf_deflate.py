@@ -1,9 +1,10 @@
-import sys, time, torch, ctypes
-sys.path.insert(0,'deflate-library-java_amd/python'); sys.path.insert(0,'tests')
+import os, sys, time, torch, ctypes
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, os.path.join(ROOT, 'deflate-library-java_amd/python')); sys.path.insert(0, os.path.join(ROOT, 'tests'))
 import ndfl, corpus
 ctx = ndfl.Context(0)
 L = ndfl._lib.load()
-for name, n in [("c4", 4<<30), ("zeros", 1<<30), ("rand", 1<<30)]:
+for name, n in [(a.split(":")[0], int(a.split(":")[1]) << 20) for a in (sys.argv[1:] or ["c4:4096", "zeros:1024", "rand:1024"])]:
     if name == "c4": x = corpus.c4_mixed(n, device="cuda")
     elif name == "zeros": x = torch.zeros(n, dtype=torch.uint8, device="cuda")
     else: x = torch.randint(0,256,(n,),dtype=torch.uint8,device="cuda")
