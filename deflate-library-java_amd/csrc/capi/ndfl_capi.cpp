@@ -263,7 +263,6 @@ int ndfl_deflate_chunks(ndfl_ctx* c, const uint8_t* hist, uint32_t hist_len, uin
     const bool prof = getenv("NDFL_DEFLATE_PROFILE") != nullptr;
     if (prof) { HIPCHK(hipMalloc(&a.prof, (size_t)nch * 128)); HIPCHK(hipMemsetAsync(a.prof, 0, (size_t)nch * 128, s)); }
     a.hist_out = nullptr; a.codes = nullptr; a.chunk_off = nullptr;
-    a.dbg = getenv("NDFL_DBG") ? atoi(getenv("NDFL_DBG")) : 0;
     // split pipeline by default (deflate_split.hip); NDFL_DEFLATE_FUSED=1 selects the one-kernel encoder
     static const bool fused = getenv("NDFL_DEFLATE_FUSED") != nullptr && atoi(getenv("NDFL_DEFLATE_FUSED")) != 0;
     const bool split = !fused && !prof;

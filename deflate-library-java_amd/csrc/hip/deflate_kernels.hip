@@ -25,13 +25,7 @@ namespace {
 constexpr int DT = 1024;                  // threads per workgroup
 constexpr int NW = DT / 64;               // waves per workgroup
 constexpr int MAX_CHUNK = 65536;
-constexpr int OUTW = 18624;               // LDS bit-buffer words (>= 594,362 bits), a multiple of 64
-
-// Bit-buffer word w lives at LDS word bsw(w): an XOR swizzle inside each 64-word row.  Lane
-// cursors sit about S/1024 words apart (4-16 words), which without it puts the 64 lanes of a wave
-// on 4-16 of the 64 banks; with it, stride-2^k cursors spread over all banks, while 64 consecutive
-// words (zeroing, the coalesced store) still hit 64 distinct banks.
-__device__ __forceinline__ uint32_t bsw(uint32_t w) { return w ^ ((w >> 6) & 63u); }
+constexpr int OUTW = 18600;               // LDS bit-buffer words (>= 594,362 bits)
 
 constexpr uint64_t ST_AGG = 1ull << 62;
 constexpr uint64_t ST_PRE = 2ull << 62;
@@ -105,7 +99,6 @@ struct Args {
     uint32_t* hist_out;       // [nchunks][HREC] histograms: literal/length [0,288), distance [288,320)
     const uint32_t* codes;    // [nchunks][CREC] code records
     const uint64_t* chunk_off;// [nchunks] global bit offset of each chunk
-    int32_t dbg;              // TEMP timing experiments
 };
 
 // Split pipeline record layouts.
@@ -274,14 +267,14 @@ struct BitPut {
         acc |= (uint64_t)v << nb;
         nb += n;
         if (nb >= 32) {
-            atomicOr(&buf[bsw(wi)], (uint32_t)acc);
+            atomicOr(&buf[wi], (uint32_t)acc);
             wi++;
             acc >>= 32;
             nb -= 32;
         }
     }
     __device__ __forceinline__ void flush() {
-        if (nb) atomicOr(&buf[bsw(wi)], (uint32_t)acc);
+        if (nb) atomicOr(&buf[wi], (uint32_t)acc);
     }
 };
 
@@ -495,8 +488,8 @@ __device__ __forceinline__ void block_store(const uint32_t* obuf, uint64_t P, ui
     const uint32_t nw = (uint32_t)((sh + S + 31) >> 5);
     const uint64_t W0 = P >> 5;
     auto outw = [&](uint32_t k) -> uint32_t {
-        const uint32_t cur = obuf[bsw(k)];
-        const uint32_t prv = k ? obuf[bsw(k - 1)] : 0u;
+        const uint32_t cur = obuf[k];
+        const uint32_t prv = k ? obuf[k - 1] : 0u;
         return sh ? (cur << sh) | (prv >> (32 - sh)) : cur;
     };
     for (uint32_t k = (uint32_t)tid + 1; k + 1 < nw; k += DT) out[W0 + k] = outw(k);
@@ -697,13 +690,11 @@ __device__ __forceinline__ void deflate_chunk(const Args& a, uint32_t* obuf, Per
     // instruction; copy stride 336 words puts a symbol's copies in 4 different banks)
     uint32_t* hl = hlit;
     uint32_t* hd = hdist;
-    if (MODE == MODE_HIST && !(a.dbg & 2)) { hl = hl4 + (tid & 3) * 336; hd = hl + 288; }
-    if (MODE == MODE_HIST) { if (tid < 288) hlit[tid] = 0; if (tid < 32) hdist[tid] = 0; __syncthreads(); }
-    if (MODE != MODE_EMIT && !(MODE == MODE_HIST && (a.dbg & 16))) {
+    if (MODE == MODE_HIST) { hl = hl4 + (tid & 3) * 336; hd = hl + 288; }
+    if (MODE != MODE_EMIT) {
 #define PF_(x) 0u
     NDFL_FOR_PIECES({
         (void)pfv;
-        if (MODE == MODE_HIST && (a.dbg & 1)) continue;
         if (single || !a.rle) { atomicAdd(&hl[v], 1u); continue; }
         const uint32_t plen = pend - gpos;
         const uint32_t lead = lead_of(gpos, v);
@@ -754,7 +745,6 @@ __device__ __forceinline__ void deflate_chunk(const Args& a, uint32_t* obuf, Per
     uint32_t mybits = 0;
 #define PF_(x) ps.litCode[x]
     NDFL_FOR_PIECES({
-        if (MODE == MODE_EMIT && (a.dbg & 8)) continue;
         const uint32_t lv = pfv >> 16;
         if (single || !a.rle) { mybits += lv; continue; }
         const uint32_t lead = lead_of(gpos, v);
@@ -788,12 +778,12 @@ __device__ __forceinline__ void deflate_chunk(const Args& a, uint32_t* obuf, Per
     const uint32_t nwl = (uint32_t)((S + 31) >> 5) + 1;
     __syncthreads();
     if (MODE == MODE_FUSED) {
-        for (uint32_t k = (uint32_t)tid; k < nwl; k += DT) obuf[bsw(k)] = 0;
+        for (uint32_t k = (uint32_t)tid; k < nwl; k += DT) obuf[k] = 0;
     } else {
         // the record's header words (zero past hdrBits) start the buffer
         const uint32_t* hdr = a.codes + (uint64_t)c * CREC + CREC_HDR;
         const uint32_t hw = (hdrBits + 31) >> 5;
-        for (uint32_t k = (uint32_t)tid; k < nwl; k += DT) obuf[bsw(k)] = k < hw ? hdr[k] : 0u;
+        for (uint32_t k = (uint32_t)tid; k < nwl; k += DT) obuf[k] = k < hw ? hdr[k] : 0u;
     }
     __syncthreads();
     const uint32_t bit0 = 0;
@@ -813,7 +803,6 @@ __device__ __forceinline__ void deflate_chunk(const Args& a, uint32_t* obuf, Per
         const uint32_t m258l = (c285 >> 16) + d0l;
 #define PF_(x) ps.litCode[x]
         NDFL_FOR_PIECES({
-            if (MODE == MODE_EMIT && (a.dbg & 4)) continue;
             const uint32_t lc = pfv;
             if (single || !a.rle) { bp.put(lc & 0xFFFF, lc >> 16); continue; }
             const uint32_t lead = lead_of(gpos, v);

@@ -361,7 +361,7 @@ ndfl_lz_encode_kernel(LzEncArgs a) {
     }
     const uint32_t nwl = (uint32_t)((S + 31) >> 5) + 1;
     __syncthreads();
-    for (uint32_t k = (uint32_t)tid; k < nwl; k += DT) obuf[bsw(k)] = 0;
+    for (uint32_t k = (uint32_t)tid; k < nwl; k += DT) obuf[k] = 0;
     __syncthreads();
 
     // ---- emit ----------------------------------------------------------------------------------
