@@ -66,6 +66,10 @@ constexpr uint64_t IN_PAD = 256;           // zero bytes after the staged input
 constexpr uint32_t FIND_WIN_WORDS = 32768;
 constexpr uint32_t FIND_PERIOD_WORDS = 32768;
 constexpr uint32_t FIND_WPT = 8;                 // finder: input words per thread
+#ifndef NDFL_STRICT_SLICE
+#define NDFL_STRICT_SLICE 128
+#endif
+constexpr uint32_t STRICT_SLICE = NDFL_STRICT_SLICE;  // strict stage: survivors per ticket
 constexpr uint32_t COUNT_WAVES = 256 * 16;       // count pass: persistent waves
 #ifndef NDFL_EMIT_WAVES_PER_SIMD
 #define NDFL_EMIT_WAVES_PER_SIMD 4
@@ -318,7 +322,13 @@ __device__ __noinline__ bool strict_stored(const In& in, uint64_t p) {
 // HCLEN+4 3-bit lengths -- kraft_bits.hpp, generated); stored headers need LEN == ~NLEN at the
 // next byte boundary (one test per byte position) and zero padding.  Survivors (about 1 in 1000
 // positions) go to a global list for the strict stage.
-extern "C" __global__ void __launch_bounds__(256)
+#ifndef NDFL_FIND_WPE
+#define NDFL_FIND_WPE 3
+#endif
+#ifndef NDFL_STRICT_WPE
+#define NDFL_STRICT_WPE 4
+#endif
+extern "C" __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(NDFL_FIND_WPE)))
 ndfl_inflate_find_kernel(const uint32_t* w, uint64_t nwords, uint64_t nbits, uint64_t* qlist, uint32_t* qcount,
                          uint32_t qcap, uint32_t win_words, uint32_t period_words) {
     using namespace inf;
@@ -432,19 +442,20 @@ struct SRd {
 // through a per-lane 128-entry table of the code-length code (LDS, indexed by the next 7 bits
 // MSB first: canonical codes fill it in (length, symbol) order).  Accepted headers go to their
 // 64 KiB segment's list.
-extern "C" __global__ void __launch_bounds__(256)
+extern "C" __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(NDFL_STRICT_WPE)))
 ndfl_inflate_strict_kernel(const uint32_t* w, uint64_t nwords, uint64_t nbits, const uint64_t* qlist,
-                           const uint32_t* qcount, uint32_t qcap, uint32_t* seg_cnt, uint64_t* seg_list) {
+                           const uint32_t* qcount, uint32_t qcap, uint32_t* seg_cnt, uint64_t* seg_list,
+                           uint32_t* ticket, unsigned long long* sst) {
     using namespace inf;
     __shared__ uint4 tabs[256 * 8];                          // 128 bytes per lane
     uint8_t* tab = (uint8_t*)&tabs[threadIdx.x * 8];
     const uint32_t n = min(*qcount, qcap);
     In in{w, nwords, nbits};
     const uint32_t lane = threadIdx.x & 63u;
-    const uint64_t nw = (uint64_t)gridDim.x * (blockDim.x / 64);
-    const uint64_t wid = (uint64_t)blockIdx.x * (blockDim.x / 64) + threadIdx.x / 64;
-    const uint32_t end = (uint32_t)((uint64_t)n * (wid + 1) / nw);
-    uint32_t next = (uint32_t)((uint64_t)n * wid / nw);
+    // survivors are claimed STRICT_SLICE at a time from a global ticket, so the grid is sized to
+    // what fits on the chip and waves that draw short headers take more slices
+    uint32_t next = 0, end = 0;
+    bool drained = false;
     const uint64_t below = (1ull << lane) - 1ull;
     auto record = [&](uint64_t p) {
         const uint32_t seg = (uint32_t)(p / ((uint64_t)SEG_BYTES * 8));
@@ -458,10 +469,20 @@ ndfl_inflate_strict_kernel(const uint32_t* w, uint64_t nwords, uint64_t nbits, c
     uint32_t i = 0, total = 0, numLit = 0, numDist = 0, litK = 0, distK = 0, ones = 0, other = 0, eob = 0, d0 = 0,
              d31 = 0;
     int runVal = -1;
+    uint64_t n_iter = 0, n_refill = 0, n_steps = 0;      // NDFL_STATS (sst != nullptr)
     for (;;) {
         const uint64_t idle = __ballot(!active);
         const uint32_t nidle = (uint32_t)__popcll(idle);
+        n_iter++;
+        if (next >= end && !drained && nidle >= 16) {
+            uint32_t t = 0;
+            if (lane == 0) t = atomicAdd(ticket, STRICT_SLICE);
+            t = __shfl(t, 0);
+            if (t >= n) drained = true;
+            else { next = t; end = min(n, t + STRICT_SLICE); }
+        }
         if (next < end && nidle >= 16) {
+            n_refill++;
             if (!active) {
                 const uint32_t k = next + (uint32_t)__popcll(idle & below);
                 if (k < end) {
@@ -513,9 +534,10 @@ ndfl_inflate_strict_kernel(const uint32_t* w, uint64_t nwords, uint64_t nbits, c
             continue;
         }
         if (!__any(active)) {
-            if (next >= end) break;
+            if (next >= end && drained) break;
             continue;
         }
+        n_steps += 64 - nidle;
         if (active) {
             // one code-length symbol (D/decomp/Open.java's dynamic header loop, same checks)
             rd.fill(in);
@@ -561,6 +583,12 @@ ndfl_inflate_strict_kernel(const uint32_t* w, uint64_t nwords, uint64_t nbits, c
                 }
             }
         }
+    }
+    if (sst && lane == 0) {
+        atomicAdd(&sst[0], (unsigned long long)n_iter);
+        atomicAdd(&sst[1], (unsigned long long)n_refill);
+        atomicAdd(&sst[2], (unsigned long long)n_steps);
+        atomicAdd(&sst[3], 1ull);
     }
 }
 
@@ -776,8 +804,19 @@ static int inflate_run(InflateScratch& S, hipStream_t s, const uint8_t* in, uint
             hipLaunchKernelGGL(ndfl_inflate_find_kernel, dim3((uint32_t)((nthr + 256 * FIND_WPT - 1) / (256 * FIND_WPT))), dim3(256), 0, s, d_w,
                                nwords, nbits, d_qlist, d_qcount, qcap, dense ? 1u : win, dense ? 1u : period);
             INF_CHK(hipGetLastError());
-            hipLaunchKernelGGL(ndfl_inflate_strict_kernel, dim3(2048), dim3(256), 0, s, d_w, nwords, nbits,
-                               (const uint64_t*)d_qlist, (const uint32_t*)d_qcount, qcap, d_cnt, d_list);
+            static const uint32_t strict_grid = [] {
+                int dev = 0, ncu = 0, per = 0;
+                if (hipGetDevice(&dev) != hipSuccess ||
+                    hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess ||
+                    hipOccupancyMaxActiveBlocksPerMultiprocessor(&per, ndfl_inflate_strict_kernel, 256, 0) != hipSuccess ||
+                    ncu <= 0 || per <= 0)
+                    return 1280u;
+                return (uint32_t)(ncu * per);
+            }();
+            hipLaunchKernelGGL(ndfl_inflate_strict_kernel, dim3(strict_grid), dim3(256), 0, s, d_w, nwords, nbits,
+                               (const uint64_t*)d_qlist, (const uint32_t*)d_qcount, qcap, d_cnt, d_list,
+                               (uint32_t*)S.d_stats + 10,
+                               getenv("NDFL_STATS") ? (unsigned long long*)((uint32_t*)S.d_stats + 16) : nullptr);
             INF_CHK(hipGetLastError());
         }
     }
@@ -970,6 +1009,9 @@ static int inflate_run(InflateScratch& S, hipStream_t s, const uint8_t* in, uint
                 "slow-verify lanes %u fixups %u rounds %u\n", st[4], chains.size(), sorted_cand.size(),
                 (unsigned long long)S.repairs, st[0], st[1], st[2]);
         const uint64_t* t64 = (const uint64_t*)(st + 32);
+        const unsigned long long* ss = (const unsigned long long*)(st + 16);
+        fprintf(stderr, "[ndfl] strict stage: %llu waves, %llu loop trips (%llu refills), %llu lane-symbol steps\n",
+                ss[3], ss[0], ss[1], ss[2]);
         fprintf(stderr, "[ndfl] count wave-time (ms x waves, 100 MHz clock): header %.1f spec %.1f verify %.1f phases %.1f "
                 "serial %.1f record %.1f build %.1f\n", t64[0] * 1e-5, t64[1] * 1e-5, t64[2] * 1e-5, t64[3] * 1e-5,
                 t64[4] * 1e-5, t64[5] * 1e-5, t64[6] * 1e-5);

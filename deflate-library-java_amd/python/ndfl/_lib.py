@@ -5,7 +5,7 @@ import os
 
 _HERE = os.path.dirname(os.path.abspath(__file__))
 PKG_ROOT = os.path.dirname(os.path.dirname(_HERE))          # deflate-library-java_amd/
-LIB_PATH = os.path.join(PKG_ROOT, "lib", "libndfl.so")
+LIB_PATH = os.environ.get("NDFL_LIB_PATH") or os.path.join(PKG_ROOT, "lib", "libndfl.so")
 
 IN_DEVICE = 1
 OUT_DEVICE = 2
