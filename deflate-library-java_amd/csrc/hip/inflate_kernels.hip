@@ -65,7 +65,10 @@ constexpr uint64_t IN_PAD = 256;           // zero bytes after the staged input
 // in the count/emit passes' load balance than it saves here.
 constexpr uint32_t FIND_WIN_WORDS = 32768;
 constexpr uint32_t FIND_PERIOD_WORDS = 32768;
-constexpr uint32_t FIND_WPT = 8;                 // finder: input words per thread
+#ifndef NDFL_FIND_WPT
+#define NDFL_FIND_WPT 16
+#endif
+constexpr uint32_t FIND_WPT = NDFL_FIND_WPT;     // finder: input words per thread
 #ifndef NDFL_STRICT_SLICE
 #define NDFL_STRICT_SLICE 128
 #endif
