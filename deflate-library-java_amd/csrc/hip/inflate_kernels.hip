@@ -72,6 +72,9 @@ constexpr uint32_t FIND_WPT = NDFL_FIND_WPT;     // finder: input words per thre
 #ifndef NDFL_STRICT_SLICE
 #define NDFL_STRICT_SLICE 128
 #endif
+#ifndef NDFL_STRICT_REFILL
+#define NDFL_STRICT_REFILL 32     // strict stage: refill a wave once this many lanes are idle
+#endif
 constexpr uint32_t STRICT_SLICE = NDFL_STRICT_SLICE;  // strict stage: survivors per ticket
 constexpr uint32_t COUNT_WAVES = 256 * 16;       // count pass: persistent waves
 #ifndef NDFL_EMIT_WAVES_PER_SIMD
@@ -477,14 +480,14 @@ ndfl_inflate_strict_kernel(const uint32_t* w, uint64_t nwords, uint64_t nbits, c
         const uint64_t idle = __ballot(!active);
         const uint32_t nidle = (uint32_t)__popcll(idle);
         n_iter++;
-        if (next >= end && !drained && nidle >= 16) {
+        if (next >= end && !drained && nidle >= NDFL_STRICT_REFILL) {
             uint32_t t = 0;
             if (lane == 0) t = atomicAdd(ticket, STRICT_SLICE);
             t = __shfl(t, 0);
             if (t >= n) drained = true;
             else { next = t; end = min(n, t + STRICT_SLICE); }
         }
-        if (next < end && nidle >= 16) {
+        if (next < end && nidle >= NDFL_STRICT_REFILL) {
             n_refill++;
             if (!active) {
                 const uint32_t k = next + (uint32_t)__popcll(idle & below);
