@@ -66,7 +66,8 @@ def main():
     ctx = ndfl.Context(local)
     L = ndfl._lib.load()
     cap = L.ndfl_deflate_bound(n, 65536) + 64
-    comp = torch.empty(cap, dtype=torch.uint8, device="cuda")
+    # IN_PAD_BYTES of slack after the stream: the decode reads the encoder's output in place
+    comp = torch.empty(cap + ndfl.IN_PAD_BYTES, dtype=torch.uint8, device="cuda")
     RLE_DYNAMIC = 3
     DEV = ndfl.IN_DEVICE | ndfl.OUT_DEVICE
     state = {"dict_len": 0}
@@ -84,7 +85,12 @@ def main():
                                                 comp.data_ptr(), cap, DEV)
             t_c = ctx.timings()["deflate"]
             cbytes = (endbits + 7) // 8
-            r, olen, bits = ctx.inflate_raw(comp.data_ptr(), cbytes, dec.data_ptr(), dec.numel(), DEV)
+            # the NDFL_IN_PADDED contract: zero bytes after the stream (the encoder's last word is
+            # already zero-filled past its end bit; the slack is not written by it)
+            comp[cbytes:cbytes + ndfl.IN_PAD_BYTES].zero_()
+            torch.cuda.current_stream().synchronize()
+            r, olen, bits = ctx.inflate_raw(comp.data_ptr(), cbytes, dec.data_ptr(), dec.numel(),
+                                            DEV | ndfl.IN_PADDED)
             ndfl.check(r, "inflate")
         else:
             # one global stream: history halo + seam index + realignment, then range decode with the

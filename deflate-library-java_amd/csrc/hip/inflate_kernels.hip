@@ -776,12 +776,18 @@ static int inflate_run(InflateScratch& S, hipStream_t s, const uint8_t* in, uint
     const uint64_t nbits = in_len * 8;
     const uint64_t nwords = (in_len + 3) / 4;
     if (start_bit > nbits) return -1;
-    // input words: always staged into a zero-padded scratch copy, so the decode lanes' 16-byte
-    // prefetches (up to IN_PAD bytes past the end) need no bounds checks
-    INF_CHK(inf_ensure(&S.d_in, &S.d_in_cap, nwords * 4 + IN_PAD));
-    if (in_len) INF_CHK(hipMemcpyAsync(S.d_in, in, in_len, (flags & 1u) ? hipMemcpyDeviceToDevice : hipMemcpyHostToDevice, s));
-    INF_CHK(hipMemsetAsync((char*)S.d_in + in_len, 0, nwords * 4 + IN_PAD - in_len, s));
-    const uint32_t* d_w = (const uint32_t*)S.d_in;
+    // input words: staged into a zero-padded scratch copy, so the decode lanes' 16-byte prefetches
+    // (up to IN_PAD bytes past the end) need no bounds checks -- unless the caller says its device
+    // buffer already is one (NDFL_IN_PADDED: 16-byte aligned, IN_PAD zero bytes after the data),
+    // in which case it is read in place
+    const bool in_place = in_len && (flags & 1u) && (flags & 8u) && ((uintptr_t)in & 15u) == 0;
+    const uint32_t* d_w = (const uint32_t*)in;
+    if (!in_place) {
+        INF_CHK(inf_ensure(&S.d_in, &S.d_in_cap, nwords * 4 + IN_PAD));
+        if (in_len) INF_CHK(hipMemcpyAsync(S.d_in, in, in_len, (flags & 1u) ? hipMemcpyDeviceToDevice : hipMemcpyHostToDevice, s));
+        INF_CHK(hipMemsetAsync((char*)S.d_in + in_len, 0, nwords * 4 + IN_PAD - in_len, s));
+        d_w = (const uint32_t*)S.d_in;
+    }
     if (!S.d_stats) INF_CHK(hipMalloc(&S.d_stats, 256));
     INF_CHK(hipMemsetAsync(S.d_stats, 0, 256, s));
     if (!S.ev[0]) for (auto& e : S.ev) INF_CHK(hipEventCreate(&e));

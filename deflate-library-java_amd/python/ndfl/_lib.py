@@ -10,6 +10,8 @@ LIB_PATH = os.environ.get("NDFL_LIB_PATH") or os.path.join(PKG_ROOT, "lib", "lib
 IN_DEVICE = 1
 OUT_DEVICE = 2
 DICT_DEFERRED = 4
+IN_PADDED = 8          # NDFL_IN_PADDED: device input read in place (aligned, IN_PAD_BYTES zeros after)
+IN_PAD_BYTES = 256
 NO_END = (1 << 64) - 1
 
 STRATEGIES = {"LITERAL_STATIC": 0, "LITERAL_DYNAMIC": 1, "RLE_STATIC": 2, "RLE_DYNAMIC": 3,

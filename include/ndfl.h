@@ -51,6 +51,10 @@ enum ndfl_strategy {
 #define NDFL_IN_DEVICE   1u    /* input pointers (data, hist) are device memory */
 #define NDFL_OUT_DEVICE  2u    /* output pointer is device memory */
 #define NDFL_DICT_DEFERRED 4u  /* ndfl_inflate_range: window bytes are written later (see resolve) */
+#define NDFL_IN_PADDED   8u    /* ndfl_inflate / ndfl_inflate_range with NDFL_IN_DEVICE: the input is
+                                 16-byte aligned and followed by NDFL_IN_PAD_BYTES readable zero bytes,
+                                 so it is decoded in place (no staging copy); otherwise ignored */
+#define NDFL_IN_PAD_BYTES 256u
 
 typedef struct ndfl_ctx ndfl_ctx;
 

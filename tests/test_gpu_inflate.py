@@ -155,3 +155,4 @@ def test_corrupted_lz77_streams_prefix_exact(ctx):
             if rng.random() < 0.3:
                 c = c[:rng.randrange(len(c) // 2, len(c))]
             check_same(ctx, bytes(c))
+
