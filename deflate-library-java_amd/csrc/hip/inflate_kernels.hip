@@ -508,26 +508,32 @@ ndfl_inflate_strict_kernel(const uint32_t* w, uint64_t nwords, uint64_t nbits, c
                         for (int j = 0; j < 19; j++)
                             if ((uint32_t)j < numCl) cl[CLO[j]] = rd.get(in, 3);
                         // the stage-1 test guarantees a complete code: the runs fill all 128 entries
-                        uint32_t pos = 0;
-#pragma unroll 1
-                        for (uint32_t l = 1; l < 8; l++) {
-                            const uint32_t run = 128u >> l;
+                        // canonical (length, symbol) order without a pass per length: each length's
+                        // first entry is the byte-wise exclusive prefix sum of count x run, all seven
+                        // held in one u64 (byte l = entries taken by lengths < l, at most 128)
+                        uint64_t wp = 0;
 #pragma unroll
-                            for (int sy = 0; sy < 19; sy++) {
-                                if (cl[sy] == l) {
-                                    const uint32_t v = ((uint32_t)sy | (l << 5)) * 0x01010101u;
-                                    if (run >= 16) {
-                                        for (uint32_t r = 0; r < run; r += 16) *(uint4*)(tab + pos + r) = make_uint4(v, v, v, v);
-                                    } else if (run == 8) {
-                                        *(uint2*)(tab + pos) = make_uint2(v, v);
-                                    } else if (run == 4) {
-                                        *(uint32_t*)(tab + pos) = v;
-                                    } else if (run == 2) {
-                                        *(uint16_t*)(tab + pos) = (uint16_t)v;
-                                    } else {
-                                        tab[pos] = (uint8_t)v;
-                                    }
-                                    pos += run;
+                        for (int sy = 0; sy < 19; sy++)
+                            wp += cl[sy] ? ((uint64_t)(128u >> cl[sy]) << (8 * cl[sy])) : 0ull;
+                        uint64_t off = (wp * 0x0101010101010101ull) << 8;
+#pragma unroll
+                        for (int sy = 0; sy < 19; sy++) {
+                            const uint32_t l = cl[sy];
+                            if (l) {
+                                const uint32_t sh = 8 * l, run = 128u >> l;
+                                const uint32_t pos = (uint32_t)(off >> sh) & 255u;
+                                off += (uint64_t)run << sh;
+                                const uint32_t v = ((uint32_t)sy | (l << 5)) * 0x01010101u;
+                                if (run >= 16) {
+                                    for (uint32_t r = 0; r < run; r += 16) *(uint4*)(tab + pos + r) = make_uint4(v, v, v, v);
+                                } else if (run == 8) {
+                                    *(uint2*)(tab + pos) = make_uint2(v, v);
+                                } else if (run == 4) {
+                                    *(uint32_t*)(tab + pos) = v;
+                                } else if (run == 2) {
+                                    *(uint16_t*)(tab + pos) = (uint16_t)v;
+                                } else {
+                                    tab[pos] = (uint8_t)v;
                                 }
                             }
                         }
