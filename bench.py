@@ -155,7 +155,7 @@ def main():
 
     cpu = None
     if rank == 0 and not args.no_cpu:
-        cpu = cpu_baseline(data, args.cpu_sample)
+        cpu = cpu_baseline(data, args.cpu_sample, comp if world == 1 else None)
 
     if rank == 0:
         line = {
@@ -185,6 +185,7 @@ def main():
                          "traffic_source": traffic_src,
                          "algorithmic_bytes_per_launch": alg, "avg_kernel_ms": round(kms, 3)},
             "cpu_baseline": cpu,
+            "bit_exact": None if cpu is None else cpu.get("bit_exact"),
         }
         print(json.dumps(line), flush=True)
     if dist is not None:
@@ -207,21 +208,71 @@ def pmc_traffic(kernel, n):
     return fb + wb, f"profiles/r01_traffic.json (fetch {fb} B + write {wb} B per launch)"
 
 
-def cpu_baseline(data_dev, sample_bytes):
-    """The oracle (C restatement of the reference algorithm, 1 thread) on a bounded sample of the
-    same workload: compress `sample_bytes` of the corpus, decompress the result; same metric."""
+def _cpu_model():
+    try:
+        for line in open("/proc/cpuinfo"):
+            if line.startswith("model name"):
+                return line.split(":", 1)[1].strip()
+    except OSError:
+        pass
+    return None
+
+
+def _append_final_empty_block(comp, nbits):
+    """A non-final stream of nbits bits + a final fixed-Huffman block holding only end-of-block
+    (bits 1, 01, 0000000): a valid stream with the same decode work."""
+    b = bytearray(comp[:(nbits + 7) // 8]) + b"\0\0"
+    v = 0b011 << (nbits % 8)
+    i = nbits // 8
+    b[i] |= v & 0xFF
+    b[i + 1] |= (v >> 8) & 0xFF
+    return bytes(b[:(nbits + 10 + 7) // 8])
+
+
+def cpu_baseline(data_dev, sample_bytes, gpu_comp=None):
+    """The oracle (C restatement of the reference algorithm) on a bounded sample of the same
+    workload: compress the first `sample_bytes` of the corpus as the first chunks of the stream
+    (non-final, exactly what the GPU wrote for them), decompress that (closed by an empty final
+    block); same metric.  1 thread; beside it the compress leg chunk-parallel on all the box's cores
+    (threads over 64 KiB-aligned pieces, each with its 32 KiB history).  The GPU stream's first
+    bits are compared with the oracle's: `bit_exact`."""
+    import hashlib
     import oracle_lib as O
+    from concurrent.futures import ThreadPoolExecutor
     m = min(sample_bytes, data_dev.numel())
+    m -= m % 65536
     host = data_dev[:m].cpu().numpy().tobytes()
     t0 = time.perf_counter()
-    comp = O.deflate(host)
+    comp, nbits = O.deflate_chunks(b"", host, final=False)
     t1 = time.perf_counter()
-    reason, out, _ = O.inflate(comp, out_cap=m + 64)
+    stream = _append_final_empty_block(comp, nbits)
+    reason, out, bits = O.inflate(stream, out_cap=m + 64)
     t2 = time.perf_counter()
-    assert reason is None and out == host
+    assert reason is None and out == host and bits == nbits + 10
+    exact = None
+    if gpu_comp is not None:
+        nb = nbits // 8
+        g = gpu_comp[:nb + 1].cpu().numpy().tobytes()
+        tail_mask = (1 << (nbits % 8)) - 1
+        exact = g[:nb] == comp[:nb] and (g[nb] & tail_mask) == (comp[nb] & tail_mask if nbits % 8 else 0)
+    cores = max(1, min(16, os.cpu_count() or 1))          # the GPU box's CPU share is 16
+    step = max(65536, (m // cores) // 65536 * 65536)
+    pieces = [(max(0, o - 32768), o, min(m, o + step)) for o in range(0, m, step)]
+    tp0 = time.perf_counter()
+    with ThreadPoolExecutor(cores) as ex:
+        list(ex.map(lambda p: O.deflate_chunks(host[p[0]:p[1]], host[p[1]:p[2]], final=False), pieces))
+    tp1 = time.perf_counter()
     return {"value": round((m + len(comp)) / (t2 - t0) / MIB, 2), "unit": "MiB/s", "cores": 1, "kind": "port",
-            "sample": f"first {m >> 20} MiB of rank 0's shard: oracle compress {t1 - t0:.2f}s + decompress {t2 - t1:.2f}s",
-            "compress_MiBps": round(m / (t1 - t0) / MIB, 2), "decompress_input_MiBps": round(len(comp) / (t2 - t1) / MIB, 2)}
+            "sample": f"first {m >> 20} MiB of rank 0's shard, as the first {m // 65536} chunks of the stream: "
+                      f"oracle compress {t1 - t0:.2f}s + decompress {t2 - t1:.2f}s (1 thread)",
+            "compress_MiBps": round(m / (t1 - t0) / MIB, 2),
+            "decompress_input_MiBps": round(len(comp) / (t2 - t1) / MIB, 2),
+            "all_cores": {"cores": cores, "compress_MiBps": round(m / (tp1 - tp0) / MIB, 2),
+                          "note": "chunk-parallel oracle compress (threads over 64 KiB-aligned pieces with their "
+                                  "32 KiB history); a single DEFLATE stream decodes serially on the CPU"},
+            "host": {"nproc": os.cpu_count(), "cpu_model": _cpu_model()},
+            "bit_exact": exact, "bits_compared": nbits,
+            "sha256_prefix": hashlib.sha256(comp[:nbits // 8]).hexdigest()}
 
 
 if __name__ == "__main__":

@@ -264,7 +264,8 @@ int ndfl_deflate_chunks(ndfl_ctx* c, const uint8_t* hist, uint32_t hist_len, uin
     if (prof) { HIPCHK(hipMalloc(&a.prof, (size_t)nch * 128)); HIPCHK(hipMemsetAsync(a.prof, 0, (size_t)nch * 128, s)); }
     a.hist_out = nullptr; a.codes = nullptr; a.chunk_off = nullptr;
     // split pipeline by default (deflate_split.hip); NDFL_DEFLATE_FUSED=1 selects the one-kernel encoder
-    static const bool fused = getenv("NDFL_DEFLATE_FUSED") != nullptr && atoi(getenv("NDFL_DEFLATE_FUSED")) != 0;
+    const char* fenv = getenv("NDFL_DEFLATE_FUSED");      // read per call (tests switch it)
+    const bool fused = fenv != nullptr && atoi(fenv) != 0;
     const bool split = !fused && !prof;
     uint64_t* d_total = nullptr;
     if (split) {
@@ -931,10 +932,12 @@ int ndfl_inflate_range(ndfl_ctx* c, const uint8_t* in, uint64_t in_len, uint64_t
     if (!c || !out_len || !consumed_bits || (!in && in_len) || (!out && (dict_len || out_cap))) return NDFL_E_ARG;
     if (dict_len > 32768 || start_bit > in_len * 8 || end_bit <= start_bit) return NDFL_E_ARG;
     const bool deferred = (flags & NDFL_DICT_DEFERRED) != 0;
+    const bool partial = (flags & NDFL_IN_PARTIAL) != 0;
     if (deferred && !(flags & NDFL_OUT_DEVICE)) return NDFL_E_ARG;
+    if (partial && (deferred || end_bit != UINT64_MAX)) return NDFL_E_ARG;
     HIPCHK(hipSetDevice(c->device));
     return inflate_run(c->inf, c->stream, in, in_len, start_bit, end_bit, out, dict_len, out_cap, out_len,
-                       consumed_bits, flags, deferred, &c->last_ms);
+                       consumed_bits, flags, deferred, &c->last_ms, partial);
 }
 
 int ndfl_inflate_resolve(ndfl_ctx* c, uint64_t* n_reemitted) {

@@ -27,6 +27,7 @@
 #pragma once
 #include "kraft_bits.hpp"
 #include "ndfl_common.hpp"
+#include "../../../include/ndfl.h"
 #include <vector>
 #include <algorithm>
 #include <unordered_map>
@@ -42,6 +43,7 @@ constexpr uint32_t SEG_CAP = 256;          // candidates kept per finder segment
 constexpr uint64_t NONE = ~0ull;
 
 enum : uint32_t { ST_BOUNDARY = 0, ST_FINAL = 1, ST_ERROR = 2 };
+constexpr int NEED_INPUT = 64;             // NDFL_NEED_INPUT (include/ndfl.h): partial-input decode stopped
 enum : int { R_UEOS = 1, R_RESERVED_BLOCK_TYPE, R_LEN_MISMATCH, R_UNDER_FULL, R_OVER_FULL, R_NO_PREV,
              R_CL_OVER_FULL, R_EOB_ZERO, R_RESERVED_LEN, R_RESERVED_DIST, R_EMPTY_DIST, R_COPY_BEFORE,
              R_INTERNAL = 100 };
@@ -60,6 +62,10 @@ __device__ __forceinline__ void dist_base(uint32_t d, uint32_t& base, uint32_t& 
 }
 
 constexpr uint64_t IN_PAD = 256;           // zero bytes after the staged input
+static_assert(IN_PAD == NDFL_IN_PAD_BYTES, "kernel pad and the NDFL_IN_PADDED contract must agree");
+// the furthest unchecked read: In::ld4 / make_rb clamp 16-byte group indices at (nwords + 3) / 4 + 1,
+// so a lane reads at most ((nwords + 3) / 4 + 2) * 16 <= nwords * 4 + 44 bytes
+static_assert(3 * 4 + 2 * 16 + 16 <= IN_PAD, "16-byte prefetch clamp must stay inside the zero padding");
 // header finder scan pattern (32-bit words): FIND_WIN_WORDS of every FIND_PERIOD_WORDS.  Dense
 // (every position) by default: sparse windows make chains span several blocks, which costs more
 // in the count/emit passes' load balance than it saves here.
@@ -512,14 +518,21 @@ ndfl_inflate_strict_kernel(const uint32_t* w, uint64_t nwords, uint64_t nbits, c
                         // first entry is the byte-wise exclusive prefix sum of count x run, all seven
                         // held in one u64 (byte l = entries taken by lengths < l, at most 128)
                         uint64_t wp = 0;
+                        uint32_t kraft = 0;
 #pragma unroll
-                        for (int sy = 0; sy < 19; sy++)
+                        for (int sy = 0; sy < 19; sy++) {
                             wp += cl[sy] ? ((uint64_t)(128u >> cl[sy]) << (8 * cl[sy])) : 0ull;
+                            kraft += cl[sy] ? (128u >> cl[sy]) : 0u;
+                        }
+                        // the byte-wise sums only hold for a complete code (every prefix <= 128): a
+                        // stage-1 regression must not let an incomplete code scribble over the
+                        // neighbouring lanes' tables, so such a survivor is dropped here
+                        const bool complete = kraft == 128u;
                         uint64_t off = (wp * 0x0101010101010101ull) << 8;
 #pragma unroll
                         for (int sy = 0; sy < 19; sy++) {
                             const uint32_t l = cl[sy];
-                            if (l) {
+                            if (l && complete) {
                                 const uint32_t sh = 8 * l, run = 128u >> l;
                                 const uint32_t pos = (uint32_t)(off >> sh) & 255u;
                                 off += (uint64_t)run << sh;
@@ -538,7 +551,7 @@ ndfl_inflate_strict_kernel(const uint32_t* w, uint64_t nwords, uint64_t nbits, c
                             }
                         }
                         i = 0; runVal = -1; litK = 0; distK = 0; ones = 0; other = 0; eob = 0; d0 = 0; d31 = 0;
-                        active = true;
+                        active = complete;
                     }
                 }
             }
@@ -629,6 +642,8 @@ struct ChainRes {
     uint32_t reason;      // for ST_ERROR
     uint32_t next;        // count pass, ST_BOUNDARY at a candidate: its index in the candidate list
     uint32_t pad;
+    uint64_t bnd_bit;     // emit pass, ST_ERROR: start bit of the block the error is in
+    uint64_t bnd_cnt;     //   and the chain's output bytes before that block (partial-input decodes)
 };
 
 struct EmitChain {
@@ -771,7 +786,7 @@ static int resolve_rounds(InflateScratch& S, hipStream_t s, uint8_t* d_out, uint
 //             chains) are recorded and re-emitted by inflate_resolve once it is written
 static int inflate_run(InflateScratch& S, hipStream_t s, const uint8_t* in, uint64_t in_len, uint64_t start_bit,
                        uint64_t end_bit, uint8_t* out, uint64_t dict_len, uint64_t out_cap, uint64_t* out_len,
-                       uint64_t* consumed_bits, uint32_t flags, bool deferred, double* last_ms) {
+                       uint64_t* consumed_bits, uint32_t flags, bool deferred, double* last_ms, bool partial = false) {
     using namespace inf;
     *out_len = 0;
     *consumed_bits = 0;
@@ -1098,6 +1113,14 @@ static int inflate_run(InflateScratch& S, hipStream_t s, const uint8_t* in, uint
     // first error in stream order (the emit pass also checks the dictionary bound exactly)
     for (uint32_t k = 0; k < nch; k++) {
         if (er[k].status == ST_ERROR) {
+            if (partial && er[k].reason == R_UEOS) {
+                // the input is a prefix of the stream: stop at the last block boundary reached
+                const uint64_t produced = chains[k].out_off - dict_len + er[k].bnd_cnt;
+                if (!direct && produced) INF_CHK(hipMemcpy(out + dict_len, d_out + dict_len, produced, hipMemcpyDeviceToHost));
+                *out_len = produced;
+                *consumed_bits = er[k].bnd_bit;
+                return NEED_INPUT;
+            }
             const uint64_t produced = chains[k].out_off - dict_len + er[k].out_count;
             if (!direct && produced) INF_CHK(hipMemcpy(out + dict_len, d_out + dict_len, produced, hipMemcpyDeviceToHost));
             *out_len = produced;

@@ -981,6 +981,7 @@ ndfl_inflate_count_wave_kernel(const uint32_t* w, uint64_t nwords, uint64_t nbit
         ChainRes o;
         o.end_bit = endpos; o.out_count = total; o.status = status; o.reason = reason;
         o.next = next_idx; o.pad = 0;
+        o.bnd_bit = 0; o.bnd_cnt = 0;
         res[c] = o;
         if (stats) {
             atomicAdd(&stats[0], nslow); atomicAdd(&stats[1], nfix); atomicAdd(&stats[2], nround);
@@ -1025,8 +1026,10 @@ ndfl_inflate_emit_wave_kernel(const uint32_t* w, uint64_t nwords, uint64_t nbits
     uint64_t endpos = ch.start_bit;
     uint32_t nslow = 0, nfix = 0;
     uint32_t rec = ch.slot < pool.nslot ? pool.head[ch.slot] : NOREC;
+    uint64_t bnd_bit = cur, bnd_out = base;     // start of the current block (partial-input decodes)
     for (int blk = 0;; blk++) {
         if (blk > 0 && cur == ch.end_bit) { status = ST_BOUNDARY; endpos = cur; break; }
+        bnd_bit = cur; bnd_out = base;
         for (uint32_t s = (uint32_t)lane; s < 320; s += 64) S.lens[s] = 0;
         __syncthreads();
         if (lane == 0) parse_hdr(in, cur, S);
@@ -1168,6 +1171,7 @@ ndfl_inflate_emit_wave_kernel(const uint32_t* w, uint64_t nwords, uint64_t nbits
         ChainRes o;
         o.end_bit = endpos; o.out_count = base - ch.out_off; o.status = status; o.reason = reason;
         o.next = 0xFFFFFFFFu; o.pad = 0;
+        o.bnd_bit = bnd_bit; o.bnd_cnt = bnd_out - ch.out_off;
         res[ci] = o;
     }
     }

@@ -17,7 +17,7 @@ import enum
 import io
 
 from . import _lib
-from ._lib import IN_DEVICE, OUT_DEVICE, DICT_DEFERRED, IN_PADDED, IN_PAD_BYTES, NO_END, STRATEGIES, NdflError, check, load, reason_name
+from ._lib import IN_DEVICE, OUT_DEVICE, DICT_DEFERRED, IN_PADDED, IN_PAD_BYTES, IN_PARTIAL, NEED_INPUT, NO_END, STRATEGIES, NdflError, check, load, reason_name
 
 __all__ = ["Context", "Reason", "DataFormatException", "Lz77Huffman", "Uncompressed", "MultiStrategy", "BinarySplit", "DeflaterOutputStream", "InflaterInputStream",
            "GzipMetadata", "GzipOutputStream", "GzipInputStream", "ZlibMetadata", "ZlibOutputStream",

@@ -12,6 +12,8 @@ OUT_DEVICE = 2
 DICT_DEFERRED = 4
 IN_PADDED = 8          # NDFL_IN_PADDED: device input read in place (aligned, IN_PAD_BYTES zeros after)
 IN_PAD_BYTES = 256
+IN_PARTIAL = 16        # NDFL_IN_PARTIAL: the input is a prefix of the stream
+NEED_INPUT = 64        # NDFL_NEED_INPUT: a partial-input decode stopped at a block boundary
 NO_END = (1 << 64) - 1
 
 STRATEGIES = {"LITERAL_STATIC": 0, "LITERAL_DYNAMIC": 1, "RLE_STATIC": 2, "RLE_DYNAMIC": 3,

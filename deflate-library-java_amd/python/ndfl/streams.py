@@ -126,41 +126,141 @@ class DeflaterOutputStream:
         self.close()
 
 
+class _Pushback:
+    """Mark support for a non-seekable underlying stream: the bytes the inflater read past the end of
+    the DEFLATE data are pushed back and served first -- the BufferedInputStream that
+    GzipInputStream / ZlibInputStream wrap around a non-markable stream (D/GzipInputStream.java:41-42,
+    D/ZlibInputStream.java:39-40)."""
+
+    def __init__(self, raw):
+        self._raw = raw
+        self._back = b""
+
+    def unread(self, b):
+        self._back = bytes(b) + self._back
+
+    def read(self, n=-1):
+        if n is None or n < 0:
+            rest = self._raw.read()
+            out, self._back = self._back + (rest or b""), b""
+            return out
+        out = self._back[:n]
+        self._back = self._back[n:]
+        while len(out) < n:
+            b = self._raw.read(n - len(out))
+            if not b:
+                break
+            out += b
+        return out
+
+    def close(self):
+        self._raw.close()
+
+
+def _markable(f):
+    return hasattr(f, "unread") or (hasattr(f, "seek") and hasattr(f, "tell") and _seekable(f))
+
+
 class InflaterInputStream:
-    """D/InflaterInputStream.java:26-181.  The whole remaining underlying stream is handed to the GPU
-    decoder on the first read; decoded bytes are then served with the reference's read contract:
-    read(b, off, len) returns -1..len and 0 only when len == 0; -1 at end of stream."""
+    """D/InflaterInputStream.java:26-181 over Open (D/decomp/Open.java).  The underlying stream is
+    read incrementally: batches of at least `inBufLen` (and by default 64 MiB) compressed bytes are
+    decoded on the GPU with ndfl_inflate_range(NDFL_IN_PARTIAL), which stops at the last block
+    boundary the batch completes; the decode continues from that bit with more input and the last
+    32 KiB of output as the window.  Memory stays bounded by the batch, whatever the stream length,
+    and pipes / sockets work.  read(b, off, len) returns -1..len and 0 only when len == 0; -1 at end
+    of stream.  A DataFormatException is raised once the bytes decoded before the error have been
+    served (the reference raises it from the read call that reaches the error); an OSError from the
+    underlying stream is sticky (StickyException, :152-159)."""
+
+    BATCH = 64 << 20
+    WINDOW = 32768
 
     def __init__(self, inp, endExactly=False, inBufLen=16 * 1024, context=None):
         if inp is None:
             raise TypeError("in")
         if inBufLen <= 0:
             raise ValueError("Non-positive input buffer size")
-        if endExactly and not (hasattr(inp, "seek") and hasattr(inp, "tell") and _seekable(inp)):
+        if endExactly and not _markable(inp):
             raise ValueError("Input stream not markable, cannot support detachment")
         self._in = inp
         self._end_exactly = endExactly
         self._ctx = _ctx(context)
         self._state = "open"
-        self._buf = None
+        self._batch = max(inBufLen, self.BATCH)
+        self._ibuf = bytearray()      # unconsumed input; its first byte holds bit self._bit of the stream
+        self._bit = 0
+        self._eof = False             # the underlying stream is exhausted
+        self._final = False           # the final block has been decoded
+        self._window = b""            # last <= 32 KiB of output (the dictionary of the next batch)
+        self._buf = b""               # decoded bytes not yet served
         self._pos = 0
         self._error = None
         self._sticky = None
+        self._on_batch = None         # container hook: called with every decoded batch (CRC / Adler)
 
-    def _decode(self):
-        from . import DataFormatException, Reason
-        start = self._in.tell() if self._end_exactly else 0
+    def _read_more(self, want):
         try:
-            data = self._in.read()
+            while len(self._ibuf) < want and not self._eof:
+                b = self._in.read(want - len(self._ibuf))
+                if not b:
+                    self._eof = True
+                else:
+                    self._ibuf += b
         except OSError as e:
             self._sticky = e
             raise
-        reason, out, bits = self._ctx.inflate(data)
-        self._buf = out
-        if reason is not None:
-            self._error = DataFormatException(reason)
-        elif self._end_exactly:
-            self._in.seek(start + (bits + 7) // 8)
+
+    def _fill(self):
+        """Decode the next batch into self._buf (empty only at end of stream or on an error)."""
+        from . import DataFormatException, Reason
+        want = self._batch
+        while True:
+            self._read_more(want)
+            flags = 0 if self._eof else _lib.IN_PARTIAL
+            n = len(self._ibuf)
+            src = ctypes.create_string_buffer(bytes(self._ibuf), max(1, n))
+            wl = len(self._window)
+            cap = wl + 4 * n + 65536
+            while True:
+                out = ctypes.create_string_buffer(self._window, max(1, cap))
+                r, olen, bits = self._ctx.inflate_range_raw(ctypes.addressof(src), n, self._bit, None,
+                                                            ctypes.addressof(out), wl, cap, flags)
+                if r == _lib.E_CAPACITY:
+                    cap = wl + olen + 16
+                    continue
+                break
+            if r == _lib.NEED_INPUT and olen == 0 and bits == self._bit:
+                want = len(self._ibuf) + self._batch        # no block completed: read more
+                continue
+            if r < 0 or (r > len(_lib.REASONS) and r != _lib.NEED_INPUT):
+                check(r, "ndfl_inflate_range")
+            data = out.raw[wl:wl + olen]
+            self._window = (self._window + data)[-self.WINDOW:]
+            self._buf, self._pos = data, 0
+            if data and self._on_batch is not None:
+                self._on_batch(data)
+            if r == _lib.NEED_INPUT:
+                del self._ibuf[:bits // 8]
+                self._bit = bits % 8
+                return
+            if r == 0:
+                self._final = True
+                used = (bits + 7) // 8          # a byte with some bits consumed counts as consumed
+                rest = bytes(self._ibuf[used:])
+                self._ibuf = bytearray()
+                if self._end_exactly and rest:   # Open.finish (D/decomp/Open.java:113-124)
+                    if hasattr(self._in, "unread"):
+                        self._in.unread(rest)
+                    else:
+                        self._in.seek(-len(rest), os.SEEK_CUR)
+                return
+            self._error = DataFormatException(Reason(r - 1))
+            return
+
+    def _ensure(self):
+        # (a batch may end at a boundary after blocks with no output, e.g. empty stored blocks)
+        while self._pos == len(self._buf) and not self._final and self._error is None:
+            self._fill()
 
     def read(self, b=None, off=0, length=None):
         """read() -> int byte or -1;  read(bytearray, off, len) -> count or -1."""
@@ -168,9 +268,8 @@ class InflaterInputStream:
             raise RuntimeError("Stream already closed")
         if self._sticky is not None:
             raise self._sticky
-        if self._buf is None:
-            self._decode()
         if b is None:
+            self._ensure()
             if self._pos < len(self._buf):
                 v = self._buf[self._pos]
                 self._pos += 1
@@ -182,24 +281,36 @@ class InflaterInputStream:
             length = len(b) - off
         if off < 0 or length < 0 or off + length > len(b):
             raise IndexError("Range out of bounds")
-        avail = len(self._buf) - self._pos
-        if avail == 0 and length > 0 and self._error is not None:
-            raise self._error
-        n = min(avail, length)
-        b[off:off + n] = self._buf[self._pos:self._pos + n]
-        self._pos += n
-        if n == 0 and self._error is None and avail == 0:
-            return -1          # also for len == 0 at end of stream (D/decomp/Open.java:109)
-        return n
+        total = 0
+        while total < length:
+            self._ensure()
+            avail = len(self._buf) - self._pos
+            if avail == 0:
+                break
+            k = min(avail, length - total)
+            b[off + total:off + total + k] = self._buf[self._pos:self._pos + k]
+            self._pos += k
+            total += k
+        if total == 0 and length > 0:
+            if self._error is not None:
+                raise self._error
+            return -1
+        if total == 0 and self._final and self._pos == len(self._buf):
+            return -1          # len == 0 at end of stream (D/decomp/Open.java:109)
+        return total
 
     def readall(self):
-        if self._buf is None:
-            self._decode()
-        out = self._buf[self._pos:]
-        self._pos = len(self._buf)
+        parts = []
+        while True:
+            self._ensure()
+            if self._pos < len(self._buf):
+                parts.append(self._buf[self._pos:])
+                self._pos = len(self._buf)
+                continue
+            break
         if self._error is not None:
             raise self._error
-        return out
+        return b"".join(parts)
 
     def close(self):
         if self._state != "closed" and self._in is not None:
@@ -367,16 +478,26 @@ class GzipOutputStream:
 
 
 class GzipInputStream:
-    """D/GzipInputStream.java:22-100.  Single member; trailing bytes ignored."""
+    """D/GzipInputStream.java:22-100.  Single member; trailing bytes ignored.  The CRC-32 and length
+    are updated on the GPU over every batch the inflater decodes."""
 
     def __init__(self, inp, context=None):
+        if inp is None:
+            raise TypeError("in")
         self._ctx = _ctx(context)
         self.metadata = GzipMetadata.read(inp, self._ctx)
+        if not _markable(inp):
+            inp = _Pushback(inp)
         self._raw = inp
         self._inf = InflaterInputStream(inp, True, context=self._ctx)
+        self._inf._on_batch = self._update
         self._done = False
         self._crc = 0
         self._len = 0
+
+    def _update(self, data):
+        self._crc = self._ctx.crc32(data, self._crc)
+        self._len += len(data)
 
     def getMetadata(self):
         return self.metadata
@@ -395,8 +516,6 @@ class GzipInputStream:
         if self._done:
             return b""
         out = self._inf.readall()
-        self._crc = self._ctx.crc32(out)
-        self._len = len(out)
         self._done = True
         self._trailer()
         return out
@@ -404,11 +523,6 @@ class GzipInputStream:
     def read(self, b=None, off=0, length=None):
         if self._done:
             return -1
-        if self._inf._buf is None:
-            self._inf._decode()
-            if self._inf._error is None:
-                self._crc = self._ctx.crc32(self._inf._buf)
-                self._len = len(self._inf._buf)
         r = self._inf.read(b, off, length)
         if r == -1:
             self._done = True
@@ -539,17 +653,23 @@ class ZlibOutputStream:
 class ZlibInputStream:
     """D/ZlibInputStream.java:22-100: header, inflate with exact end, big-endian Adler-32 trailer
     (EOF -> UNEXPECTED_END_OF_STREAM, mismatch -> DECOMPRESSED_CHECKSUM_MISMATCH).  A preset
-    dictionary is recorded but not applied, as in the reference."""
+    dictionary is recorded but not applied, as in the reference.  Adler-32 on the GPU per batch."""
 
     def __init__(self, inp, context=None):
         if inp is None:
             raise TypeError("in")
         self._ctx = _ctx(context)
         self.metadata = ZlibMetadata.read(inp)
+        if not _markable(inp):
+            inp = _Pushback(inp)
         self._raw = inp
         self._inf = InflaterInputStream(inp, True, context=self._ctx)
+        self._inf._on_batch = self._update
         self._done = False
         self._adler = 1
+
+    def _update(self, data):
+        self._adler = self._ctx.adler32(data, self._adler)
 
     def getMetadata(self):
         return self.metadata
@@ -566,7 +686,6 @@ class ZlibInputStream:
         if self._done:
             return b""
         out = self._inf.readall()
-        self._adler = self._ctx.adler32(out) if out else 1
         self._done = True
         self._trailer()
         return out
@@ -574,10 +693,6 @@ class ZlibInputStream:
     def read(self, b=None, off=0, length=None):
         if self._done:
             return -1
-        if self._inf._buf is None:
-            self._inf._decode()
-            if self._inf._error is None:
-                self._adler = self._ctx.adler32(self._inf._buf) if self._inf._buf else 1
         r = self._inf.read(b, off, length)
         if r == -1:
             self._done = True

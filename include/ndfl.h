@@ -55,6 +55,16 @@ enum ndfl_strategy {
                                  16-byte aligned and followed by NDFL_IN_PAD_BYTES readable zero bytes,
                                  so it is decoded in place (no staging copy); otherwise ignored */
 #define NDFL_IN_PAD_BYTES 256u
+#define NDFL_IN_PARTIAL  16u   /* ndfl_inflate_range: `in` is a prefix of the stream (more input may
+                                 follow); see NDFL_NEED_INPUT */
+
+/* ndfl_inflate_range with NDFL_IN_PARTIAL: the decode ran out of input inside a block.  Nothing is
+ * reported for that block: *consumed_bits is its start (the last block boundary reached) and
+ * *out_len the bytes decoded before it.  The caller continues from there with more input and the
+ * last <= 32 KiB of output as the window -- Open.read's incremental refill
+ * (D/decomp/Open.java:137-192) at block granularity.  Not a Reason: at true end of input the
+ * caller decodes without the flag and gets UNEXPECTED_END_OF_STREAM. */
+#define NDFL_NEED_INPUT  64
 
 typedef struct ndfl_ctx ndfl_ctx;
 
@@ -162,6 +172,9 @@ int ndfl_inflate(ndfl_ctx* ctx, const uint8_t* in, uint64_t in_len, uint8_t* out
 
 /*
  * Decompress the block-aligned bit range [start_bit, end_bit) of one raw DEFLATE stream: one GPU's
+ * shard of a stream decoded across GPUs, or one batch of a stream read incrementally
+ * (NDFL_IN_PARTIAL, end_bit UINT64_MAX: InflaterInputStream's bounded input buffer,
+ * D/InflaterInputStream.java:96-106).  For the multi-GPU case: one GPU's
  * shard of a stream decoded across GPUs.  Same decoder as ndfl_inflate, i.e.
  * Open.read (D/decomp/Open.java:83-124), started at a block boundary with the reference's
  * dictionary state (the 32 KiB ring, :592-603) given by the caller instead of built up.

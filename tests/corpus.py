@@ -139,3 +139,67 @@ def mixed_bytes(n_total, seed):
             parts.append(bytes(rng.choice(list(b"abcde \n"), ln).astype(np.uint8)))
         size += ln
     return b"".join(parts)[:n_total]
+
+
+def c2_gzip(target_comp=64 << 20, seed=0xC2):
+    """Config 2: one gzip member whose DEFLATE stream alternates stored blocks (random
+    bytes, random lengths 1..65535, plus the empty stored blocks of each sync flush) and fixed-Huffman
+    blocks (about 64 KiB of enwik-style text, greedily LZ77-coded with dist 1..32768, len 3..258 by
+    zlib's Z_FIXED strategy), until the compressed size reaches `target_comp`.  Pieces are
+    byte-aligned by Z_SYNC_FLUSH, so their concatenation is one valid stream.
+    Returns (gz_bytes, raw_deflate_bytes, data).  Deterministic (numpy PCG64 + zlib 1.2.11)."""
+    import zlib
+    import numpy as np
+    rng = np.random.default_rng(seed)
+    text = c3_text(8 << 20, seed=seed).numpy().tobytes()
+    parts, datas, size = [], [], 0
+    while size < target_comp:
+        if rng.random() < 0.5:
+            ln = int(rng.integers(1, 65536))
+            d = rng.integers(0, 256, ln, dtype=np.uint8).tobytes()
+            co = zlib.compressobj(0, zlib.DEFLATED, -15)
+        else:
+            ln = int(rng.integers(32768, 98304))
+            o = int(rng.integers(0, len(text) - ln))
+            d = text[o:o + ln]
+            co = zlib.compressobj(6, zlib.DEFLATED, -15, 9, zlib.Z_FIXED)
+        p = co.compress(d) + co.flush(zlib.Z_SYNC_FLUSH)
+        parts.append(p)
+        datas.append(d)
+        size += len(p)
+    raw = b"".join(parts) + b"\x03\x00"          # final fixed block holding only EOB
+    data = b"".join(datas)
+    hdr = bytes([0x1F, 0x8B, 8, 0, 0, 0, 0, 0, 0, 3])
+    trailer = (zlib.crc32(data) & 0xFFFFFFFF).to_bytes(4, "little") + (len(data) & 0xFFFFFFFF).to_bytes(4, "little")
+    return hdr + raw + trailer, raw, data
+
+
+def c5_random_repeat(n, seed=0xC5):
+    """Config 5: 50 % random-byte spans and 50 % "repeat" spans -- copies of earlier
+    data at dist U[1, 32768] with lengths 3 + geometric (capped at 258), and byte runs up to 4 KiB.
+    numpy PCG64, deterministic; returns a uint8 numpy array of n bytes."""
+    import numpy as np
+    rng = np.random.default_rng(seed)
+    a = np.empty(n + 4096 + 258 * 16, dtype=np.uint8)
+    p = 0
+    while p < n:
+        u = rng.random()
+        if u < 0.5 or p < 64:                         # random span
+            ln = int(rng.integers(64, 4096))
+            a[p:p + ln] = rng.integers(0, 256, ln, dtype=np.uint8)
+        elif u < 0.6:                                 # byte run up to 4 KiB
+            ln = int(rng.integers(3, 4097))
+            a[p:p + ln] = int(rng.integers(0, 256))
+        else:                                         # a few copies from earlier data
+            ln = 0
+            for _ in range(int(rng.integers(1, 16))):
+                q = p + ln
+                d = int(rng.integers(1, min(32768, q) + 1))
+                ll = min(258, 3 + int(rng.geometric(1 / 20)))
+                if d >= ll:
+                    a[q:q + ll] = a[q - d:q - d + ll]
+                else:
+                    a[q:q + ll] = np.resize(a[q - d:q], ll)
+                ln += ll
+        p += ln
+    return a[:n]

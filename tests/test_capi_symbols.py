@@ -52,3 +52,15 @@ def test_crc32_combine_host():
     lib.ndfl_crc32_combine.argtypes = [ctypes.c_uint32, ctypes.c_uint32, ctypes.c_uint64]
     a, b = b"hello ", b"world" * 1000
     assert lib.ndfl_crc32_combine(zlib.crc32(a), zlib.crc32(b), len(b)) == zlib.crc32(a + b)
+
+
+def test_header_constants_match_python_binding():
+    """The flag / size constants of include/ndfl.h and the ctypes binding agree (the kernels
+    static_assert the pad size against the header themselves)."""
+    hdr = open(os.path.join(ROOT, "include", "ndfl.h")).read()
+    consts = {m.group(1): int(m.group(2)) for m in re.finditer(r"#define NDFL_(\w+)\s+\(?(-?\d+)u?\)?", hdr)}
+    import ndfl._lib as L
+    assert consts["IN_DEVICE"] == L.IN_DEVICE and consts["OUT_DEVICE"] == L.OUT_DEVICE
+    assert consts["DICT_DEFERRED"] == L.DICT_DEFERRED and consts["IN_PADDED"] == L.IN_PADDED
+    assert consts["IN_PAD_BYTES"] == L.IN_PAD_BYTES and consts["IN_PARTIAL"] == L.IN_PARTIAL
+    assert consts["NEED_INPUT"] == L.NEED_INPUT and consts["E_CAPACITY"] == L.E_CAPACITY

@@ -156,3 +156,129 @@ def test_corrupted_lz77_streams_prefix_exact(ctx):
                 c = c[:rng.randrange(len(c) // 2, len(c))]
             check_same(ctx, bytes(c))
 
+
+
+def test_in_padded_device_input_matches_oracle(ctx):
+    """NDFL_IN_PADDED: a device buffer that is 16-byte aligned with IN_PAD_BYTES zeros after the
+    stream is decoded in place; results (Reason, bytes, consumed bits) equal the oracle's, for ragged
+    lengths, truncated/corrupted streams, and a misaligned pointer (which is staged instead); the
+    same through ndfl_inflate_range from a block boundary past bit 0, with and without
+    NDFL_DICT_DEFERRED."""
+    import torch
+    import ndfl
+    rng = random.Random(31)
+    cases = []
+    for strategy in ["RLE_DYNAMIC", "FULL_DYNAMIC", "UNCOMPRESSED", "LITERAL_STATIC"]:
+        data = b"".join(bytes([rng.randrange(5)]) * rng.randrange(1, 90) + rng.randbytes(rng.randrange(0, 9))
+                        for _ in range(rng.randrange(50, 4000)))
+        comp = O.deflate(data, strategy)
+        cases.append(comp)
+        c = bytearray(comp)
+        c[rng.randrange(len(c))] ^= 1 << rng.randrange(8)
+        cases.append(bytes(c[:rng.randrange(1, len(c) + 1)]))
+    cases.append(b"\x01\x00\x00\xff\xff")                       # empty stored final block
+    D = ndfl.IN_DEVICE | ndfl.OUT_DEVICE
+    for comp in cases:
+        o = O.inflate(comp)
+        for shift in (0, 4):                                     # 4: not 16-byte aligned -> staged
+            buf = torch.zeros(len(comp) + ndfl.IN_PAD_BYTES + 16, dtype=torch.uint8, device="cuda")
+            buf[shift:shift + len(comp)] = torch.frombuffer(bytearray(comp), dtype=torch.uint8).cuda()
+            out = torch.zeros(max(len(o[1]), 1) + 1024, dtype=torch.uint8, device="cuda")
+            torch.cuda.synchronize()
+            r, olen, bits = ctx.inflate_raw(buf.data_ptr() + shift, len(comp), out.data_ptr(), out.numel(),
+                                            D | ndfl.IN_PADDED)
+            reason = None if r == 0 else ndfl.Reason(r - 1).name
+            assert r >= 0, r
+            assert reason == o[0], (reason, o[0])
+            assert olen == len(o[1]) and out[:olen].cpu().numpy().tobytes() == o[1]
+            if o[0] != "UNEXPECTED_END_OF_STREAM":     # (where the input ran out is not pinned)
+                assert bits == o[2], (reason, bits, o[2])
+    # range decodes in place: start at the 3rd chunk's block boundary
+    data = b"".join(bytes([rng.randrange(4)]) * rng.randrange(1, 200) + rng.randbytes(rng.randrange(0, 30))
+                    for _ in range(6000))
+    seams = [0] + O.block_bits(data)
+    for k in range(1, len(seams)):
+        seams[k] += seams[k - 1]
+    comp = O.deflate(data)
+    a = 2
+    pre = a * 65536
+    window = data[pre - 32768:pre]
+    oref = O.inflate_range(comp, seams[a], None, window)
+    buf = torch.zeros(len(comp) + ndfl.IN_PAD_BYTES, dtype=torch.uint8, device="cuda")
+    buf[:len(comp)] = torch.frombuffer(bytearray(comp), dtype=torch.uint8).cuda()
+    for deferred in (False, True):
+        out = torch.zeros(32768 + len(oref[1]) + 64, dtype=torch.uint8, device="cuda")
+        if not deferred:
+            out[:32768] = torch.frombuffer(bytearray(window), dtype=torch.uint8).cuda()
+        torch.cuda.synchronize()
+        fl = D | ndfl.IN_PADDED | (ndfl.DICT_DEFERRED if deferred else 0)
+        r, olen, bits = ctx.inflate_range_raw(buf.data_ptr(), len(comp), seams[a], None, out.data_ptr(), 32768,
+                                              out.numel() - 32768, fl)
+        if deferred:
+            out[:32768] = torch.frombuffer(bytearray(window), dtype=torch.uint8).cuda()
+            ctx.inflate_resolve()
+        assert (r, olen, bits) == (0, len(oref[1]), oref[2])
+        assert out[32768:32768 + olen].cpu().numpy().tobytes() == oref[1] == data[pre:]
+
+
+class _Pipe(io.RawIOBase):
+    """Non-seekable reader handing out at most `step` bytes per read."""
+
+    def __init__(self, data, step):
+        self._d, self._p, self._step = data, 0, step
+
+    def readable(self):
+        return True
+
+    def read(self, n=-1):
+        n = len(self._d) - self._p if n is None or n < 0 else n
+        b = self._d[self._p:self._p + min(n, self._step)]
+        self._p += len(b)
+        return b
+
+
+@pytest.mark.parametrize("batch", [1 << 10, 40000, 1 << 20])
+def test_streaming_inflater_matches_oracle(ctx, batch):
+    """InflaterInputStream reads its input incrementally (ndfl_inflate_range with NDFL_IN_PARTIAL):
+    fed through a non-seekable pipe in small pieces with small device batches, the output equals the
+    oracle's for RLE / FULL / stored / fixed / zlib -6 streams; endExactly leaves a seekable stream
+    right after the final block; a corrupted stream yields the oracle's prefix and Reason."""
+    import zlib as Z
+    import ndfl
+    rng = random.Random(batch)
+    words = [rng.randbytes(rng.randrange(3, 12)) for _ in range(300)]
+    text = b"".join(rng.choice(words) for _ in range(60_000))[:400_000]
+    co = Z.compressobj(6, Z.DEFLATED, -15)
+    streams = [O.deflate(text), O.deflate(text[:150_000], "FULL_DYNAMIC"), co.compress(text) + co.flush(),
+               O.deflate_mixed(text, ["UNCOMPRESSED", "FULL_STATIC", "RLE_DYNAMIC"], chunk_len=30000), O.deflate(b"")]
+    old = ndfl.InflaterInputStream.BATCH
+    ndfl.InflaterInputStream.BATCH = batch
+    try:
+        for comp in streams:
+            o = O.inflate(comp)
+            s = ndfl.InflaterInputStream(_Pipe(comp + b"tail", 777), context=ctx)
+            got = bytearray()
+            buf = bytearray(5000)
+            while (k := s.read(buf, 0, len(buf))) != -1:
+                got += buf[:k]
+            assert bytes(got) == o[1]
+            f = io.BytesIO(b"head" + comp + b"tail")
+            f.seek(4)
+            s = ndfl.InflaterInputStream(f, True, context=ctx)
+            assert s.readall() == o[1]
+            assert f.tell() == 4 + (o[2] + 7) // 8 and f.read() == b"tail"
+        for pos in range(len(streams[0]) * 2 // 3, len(streams[0])):
+            bad = bytearray(streams[0])
+            bad[pos] ^= 0x10
+            o = O.inflate(bytes(bad))
+            if o[0] is not None:
+                break
+        assert o[0] is not None
+        s = ndfl.InflaterInputStream(_Pipe(bytes(bad), 1000), context=ctx)
+        got = bytearray()
+        with pytest.raises(ndfl.DataFormatException) as ei:
+            while (k := s.read(buf, 0, len(buf))) != -1:
+                got += buf[:k]
+        assert ei.value.getReason().name == o[0] and bytes(got) == o[1]
+    finally:
+        ndfl.InflaterInputStream.BATCH = old
