@@ -63,9 +63,11 @@ __device__ __forceinline__ void dist_base(uint32_t d, uint32_t& base, uint32_t& 
 
 constexpr uint64_t IN_PAD = 256;           // zero bytes after the staged input
 static_assert(IN_PAD == NDFL_IN_PAD_BYTES, "kernel pad and the NDFL_IN_PADDED contract must agree");
-// the furthest unchecked read: In::ld4 / make_rb clamp 16-byte group indices at (nwords + 3) / 4 + 1,
-// so a lane reads at most ((nwords + 3) / 4 + 2) * 16 <= nwords * 4 + 44 bytes
+// the furthest unchecked reads: In::ld4 clamps 16-byte group indices at (nwords + 3) / 4 + 1, so a
+// lane reads at most ((nwords + 3) / 4 + 2) * 16 <= nwords * 4 + 44 bytes; the decode passes' round
+// staging (wv::stage_round) clamps word indices at nwords + 60, i.e. nwords * 4 + 244 bytes
 static_assert(3 * 4 + 2 * 16 + 16 <= IN_PAD, "16-byte prefetch clamp must stay inside the zero padding");
+static_assert((60 + 1) * 4 <= IN_PAD, "round staging clamp must stay inside the zero padding");
 // header finder scan pattern (32-bit words): FIND_WIN_WORDS of every FIND_PERIOD_WORDS.  Dense
 // (every position) by default: sparse windows make chains span several blocks, which costs more
 // in the count/emit passes' load balance than it saves here.
@@ -82,11 +84,8 @@ constexpr uint32_t FIND_WPT = NDFL_FIND_WPT;     // finder: input words per thre
 #define NDFL_STRICT_REFILL 32     // strict stage: refill a wave once this many lanes are idle
 #endif
 constexpr uint32_t STRICT_SLICE = NDFL_STRICT_SLICE;  // strict stage: survivors per ticket
-constexpr uint32_t COUNT_WAVES = 256 * 16;       // count pass: persistent waves
-#ifndef NDFL_EMIT_WAVES_PER_SIMD
-#define NDFL_EMIT_WAVES_PER_SIMD 4
-#endif
-constexpr uint32_t EMIT_WAVES = 256 * 4 * NDFL_EMIT_WAVES_PER_SIMD;   // emit pass: persistent waves
+constexpr uint32_t COUNT_WAVES = 256 * 16;       // count / emit passes: persistent waves at most (the
+constexpr uint32_t EMIT_WAVES = 256 * 16;        // grids are sized by occupancy, wave_grid below)
 
 struct In {
     const uint32_t* w;
@@ -661,6 +660,7 @@ constexpr uint32_t NOREC = 0xFFFFFFFFu;
 struct SegMeta {
     uint32_t ft, kind_ft, reason_ft, next;
     uint64_t end_ft, exit63;
+    uint32_t pw, pad;     // the round's words per lane segment (staging geometry)
 };
 struct SegPool {
     uint64_t* start;      // [nrec][64]
@@ -717,6 +717,17 @@ struct InflateScratch {
         pending = false;
     }
 };
+
+// Persistent-wave grid of a one-wave-workgroup kernel: what fits on the chip at once (occupancy),
+// at most `cap` waves.
+template <typename K>
+static uint32_t wave_grid(K kernel, uint32_t cap) {
+    int dev = 0, ncu = 0, per = 0;
+    if (hipGetDevice(&dev) != hipSuccess || hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess ||
+        hipOccupancyMaxActiveBlocksPerMultiprocessor(&per, kernel, 64, 0) != hipSuccess || ncu <= 0 || per <= 0)
+        return cap;
+    return std::min<uint32_t>(cap, (uint32_t)(ncu * per));
+}
 
 static hipError_t inf_ensure(void** p, size_t* cap, size_t n) {
     if (n <= *cap && *p) return hipSuccess;
@@ -888,7 +899,7 @@ static int inflate_run(InflateScratch& S, hipStream_t s, const uint8_t* in, uint
     // segment records: a pool for the rounds of all chains, one head per counted chain start (index
     // in `starts`), with room for repairs
     const uint64_t nslot = starts.size() + std::max<uint64_t>(4096, starts.size() / 2);
-    const uint64_t nrec = std::min<uint64_t>(0xFFFFFFF0ull, 2 * starts.size() + nbits / (1u << 17) + 65536);
+    const uint64_t nrec = std::min<uint64_t>(0xFFFFFFF0ull, 2 * starts.size() + nbits / (wv::MAX_SPAN / 2) + 65536);
     const uint64_t seg_bytes = nrec * (64 * 8 + 64 * 4 + sizeof(SegMeta)) + nslot * 4;
     INF_CHK(inf_ensure(&S.d_seg, &S.d_seg_cap, seg_bytes));
     SegPool pool;
@@ -940,7 +951,8 @@ static int inflate_run(InflateScratch& S, hipStream_t s, const uint8_t* in, uint
         if (!S.d_cticket) INF_CHK(hipMalloc(&S.d_cticket, 64));
         INF_CHK(hipMemsetAsync(S.d_cticket, 0, 4, s));
         if (S.count_first) INF_CHK(hipEventRecord(S.ev[2], s));
-        hipLaunchKernelGGL(ndfl_inflate_count_wave_kernel, dim3((uint32_t)std::min<size_t>(n, COUNT_WAVES)), dim3(64), 0, s,
+        static const uint32_t count_grid = wave_grid(ndfl_inflate_count_wave_kernel, COUNT_WAVES);
+        hipLaunchKernelGGL(ndfl_inflate_count_wave_kernel, dim3((uint32_t)std::min<size_t>(n, count_grid)), dim3(64), 0, s,
                            d_w, nwords, nbits,
                            (const uint64_t*)S.d_starts, (const uint64_t*)S.d_stops, (uint32_t)n,
                            (const uint64_t*)S.d_cands, ncand, limit, (ChainRes*)S.d_res, stats_on ? (uint32_t*)S.d_stats : nullptr,
@@ -1046,8 +1058,8 @@ static int inflate_run(InflateScratch& S, hipStream_t s, const uint8_t* in, uint
         fprintf(stderr, "[ndfl] strict stage: %llu waves, %llu loop trips (%llu refills), %llu lane-symbol steps\n",
                 ss[3], ss[0], ss[1], ss[2]);
         fprintf(stderr, "[ndfl] count wave-time (ms x waves, 100 MHz clock): header %.1f spec %.1f verify %.1f phases %.1f "
-                "serial %.1f record %.1f build %.1f\n", t64[0] * 1e-5, t64[1] * 1e-5, t64[2] * 1e-5, t64[3] * 1e-5,
-                t64[4] * 1e-5, t64[5] * 1e-5, t64[6] * 1e-5);
+                "serial %.1f record %.1f build %.1f phase-mapped %.1f\n", t64[0] * 1e-5, t64[1] * 1e-5, t64[2] * 1e-5, t64[3] * 1e-5,
+                t64[4] * 1e-5, t64[5] * 1e-5, t64[6] * 1e-5, t64[7] * 1e-5);
     }
     const uint64_t total = off - dict_len;
     ht[3] = hnow();
@@ -1078,7 +1090,8 @@ static int inflate_run(InflateScratch& S, hipStream_t s, const uint8_t* in, uint
     hipEvent_t e2 = S.ev[4], e3 = S.ev[5];
     INF_CHK(hipEventRecord(e2, s));
     if (!S.d_ph) INF_CHK(hipMalloc(&S.d_ph, (size_t)std::max(COUNT_WAVES, EMIT_WAVES) * sizeof(wv::PhArr)));
-    hipLaunchKernelGGL(ndfl_inflate_emit_wave_kernel, dim3(std::min<uint32_t>(nch, EMIT_WAVES)), dim3(64), 0, s, d_w,
+    static const uint32_t emit_grid = wave_grid(ndfl_inflate_emit_wave_kernel, EMIT_WAVES);
+    hipLaunchKernelGGL(ndfl_inflate_emit_wave_kernel, dim3(std::min<uint32_t>(nch, emit_grid)), dim3(64), 0, s, d_w,
                        nwords, nbits, (const EmitChain*)S.d_chains, nch, (uint32_t*)S.d_ticket, d_out,
                        (ChainRes*)S.d_res, (const uint64_t*)S.d_cands, ncand, (uint32_t*)S.d_ref, (uint32_t*)S.d_pend,
                        pool, (wv::PhArr*)S.d_ph);

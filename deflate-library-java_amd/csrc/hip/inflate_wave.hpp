@@ -27,7 +27,6 @@ using namespace inf;
 
 constexpr uint32_t LB = 10;                 // literal/length primary bits
 constexpr uint32_t DB = 8;                  // distance primary bits
-constexpr int BUDGET = 32;                  // tokens per emit step
 // table entry: [4:0] code length (0: longer than the primary), [8:5] extra bits, [10:9] kind,
 // [31:16] literal byte / run base / distance base
 enum : uint32_t { K_LIT = 0, K_LEN = 1, K_EOB = 2, K_BAD = 3 };
@@ -104,107 +103,144 @@ __device__ __forceinline__ uint32_t slow_dist(uint32_t p15, const Tabs& t) {
 }
 
 struct Tok {
-    uint32_t kind;      // K_LIT (val = n bytes), K_LEN (val = run, dist), K_EOB, K_BAD (val = reason)
+    uint32_t kind;      // K_LIT (n bytes in val), K_LEN (n = run, dist), K_EOB, K_BAD (val = reason)
     uint32_t val, dist, n;
 };
 
-// Round-relative bit reader: positions are 32-bit offsets from a 128-bit-aligned round base, so
-// the per-token arithmetic is 32-bit.  64-bit active buffer refilled 32 bits at a time; the next two
-// 16-byte groups are always in flight (unconditional loads from the zero-padded input).
-struct RB {
-    const u32x4* gp;      // group 0 = round base
-    uint32_t gmax;        // last readable group (relative; clamped into the padding)
-    uint32_t nb;          // input bits relative to the base (saturated)
-    uint64_t base;        // absolute bit of the base
-};
-__device__ __forceinline__ RB make_rb(const In& in, uint64_t rs) {
-    RB b;
-    b.base = rs & ~127ull;
-    b.gp = (const u32x4*)in.w + (b.base >> 7);
+// ---- staged round input -------------------------------------------------------------------------
+// A round is decoded by the wave's 64 lanes over consecutive segments of pw words each.  Its input
+// is staged in LDS transposed: word i of lane j's region (the segment plus the words a token that
+// starts inside it can still read) at w[i * 64 + j], so every lane's window read is bank-conflict
+// free whatever its position.  The loads are LDS-DMA (global_load_lds_dword, one 256-byte row of
+// the image per instruction), so the decode loop carries no prefetch state at all: a token is read
+// from its absolute position with one ds_read2st64 + one ds_read and two funnel shifts.
+#ifndef NDFL_LPW
+#define NDFL_LPW 16
+#endif
+constexpr uint32_t LPW = NDFL_LPW;             // words per lane segment at most (512 bits by default)
+constexpr uint32_t SW = LPW + 4;               // staged words per lane region
+constexpr uint64_t RSPAN = 64ull * LPW * 32;   // round span cap (bits)
 
-    b.gmax = (uint32_t)((in.nwords + 3) / 4 + 1 - (b.base >> 7));
-    b.nb = (uint32_t)min(in.nbits - min(in.nbits, b.base), (uint64_t)0xFFFFFFFFu);
-    return b;
+struct Stage {
+    uint32_t w[SW * 64];
+};
+
+struct Geo {            // wave-uniform geometry of one round
+    uint64_t base;      // absolute bit of the round's word 0 (word-aligned)
+    uint32_t r0, re;    // round start / end relative to base
+    uint32_t pw;        // words per lane segment
+    uint32_t nb;        // input bits relative to base (saturated)
+};
+__device__ __forceinline__ Geo make_geo(const In& in, uint64_t rs, uint64_t E, uint32_t pw = 0) {
+    Geo g;
+    g.base = rs & ~31ull;
+    g.r0 = (uint32_t)(rs - g.base);
+    g.re = (uint32_t)(E - g.base);
+    const uint32_t span = g.re - g.r0;
+    g.pw = pw ? pw : max(1u, ((span + 63) / 64 + 31) / 32);
+    g.nb = (uint32_t)min(in.nbits - min(in.nbits, g.base), (uint64_t)0xFFFFFFFFu);
+    return g;
 }
-struct Rq {
-    // `cur` is the group being consumed; the next group is in flight into `nxt`.  At a group
-    // boundary `cur = nxt` is materialised BEFORE the next load is issued (compiler barrier), so
-    // the load can land in nxt's own registers: no copy of in-flight data, no early s_waitcnt.
-    uint64_t bb;
-    uint32_t bn, ci, qw, pos;
-    u32x4 cur, nxt;
-    __device__ __forceinline__ static uint32_t pick(const u32x4& v, uint32_t i) {
-        uint32_t a = (i & 1) ? v.y : v.x, b = (i & 1) ? v.w : v.z;
-        return (i & 2) ? b : a;
-    }
-    __device__ __forceinline__ void adv(const RB& b) {
-        if (++ci == 4) {
-            ci = 0;
-            qw++;
-            cur = nxt;
-            asm volatile("" : "+v"(cur) :: "memory");
-            nxt = b.gp[min(qw + 1, b.gmax)];
-        }
-    }
-    __device__ __forceinline__ void init(const RB& b, uint32_t p) {
-        pos = p;
-        qw = p >> 7;
-        cur = b.gp[min(qw, b.gmax)];
-        nxt = b.gp[min(qw + 1, b.gmax)];
-        ci = (p >> 5) & 3;
-        bb = (uint64_t)(pick(cur, ci) >> (p & 31));
-        bn = 32 - (p & 31);
-        adv(b);
-        fill(b);
-    }
-    __device__ __forceinline__ void fill(const RB& b) {
-        if (bn <= 32) { bb |= (uint64_t)pick(cur, ci) << bn; bn += 32; adv(b); }
-    }
-    __device__ __forceinline__ uint32_t peek(uint32_t n) const { return (uint32_t)bb & ((1u << n) - 1u); }
-    __device__ __forceinline__ void skip(uint32_t n) { bb >>= n; bn -= n; pos += n; }
-    __device__ __forceinline__ uint32_t get(const RB& b, uint32_t n) {
-        fill(b);
-        const uint32_t v = peek(n);
-        skip(n);
-        return v;
+// lane j's segment [s, e) (relative bits); lane 63 ends at the round end
+__device__ __forceinline__ void lane_seg(const Geo& g, int lane, uint32_t& s, uint32_t& e) {
+    const uint32_t per = g.pw * 32;
+    s = min(g.r0 + (uint32_t)lane * per, g.re);
+    e = lane == 63 ? g.re : min(g.r0 + (uint32_t)(lane + 1) * per, g.re);
+}
+
+// Stage the round's input (all lanes call).  Words past the input end read the zero padding.
+__device__ __forceinline__ void stage_round(const In& in, const Geo& g, Stage& st, int lane) {
+    const uint64_t w0 = (g.base >> 5) + (uint64_t)lane * g.pw;
+    const uint64_t wmax = in.nwords + 60;          // inside the IN_PAD zero bytes after the input
+    __syncthreads();                               // the previous round's reads are done
+#pragma unroll 4
+    for (uint32_t i = 0; i < SW; i++)
+        __builtin_amdgcn_global_load_lds((const __attribute__((address_space(1))) void*)(in.w + min(w0 + i, wmax)),
+                                         (__attribute__((address_space(3))) void*)&st.w[i * 64], 4, 0, 0);
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __syncthreads();
+}
+
+// The lane's view of the staged round: 64 bits of input from relative bit `pos`.
+struct Lv {
+    const uint32_t* p;     // &st.w[lane] less the region's first word (as a row offset)
+    uint32_t rw;           // region's first word (relative to base)
+    __device__ __forceinline__ void win(uint32_t pos, uint32_t& lo, uint32_t& hi) const {
+        const uint32_t* q = p + ((pos >> 5) - rw) * 64;
+        const uint32_t a = q[0], b = q[64], c = q[128];
+        lo = __builtin_amdgcn_alignbit(b, a, pos & 31);
+        hi = __builtin_amdgcn_alignbit(c, b, pos & 31);
     }
 };
+__device__ __forceinline__ Lv make_lv(const Stage& st, const Geo& g, int lane) {
+    Lv v;
+    v.p = st.w + lane;
+    v.rw = (uint32_t)lane * g.pw;
+    return v;
+}
 
-// One token of a Huffman block, with the reference's check order (D/decomp/Open.java:446-618).
-// Two literals whose codes fit the primary table together come as one step (tk.n = 2), except
-// when the first one already reaches `stop` (a checkpoint or the segment end): every decode then
+// One token at `pos` with the reference's check order (D/decomp/Open.java:446-618).  A literal
+// pair (two literal codes fitting the primary table together) comes as one step (tk.n = 2), except
+// when its first literal already reaches `stop` (a checkpoint or the segment end): every decode then
 // stands on the first token boundary at or past each stop, whatever its grouping before it.
-__device__ __forceinline__ void next_tok(Rq& rd, const RB& b, const Tabs& t, bool empty_dist, uint32_t stop,
-                                         Tok& tk) {
-    rd.fill(b);
-    uint32_t e = t.lit[rd.peek(LB)];
+// CAREFUL = false: the caller guarantees pos + 48 < stop <= nb (no token can reach the stop or the
+// input end), so those checks are dropped.
+template <bool CAREFUL>
+__device__ __forceinline__ void tok(const Lv& v, uint32_t& pos, const Tabs& t, bool empty_dist, uint32_t stop,
+                                    uint32_t nb, Tok& tk) {
+    uint32_t lo, hi;
+    v.win(pos, lo, hi);
+    uint32_t e = t.lit[lo & ((1u << LB) - 1u)];
     if (e >> 31) {
-        const uint32_t l1 = e & 15, l2 = (e >> 4) & 15;
-        const bool two = ((e >> 8) & 1) && rd.pos + l1 < stop && rd.pos + l2 <= b.nb;
-        rd.skip(two ? l2 : l1);
-        if (rd.pos > b.nb) { tk.kind = K_BAD; tk.val = R_UEOS; return; }
+        const uint32_t l1 = e & 15, l12 = (e >> 4) & 15;
+        bool two = (e >> 8) & 1;
+        if (CAREFUL) two = two && pos + l1 < stop && pos + l12 <= nb;
+        pos += two ? l12 : l1;
+        if (CAREFUL && pos > nb) { tk.kind = K_BAD; tk.val = R_UEOS; return; }
         tk.kind = K_LIT; tk.n = two ? 2u : 1u; tk.val = (e >> 9) & (two ? 0xFFFFu : 0xFFu);
         return;
     }
-    if (!(e & 31)) e = slow_lit(rd.peek(15), t);
-    rd.skip(e & 31);
-    if (rd.pos > b.nb) { tk.kind = K_BAD; tk.val = R_UEOS; return; }
-    const uint32_t k = (e >> 9) & 3;
-    if (k == K_LIT) { tk.kind = K_LIT; tk.n = 1; tk.val = e >> 16; return; }
-    if (k == K_EOB) { tk.kind = K_EOB; return; }
-    if (k == K_BAD) { tk.kind = K_BAD; tk.val = R_RESERVED_LEN; return; }
-    const uint32_t run = (e >> 16) + rd.get(b, (e >> 5) & 15);
-    if (rd.pos > b.nb) { tk.kind = K_BAD; tk.val = R_UEOS; return; }
-    if (empty_dist) { tk.kind = K_BAD; tk.val = R_EMPTY_DIST; return; }
-    rd.fill(b);
-    uint32_t d = t.dst[rd.peek(DB)];
-    if (!(d & 31)) d = slow_dist(rd.peek(15), t);
-    rd.skip(d & 31);
-    if (rd.pos > b.nb) { tk.kind = K_BAD; tk.val = R_UEOS; return; }
-    if (((d >> 9) & 3) == K_BAD) { tk.kind = K_BAD; tk.val = R_RESERVED_DIST; return; }
-    const uint32_t dist = (d >> 16) + rd.get(b, (d >> 5) & 15);
-    if (rd.pos > b.nb) { tk.kind = K_BAD; tk.val = R_UEOS; return; }
-    tk.kind = K_LEN; tk.val = run; tk.dist = dist;
+    if (!(e & 31)) e = slow_lit(lo & 0x7FFFu, t);
+    const uint32_t cl = e & 31, k = (e >> 9) & 3;
+    if (k != K_LEN) {
+        pos += cl;
+        if (CAREFUL && pos > nb) { tk.kind = K_BAD; tk.val = R_UEOS; return; }
+        tk.kind = k; tk.n = 1; tk.val = k == K_LIT ? e >> 16 : (uint32_t)R_RESERVED_LEN;
+        return;
+    }
+    const uint32_t xb = (e >> 5) & 15;
+    if (CAREFUL && pos + cl > nb) { pos += cl; tk.kind = K_BAD; tk.val = R_UEOS; return; }
+    const uint32_t run = (e >> 16) + ((lo >> cl) & ((1u << xb) - 1u));
+    const uint32_t sh = cl + xb;
+    if (CAREFUL && pos + sh > nb) { pos += sh; tk.kind = K_BAD; tk.val = R_UEOS; return; }
+    if (empty_dist) { pos += sh; tk.kind = K_BAD; tk.val = R_EMPTY_DIST; return; }
+    const uint32_t dw = __builtin_amdgcn_alignbit(hi, lo, sh);      // 32 bits from the distance code
+    uint32_t d = t.dst[dw & ((1u << DB) - 1u)];
+    if (!(d & 31)) d = slow_dist(dw & 0x7FFFu, t);
+    const uint32_t dl = d & 31, dxb = (d >> 5) & 15;
+    if (CAREFUL && pos + sh + dl > nb) { pos += sh + dl; tk.kind = K_BAD; tk.val = R_UEOS; return; }
+    if (((d >> 9) & 3) == K_BAD) { pos += sh + dl; tk.kind = K_BAD; tk.val = R_RESERVED_DIST; return; }
+    const uint32_t dist = (d >> 16) + ((dw >> dl) & ((1u << dxb) - 1u));
+    pos += sh + dl + dxb;
+    if (CAREFUL && pos > nb) { tk.kind = K_BAD; tk.val = R_UEOS; return; }
+    tk.kind = K_LEN; tk.n = run; tk.dist = dist;
+}
+
+// Count tokens from pos to the first token boundary at or past `stop` (<= input end) or to a
+// terminal token (true: end of block or an error, in tk).
+__device__ __forceinline__ bool run_to(const Lv& v, uint32_t& pos, const Tabs& t, bool ed, uint32_t stop, uint32_t nb,
+                                       uint32_t& cnt, Tok& tk) {
+    while (pos + 48 < stop) {
+        tok<false>(v, pos, t, ed, stop, nb, tk);
+        if (tk.kind > K_LEN) return true;
+        cnt += tk.n;
+    }
+    while (pos < stop) {
+        tok<true>(v, pos, t, ed, stop, nb, tk);
+        if (tk.kind > K_LEN) return true;
+        cnt += tk.n;
+    }
+    return false;
 }
 
 // ---- block header (lane 0) ----------------------------------------------------------------------
@@ -423,7 +459,7 @@ __device__ int build_tables(Shared& S, int lane, bool& empty_dist) {
 constexpr uint32_t XCP1 = 128, XCP2 = 1024;
 constexpr uint32_t NPH = 8;
 constexpr uint32_t NOCP = 0xFFFFFFFFu;
-constexpr uint64_t MAX_SPAN = 1ull << 29;    // round span cap: 32-bit positions and counts
+constexpr uint64_t MAX_SPAN = RSPAN;         // round span cap
 
 struct Seg {
     uint64_t start, end, cnt;                // absolute bits
@@ -437,44 +473,52 @@ struct Spec {
     uint32_t cp1, cpc1, cp2, cpc2;
 };
 
-__device__ void spec_run(const RB& b, const Tabs& t, bool ed, uint32_t st, uint32_t s, uint32_t C1, uint32_t C2,
-                         uint32_t e, Spec& o) {
-    Rq rd;
-    rd.init(b, st);
-    uint32_t cnt = 0, kind = T_EXIT, reason = 0;
+__device__ __forceinline__ void spec_run(const Lv& v, const Tabs& t, bool ed, uint32_t nb, uint32_t st, uint32_t s,
+                                         uint32_t C1, uint32_t C2, uint32_t e, Spec& o) {
+    uint32_t pos = st, cnt = 0, kind = T_EXIT, reason = 0;
     o.cp1 = NOCP; o.cp2 = NOCP; o.cpc1 = 0; o.cpc2 = 0;
     Tok tk;
+    // three legs -- to C1, to C2, to e -- each recording its stop's checkpoint
+    uint32_t stop = C1, leg = 0;
     for (;;) {
-        if (o.cp2 == NOCP && rd.pos >= C1) {
-            if (o.cp1 == NOCP) { o.cp1 = rd.pos - s; o.cpc1 = cnt; }
-            if (rd.pos >= C2) { o.cp2 = rd.pos - s; o.cpc2 = cnt; }
+        if (run_to(v, pos, t, ed, stop, nb, cnt, tk)) {
+            kind = tk.kind == K_EOB ? T_EOB : T_ERR;
+            reason = tk.kind == K_EOB ? 0u : tk.val;
+            break;
         }
-        if (rd.pos >= e) break;
-        next_tok(rd, b, t, ed, o.cp1 == NOCP ? C1 : o.cp2 == NOCP ? C2 : e, tk);
-        if (tk.kind == K_LIT) { cnt += tk.n; continue; }
-        if (tk.kind == K_LEN) { cnt += tk.val; continue; }
-        kind = tk.kind == K_EOB ? T_EOB : T_ERR;
-        reason = tk.kind == K_EOB ? 0u : tk.val;
-        break;
+        if (leg == 0) {
+            o.cp1 = pos - s; o.cpc1 = cnt;
+            if (pos >= C2) { o.cp2 = pos - s; o.cpc2 = cnt; leg = 2; stop = e; }
+            else { leg = 1; stop = C2; }
+        } else if (leg == 1) {
+            o.cp2 = pos - s; o.cpc2 = cnt; leg = 2; stop = e;
+        } else {
+            break;
+        }
     }
-    o.end = rd.pos; o.cnt = cnt; o.kind = kind; o.reason = reason;
+    o.end = pos; o.cnt = cnt; o.kind = kind; o.reason = reason;
 }
 
 // Decode from the true start t0; at C1 compare with phase 0 (registers) and, when nph > 1, phases
-// 1..nph-1 (LDS); at C2 with phase 0 again; on a match take that run's end state, otherwise
-// decode the rest of the segment (authoritative).  Returns true when it synchronised.
-__device__ bool verify_run(const RB& b, const Tabs& t, bool ed, uint32_t t0, uint32_t s, uint32_t C1, uint32_t C2,
-                           uint32_t e, const Spec& p0, const PhArr* ph, int lane, uint32_t nph, SegR& r) {
-    Rq rd;
-    rd.init(b, t0);
-    uint32_t c = 0, stage = 0;
+// 1..nph-1 (per-wave slot); at C2 with phase 0 again; on a match take that run's end state,
+// otherwise decode the rest of the segment (authoritative).  Returns true when it synchronised.
+__device__ __forceinline__ bool verify_run(const Lv& v, const Tabs& t, bool ed, uint32_t nb, uint32_t t0, uint32_t s,
+                                           uint32_t C1, uint32_t C2, uint32_t e, const Spec& p0, const PhArr* ph,
+                                           int lane, uint32_t nph, SegR& r) {
+    uint32_t pos = t0, c = 0, stage = 0;
     Tok tk;
     r.start = t0;
     for (;;) {
-        const uint32_t q = rd.pos;
-        if (stage == 0 && q >= C1) {
+        const uint32_t stop = stage == 0 ? C1 : stage == 1 ? C2 : e;
+        if (run_to(v, pos, t, ed, stop, nb, c, tk)) {
+            r.end = pos; r.cnt = c;
+            r.kind = tk.kind == K_EOB ? T_EOB : T_ERR;
+            r.reason = tk.kind == K_EOB ? 0u : tk.val;
+            return false;
+        }
+        if (stage == 0) {
             stage = 1;
-            const uint32_t off = q - s;
+            const uint32_t off = pos - s;
             if (p0.cp1 == off) {
                 r.end = p0.end; r.cnt = c + (p0.cnt - p0.cpc1); r.kind = p0.kind; r.reason = p0.reason;
                 return true;
@@ -489,43 +533,39 @@ __device__ bool verify_run(const RB& b, const Tabs& t, bool ed, uint32_t t0, uin
                     return true;
                 }
             }
+            if (pos < C2) continue;
         }
-        if (stage == 1 && q >= C2) {
+        if (stage == 1) {
             stage = 2;
-            if (p0.cp2 == q - s) {
+            if (p0.cp2 == pos - s) {
                 r.end = p0.end; r.cnt = c + (p0.cnt - p0.cpc2); r.kind = p0.kind; r.reason = p0.reason;
                 return true;
             }
+            continue;
         }
-        if (q >= e) { r.end = q; r.cnt = c; r.kind = T_EXIT; r.reason = 0; return false; }
-        next_tok(rd, b, t, ed, stage == 0 ? C1 : stage == 1 ? C2 : e, tk);
-        if (tk.kind == K_LIT) { c += tk.n; continue; }
-        if (tk.kind == K_LEN) { c += tk.val; continue; }
-        r.end = rd.pos; r.cnt = c;
-        r.kind = tk.kind == K_EOB ? T_EOB : T_ERR;
-        r.reason = tk.kind == K_EOB ? 0u : tk.val;
+        r.end = pos; r.cnt = c; r.kind = T_EXIT; r.reason = 0;
         return false;
     }
 }
 
-// One round over [rs, E) (E - rs <= MAX_SPAN): exact per-lane segments; first_term = first lane
-// ending the block (64: none).  All lanes call.
+// One round over [rs, E) (E - rs <= MAX_SPAN): stage its input, then exact per-lane segments;
+// first_term = first lane ending the block (64: none).  All lanes call.
 struct PhaseClock {                            // count-pass phase times (wall clock ticks), wave-uniform
-    uint64_t hdr, spec, verify, phases, serial, rec, build;
+    uint64_t hdr, spec, verify, phases, serial, rec, build, phmap;
 };
-__device__ void round_decode(const In& in, const Tabs& t, bool ed, uint64_t rs, uint64_t E, Shared& S, int lane,
-                             Seg& out, uint32_t& first_term, uint32_t& nslow, uint32_t& nfix, PhArr* ph,
-                             PhaseClock* pc = nullptr) {
+__device__ void round_decode(const In& in, const Tabs& t, bool ed, uint64_t rs, uint64_t E, Shared& S, Stage& stg,
+                             int lane, Seg& out, uint32_t& first_term, uint32_t& nslow, uint32_t& nfix, PhArr* ph,
+                             Geo& g, PhaseClock* pc = nullptr) {
     uint64_t tk0 = pc ? wall_clock64() : 0;
-    const RB b = make_rb(in, rs);
-    const uint32_t r0 = (uint32_t)(rs - b.base), re = (uint32_t)(E - b.base);
-    const uint32_t span = re - r0;
-    const uint32_t per = (span + 63) / 64;
-    const uint32_t s = min(r0 + (uint32_t)lane * per, re);
-    const uint32_t e = (lane == 63) ? re : min(r0 + (uint32_t)(lane + 1) * per, re);
+    g = make_geo(in, rs, E);
+    stage_round(in, g, stg, lane);
+    const Lv v = make_lv(stg, g, lane);
+    const uint32_t nb = g.nb;
+    uint32_t s, e;
+    lane_seg(g, lane, s, e);
     const uint32_t C1 = s + min(XCP1, e - s), C2 = s + min(XCP2, e - s);
     Spec p0;
-    spec_run(b, t, ed, s, s, C1, C2, e, p0);
+    spec_run(v, t, ed, nb, s, s, C1, C2, e, p0);
     S.exit_[lane] = p0.end;
     __syncthreads();
     if (pc) { const uint64_t x = wall_clock64(); pc->spec += x - tk0; tk0 = x; }
@@ -535,7 +575,7 @@ __device__ void round_decode(const In& in, const Tabs& t, bool ed, uint64_t rs, 
         r.start = s; r.end = p0.end; r.cnt = p0.cnt; r.kind = p0.kind; r.reason = p0.reason;
         fin = true;
     } else {
-        fin = verify_run(b, t, ed, (uint32_t)S.exit_[lane - 1], s, C1, C2, e, p0, ph, lane, 1, r);
+        fin = verify_run(v, t, ed, nb, (uint32_t)S.exit_[lane - 1], s, C1, C2, e, p0, ph, lane, 1, r);
     }
     // exact prefix: lanes before the first unsynchronised lane
     const uint64_t um = __ballot(!fin);
@@ -553,7 +593,7 @@ __device__ void round_decode(const In& in, const Tabs& t, bool ed, uint64_t rs, 
         if (nph > 1 && (uint32_t)lane > j0) {
             for (uint32_t f = 1; f < NPH; f++) {
                 Spec q;
-                spec_run(b, t, ed, min(s + f, e), s, C1, C1, e, q);
+                spec_run(v, t, ed, nb, min(s + f, e), s, C1, C1, e, q);
                 // (offsets and byte counts at the first checkpoint fit 16 bits; otherwise no match)
                 ph->cp[f - 1][lane] = (q.cp1 < 0xFFFFu && q.cpc1 <= 0xFFFFu) ? (q.cp1 | (q.cpc1 << 16)) : 0xFFFFu;
                 ph->end[f - 1][lane] = q.end - s;
@@ -572,7 +612,7 @@ __device__ void round_decode(const In& in, const Tabs& t, bool ed, uint64_t rs, 
             if ((uint32_t)lane == j) {
                 const uint32_t st = (uint32_t)S.exit_[j - 1];
                 if (!(fin && st == r.start)) {
-                    verify_run(b, t, ed, st, s, C1, C2, e, p0, ph, lane, nph, r);
+                    verify_run(v, t, ed, nb, st, s, C1, C2, e, p0, ph, lane, nph, r);
                     S.exit_[lane] = r.end;
                     S.kind_[lane] = r.kind;
                 }
@@ -582,7 +622,7 @@ __device__ void round_decode(const In& in, const Tabs& t, bool ed, uint64_t rs, 
         }
         if (pc) { const uint64_t x = wall_clock64(); pc->serial += x - tk0; tk0 = x; }
     }
-    out.start = b.base + r.start; out.end = b.base + r.end; out.cnt = r.cnt;
+    out.start = g.base + r.start; out.end = g.base + r.end; out.cnt = r.cnt;
     out.kind = r.kind; out.reason = r.reason;
 }
 
@@ -601,23 +641,19 @@ static_assert(sizeof(PhMap) <= sizeof(PhArr), "phase map shares the fallback slo
 
 // count run from st to the first token boundary at or past e (or the block end); the first step is
 // a single token whose end and bytes are returned in fb / fbc (fb = NOCP: none)
-__device__ void phase_run(const RB& b, const Tabs& t, bool ed, uint32_t st, uint32_t e, uint32_t& end,
-                          uint32_t& cnt, uint32_t& kr, uint32_t& fb, uint32_t& fbc) {
-    Rq rd;
-    rd.init(b, st);
-    uint32_t c = 0;
+__device__ __forceinline__ void phase_run(const Lv& v, const Tabs& t, bool ed, uint32_t nb, uint32_t st, uint32_t e,
+                                          uint32_t& end, uint32_t& cnt, uint32_t& kr, uint32_t& fb, uint32_t& fbc) {
+    uint32_t pos = st, c = 0;
     kr = T_EXIT << 5; fb = NOCP; fbc = 0;
     Tok tk;
-    while (rd.pos < e) {
-        next_tok(rd, b, t, ed, fb == NOCP ? rd.pos + 1 : e, tk);
-        uint32_t add;
-        if (tk.kind == K_LIT) add = tk.n;
-        else if (tk.kind == K_LEN) add = tk.val;
-        else { kr = tk.kind == K_EOB ? (T_EOB << 5) : ((T_ERR << 5) | tk.val); break; }
-        c += add;
-        if (fb == NOCP) { fb = rd.pos; fbc = add; }
+    if (pos < e) {
+        tok<true>(v, pos, t, ed, pos + 1, nb, tk);      // a single token (no pair)
+        if (tk.kind > K_LEN) kr = tk.kind == K_EOB ? (T_EOB << 5) : ((T_ERR << 5) | tk.val);
+        else { c = tk.n; fb = pos; fbc = tk.n; }
+        if (tk.kind <= K_LEN && run_to(v, pos, t, ed, e, nb, c, tk))
+            kr = tk.kind == K_EOB ? (T_EOB << 5) : ((T_ERR << 5) | tk.val);
     }
-    end = rd.pos; cnt = c;
+    end = pos; cnt = c;
 }
 
 __device__ __forceinline__ uint32_t sel8(const uint32_t (&v)[8], uint32_t i) {
@@ -649,20 +685,21 @@ __device__ __forceinline__ uint32_t map_compose(uint32_t A, uint32_t B) {
     return r;
 }
 
-__device__ __noinline__ void round_decode_phased(const In& in, const Tabs& t, bool ed, uint64_t rs, uint64_t E, Shared& S,
-                                    int lane, Seg& out, uint32_t& first_term, uint32_t& nfix, PhArr* ph) {
-    const RB b = make_rb(in, rs);
-    const uint32_t r0 = (uint32_t)(rs - b.base), re = (uint32_t)(E - b.base);
-    const uint32_t span = re - r0;
-    const uint32_t per = (span + 63) / 64;
-    const uint32_t s = min(r0 + (uint32_t)lane * per, re);
-    const uint32_t e = (lane == 63) ? re : min(r0 + (uint32_t)(lane + 1) * per, re);
+__device__ __noinline__ void round_decode_phased(const In& in, const Tabs& t, bool ed, uint64_t rs, uint64_t E,
+                                                 Shared& S, Stage& stg, int lane, Seg& out, uint32_t& first_term,
+                                                 uint32_t& nfix, PhArr* ph, Geo& g) {
+    g = make_geo(in, rs, E);
+    stage_round(in, g, stg, lane);
+    const Lv v = make_lv(stg, g, lane);
+    const uint32_t nb = g.nb;
+    uint32_t s, e;
+    lane_seg(g, lane, s, e);
     PhMap* pm = (PhMap*)ph;
     uint32_t endv[8];
     uint32_t fbl = 0, fbh = 0;
     for (uint32_t f = 0; f < 8; f++) {
         uint32_t en, cn, kr, fb, fbc;
-        phase_run(b, t, ed, s + f, e, en, cn, kr, fb, fbc);      // (past e: empty, ends at s + f)
+        phase_run(v, t, ed, nb, s + f, e, en, cn, kr, fb, fbc);      // (past e: empty, ends at s + f)
 #pragma unroll
         for (uint32_t k = 0; k < 8; k++) endv[k] = k == f ? en : endv[k];
         pm->cnt[f][lane] = cn;
@@ -676,8 +713,8 @@ __device__ __noinline__ void round_decode_phased(const In& in, const Tabs& t, bo
 #pragma unroll
     for (uint32_t f = 0; f < 8; f++) {
         const uint32_t x = __shfl_up(endv[f], 1, 64);
-        const uint32_t v = phase_of(x - s, fbl, fbh) & 15u;
-        if (lane > 0) Q |= v << (4 * f);
+        const uint32_t vv = phase_of(x - s, fbl, fbh) & 15u;
+        if (lane > 0) Q |= vv << (4 * f);
     }
 #pragma unroll
     for (int k = 1; k < 64; k <<= 1) {
@@ -717,7 +754,7 @@ __device__ __noinline__ void round_decode_phased(const In& in, const Tabs& t, bo
             if ((uint32_t)lane == j) {
                 const uint32_t st = j ? (uint32_t)S.exit_[j - 1] : s;
                 uint32_t en, cn, kr, fb, fbc;
-                phase_run(b, t, ed, st, e, en, cn, kr, fb, fbc);
+                phase_run(v, t, ed, nb, st, e, en, cn, kr, fb, fbc);
                 r.start = st; r.end = en; r.cnt = cn; r.kind = kr >> 5; r.reason = kr & 31u;
                 S.exit_[lane] = en;
                 S.kind_[lane] = r.kind;
@@ -726,7 +763,7 @@ __device__ __noinline__ void round_decode_phased(const In& in, const Tabs& t, bo
             if (S.kind_[j] != T_EXIT) first_term = j;
         }
     }
-    out.start = b.base + r.start; out.end = b.base + r.end; out.cnt = r.cnt;
+    out.start = g.base + r.start; out.end = g.base + r.end; out.cnt = r.cnt;
     out.kind = r.kind; out.reason = r.reason;
 }
 
@@ -762,103 +799,94 @@ __device__ __forceinline__ uint64_t next_cand(const uint64_t* cands, uint32_t nc
 }
 
 // ---- emit: write pass of one lane ---------------------------------------------------------------
-// Output bytes are assembled into aligned 32-bit words; completed words wait in a 4-word queue that
-// is stored right after the bit reader crosses a 16-byte input group.  On this ISA stores and loads
-// share one counter (vmcnt), and the reader waits for its prefetched group at every group
-// boundary: stores issued just after that wait have a whole group's decode time to complete, so
-// the next boundary's wait does not stall on them.
+// Literal bytes gather in a 64-bit register and leave as 4-byte stores (unaligned global stores are
+// fine on gfx950); before a copy the pending 0..3 bytes go out as one 4-byte store whose spare bytes
+// the copy (or, for a deferred copy, the resolve rounds) overwrites -- always the lane's own bytes.
+// Copies move 8 or 4 bytes per load/store pair; the last chunk is stored overlapping so that no
+// store reaches past the copy's end (the next lane's bytes).
 typedef __attribute__((address_space(1))) uint8_t gu8;       // global (not flat) pointers
 typedef __attribute__((address_space(1))) uint32_t gu32;
-typedef __attribute__((address_space(1))) u32x4 gu32x4;
+typedef __attribute__((address_space(1))) uint64_t gu64;
 
-struct WLane {
-    Rq rd;
-    uint32_t end;               // round-relative stop bit (segment exit)
-    uint64_t dst0, n, cnt;
-    uint32_t cp_len, cp_dist, lastb, wc, wcn;
-    uint32_t q0, q1, q2, q3, qn, lastqw;
-    uint64_t qaddr;             // byte address of q0
-    uint32_t kind, reason;      // final state (T_ERR also for COPY_BEFORE found here)
-    bool active;
+struct Wr {
+    uint64_t acc;               // pending literal bytes (low byte first)
+    uint32_t an;                // pending byte count (0..3 between tokens)
+    uint64_t dst;               // output address of acc's first byte
 };
-
-__device__ __forceinline__ void wq_flush(WLane& L, gu8* out) {
-    if (L.qn == 0) return;
-    gu32* p = (gu32*)(out + L.qaddr);
-    if (L.qn == 4 && (L.qaddr & 15) == 0) {
-        u32x4 v; v.x = L.q0; v.y = L.q1; v.z = L.q2; v.w = L.q3;
-        *(gu32x4*)p = v;
-    } else {
-        p[0] = L.q0;
-        if (L.qn > 1) p[1] = L.q1;
-        if (L.qn > 2) p[2] = L.q2;
-        if (L.qn > 3) p[3] = L.q3;
+__device__ __forceinline__ void wr_lit(Wr& w, gu8* out, uint32_t val, uint32_t n) {
+    w.acc |= (uint64_t)val << (8 * w.an);
+    w.an += n;
+    if (w.an >= 4) {
+        *(gu32*)(out + w.dst) = (uint32_t)w.acc;
+        w.acc >>= 32;
+        w.an -= 4;
+        w.dst += 4;
     }
-    L.qn = 0;
 }
-__device__ __forceinline__ void wq_push(WLane& L, gu8* out, uint64_t addr, uint32_t v) {
-    // (pushes are consecutive: direct stores elsewhere are preceded by wq_flush)
-    if (L.qn == 0) L.qaddr = addr;
-    L.q0 = L.qn == 0 ? v : L.q0;
-    L.q1 = L.qn == 1 ? v : L.q1;
-    L.q2 = L.qn == 2 ? v : L.q2;
-    L.q3 = L.qn == 3 ? v : L.q3;
-    if (++L.qn == 4) wq_flush(L, out);
+// pending bytes out before a copy at w.dst + w.an (which covers the store's spare bytes)
+__device__ __forceinline__ void wr_flush_word(Wr& w, gu8* out) {
+    if (w.an) {
+        *(gu32*)(out + w.dst) = (uint32_t)w.acc;
+        w.dst += w.an;
+        w.acc = 0;
+        w.an = 0;
+    }
 }
-__device__ __forceinline__ void wputb(WLane& L, gu8* out, uint64_t P, uint32_t b) {
-    if (L.wcn == 0 && (P & 3)) { out[P] = (uint8_t)b; return; }
-    L.wc |= b << (8 * (uint32_t)(P & 3));
-    L.wcn++;
-    if ((P & 3) == 3) { wq_push(L, out, P - 3, L.wc); L.wc = 0; L.wcn = 0; }
+// pending bytes out exactly (end of the lane's output)
+__device__ __forceinline__ void wr_flush_exact(Wr& w, gu8* out) {
+    for (uint32_t k = 0; k < w.an; k++) out[w.dst + k] = (uint8_t)(w.acc >> (8 * k));
+    w.dst += w.an;
+    w.acc = 0;
+    w.an = 0;
 }
-// as wputb, but a completed word is stored at once (copy loops read back what they just wrote)
-__device__ __forceinline__ void wputb_now(WLane& L, gu8* out, uint64_t P, uint32_t b) {
-    if (L.wcn == 0 && (P & 3)) { out[P] = (uint8_t)b; return; }
-    L.wc |= b << (8 * (uint32_t)(P & 3));
-    L.wcn++;
-    if ((P & 3) == 3) { *(gu32*)(out + P - 3) = L.wc; L.wc = 0; L.wcn = 0; }
-}
-// store everything pending (queue, then the partial word ending at Pnext)
-__device__ __forceinline__ void wflush(WLane& L, gu8* out, uint64_t Pnext) {
-    wq_flush(L, out);
-    for (uint32_t k = 0; k < L.wcn; k++) out[Pnext - L.wcn + k] = (uint8_t)(L.wc >> (8 * k));
-    L.wc = 0; L.wcn = 0;
-}
-__device__ __forceinline__ void wcopy(WLane& L, gu8* out, uint64_t dst, uint64_t src, uint32_t len, uint32_t dist) {
-    if (dist == 1) {
-        const uint32_t v = (L.n > 0) ? L.lastb : (uint32_t)out[src];
+__device__ __forceinline__ uint64_t ld8(const gu8* p) { return *(const gu64*)p; }
+__device__ __forceinline__ uint32_t ld4(const gu8* p) { return *(const gu32*)p; }
+// out[dst, dst + len) = out[dst - dist, ...), byte-serial semantics; every source byte is final and
+// this lane's own (or the window's)
+__device__ __forceinline__ void wr_copy(gu8* out, uint64_t dst, uint32_t len, uint32_t dist) {
+    gu8* d = out + dst;
+    const gu8* sp = d - dist;
+    if (dist >= 8) {
+        if (len >= 8) {
+            uint32_t k = 0;
+            for (; k + 8 <= len; k += 8) *(gu64*)(d + k) = ld8(sp + k);
+            if (k < len) *(gu64*)(d + len - 8) = ld8(sp + len - 8);
+            return;
+        }
+    } else if (dist == 1) {
+        const uint32_t v4 = (uint32_t)sp[0] * 0x01010101u;
+        if (len >= 4) {
+            uint32_t k = 0;
+            for (; k + 4 <= len; k += 4) *(gu32*)(d + k) = v4;
+            if (k < len) *(gu32*)(d + len - 4) = v4;
+            return;
+        }
+    }
+    if (dist >= 4 && len >= 4) {
         uint32_t k = 0;
-        for (; k < len && (L.wcn > 0 || ((dst + k) & 3)); k++) wputb(L, out, dst + k, v);
-        const uint32_t v4 = v * 0x01010101u;
-        if (k + 4 <= len) wq_flush(L, out);        // the queue stays the newest consecutive words
-        for (; k + 4 <= len; k += 4) *(gu32*)(out + dst + k) = v4;
-        for (; k < len; k++) wputb(L, out, dst + k, v);
-        L.lastb = v;
+        for (; k + 4 <= len; k += 4) *(gu32*)(d + k) = ld4(sp + k);
+        if (k < len) *(gu32*)(d + len - 4) = ld4(sp + len - 4);
         return;
     }
-    uint32_t b = L.lastb;
-    if (dist < 4) {
-        wflush(L, out, dst);
-        for (uint32_t k = 0; k < len; k++) { b = out[src + k]; out[dst + k] = (uint8_t)b; }
-    } else {
-        // sources lie >= 4 bytes back: before the partial word, possibly in the queue
-        wq_flush(L, out);
-        for (uint32_t k = 0; k < len; k++) { b = out[src + k]; wputb_now(L, out, dst + k, b); }
-    }
-    L.lastb = b;
+    for (uint32_t k = 0; k < len; k++) d[k] = sp[k];
 }
 
 }  // namespace wv
 
 // Count pass: persistent waves, each claiming candidate chains through `ticket`; the phase-fallback
-// arrays live in the wave's own global slot (ph_all[blockIdx.x]), keeping LDS to the tables.
-extern "C" __global__ void __launch_bounds__(64, 4)
+// arrays live in the wave's own global slot (ph_all[blockIdx.x]); LDS holds the tables and the
+// round's staged input.
+#ifndef NDFL_COUNT_WPE
+#define NDFL_COUNT_WPE 3
+#endif
+extern "C" __global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(NDFL_COUNT_WPE)))
 ndfl_inflate_count_wave_kernel(const uint32_t* w, uint64_t nwords, uint64_t nbits, const uint64_t* starts,
                                const uint64_t* stops, uint32_t nchains, const uint64_t* cands, uint32_t ncand,
                                uint64_t limit, ChainRes* res, uint32_t* stats, uint64_t slot_base, SegPool pool,
                                uint32_t* ticket, wv::PhArr* ph_all, const uint32_t* order) {
     using namespace wv;
     __shared__ Shared S;
+    __shared__ Stage stg;
     __shared__ uint32_t s_ticket;
     const int lane = threadIdx.x;
     PhArr* ph = ph_all + blockIdx.x;
@@ -874,8 +902,7 @@ ndfl_inflate_count_wave_kernel(const uint32_t* w, uint64_t nwords, uint64_t nbit
     uint32_t status = ST_BOUNDARY, reason = 0, nslow = 0, nfix = 0, nround = 0, next_idx = 0xFFFFFFFFu;
     bool recording = slot_base + c < pool.nslot;
     uint32_t prev_rec = NOREC;
-    uint64_t span_est = 1ull << 18;             // round span: the previous block's size once known
-    PhaseClock pcl = {0, 0, 0, 0, 0, 0, 0};
+    PhaseClock pcl = {0, 0, 0, 0, 0, 0, 0, 0};
 #ifdef NDFL_PHASE_CLOCK
     PhaseClock* pc = stats ? &pcl : nullptr;     // costs registers: build with -DNDFL_PHASE_CLOCK to profile
 #else
@@ -919,20 +946,23 @@ ndfl_inflate_count_wave_kernel(const uint32_t* w, uint64_t nwords, uint64_t nbit
             phased = n8 >= 192;
         }
         while (!block_done) {
-            uint64_t E = min(next_cand(cands, ncand, rs, limit), rs + min(span_est, MAX_SPAN));
+            uint64_t E = min(next_cand(cands, ncand, rs, limit), rs + MAX_SPAN);
             if (E <= rs) E = rs + 1;
             Seg r;
             uint32_t ft;
+            Geo g;
             if (phased) {
-                round_decode_phased(in, S.t, ed, rs, E, S, lane, r, ft, nfix, ph);
+                const uint64_t t0p = pc ? wall_clock64() : 0;
+                round_decode_phased(in, S.t, ed, rs, E, S, stg, lane, r, ft, nfix, ph, g);
+                if (pc) pc->phmap += wall_clock64() - t0p;
             } else {
                 const uint32_t ns0 = nslow;
-                round_decode(in, S.t, ed, rs, E, S, lane, r, ft, nslow, nfix, ph, pc);
+                round_decode(in, S.t, ed, rs, E, S, stg, lane, r, ft, nslow, nfix, ph, g, pc);
                 if (nslow - ns0 > 32) phased = true;    // phase-locked code: map the next rounds
             }
             if (pc) tb = wall_clock64();
             if (recording) {
-                // record the exact segments of this round for the emit pass
+                // record the exact segments of this round (and its geometry) for the emit pass
                 const bool live = (uint32_t)lane <= ft;
                 uint32_t idx = NOREC;
                 if (__all(!live || r.cnt < 0xFFFFFFFFull)) {
@@ -948,7 +978,7 @@ ndfl_inflate_count_wave_kernel(const uint32_t* w, uint64_t nwords, uint64_t nbit
                     if (lane == 0) {
                         SegMeta m;
                         m.ft = ft; m.kind_ft = fk; m.reason_ft = fr; m.next = NOREC;
-                        m.end_ft = fe; m.exit63 = fe;
+                        m.end_ft = fe; m.exit63 = fe; m.pw = g.pw; m.pad = 0;
                         pool.meta[idx] = m;
                         if (prev_rec == NOREC) pool.head[slot_base + c] = idx;
                         else pool.meta[prev_rec].next = idx;
@@ -967,7 +997,6 @@ ndfl_inflate_count_wave_kernel(const uint32_t* w, uint64_t nwords, uint64_t nbit
                 block_done = true;
                 if (fk == T_ERR) { status = ST_ERROR; reason = fr; endpos = fe; chain_done = true; }
                 else {
-                    span_est = max((fe - d0) + ((fe - d0) >> 3), (uint64_t)4096);
                     cur = fe;
                     if (bfinal) { status = ST_FINAL; endpos = cur; chain_done = true; }
                 }
@@ -988,7 +1017,7 @@ ndfl_inflate_count_wave_kernel(const uint32_t* w, uint64_t nwords, uint64_t nbit
             unsigned long long* st64 = (unsigned long long*)(stats + 32);
             atomicAdd(&st64[0], pcl.hdr); atomicAdd(&st64[1], pcl.spec); atomicAdd(&st64[2], pcl.verify);
             atomicAdd(&st64[3], pcl.phases); atomicAdd(&st64[4], pcl.serial); atomicAdd(&st64[5], pcl.rec);
-            atomicAdd(&st64[6], pcl.build);
+            atomicAdd(&st64[6], pcl.build); atomicAdd(&st64[7], pcl.phmap);
         }
     }
     }
@@ -1001,14 +1030,15 @@ ndfl_inflate_count_wave_kernel(const uint32_t* w, uint64_t nwords, uint64_t nbit
 // and a pending bit, and ndfl_inflate_resolve_kernel rounds resolve them afterwards by pointer
 // jumping.  So every chain decodes in parallel whatever the LZ77 distances.
 #ifndef NDFL_EMIT_WAVES_PER_SIMD
-#define NDFL_EMIT_WAVES_PER_SIMD 4
+#define NDFL_EMIT_WAVES_PER_SIMD 2
 #endif
-extern "C" __global__ void __launch_bounds__(64, NDFL_EMIT_WAVES_PER_SIMD)
+extern "C" __global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(NDFL_EMIT_WAVES_PER_SIMD)))
 ndfl_inflate_emit_wave_kernel(const uint32_t* w, uint64_t nwords, uint64_t nbits, const EmitChain* chains,
                               uint32_t nlist, uint32_t* ticket, uint8_t* out, ChainRes* res, const uint64_t* cands,
                               uint32_t ncand, uint32_t* ref, uint32_t* pend, SegPool pool, wv::PhArr* ph_all) {
     using namespace wv;
     __shared__ Shared S;
+    __shared__ Stage stg;
     __shared__ uint32_t s_ticket;
     const int lane = threadIdx.x;
     gu8* gout = (gu8*)out;
@@ -1059,8 +1089,9 @@ ndfl_inflate_emit_wave_kernel(const uint32_t* w, uint64_t nwords, uint64_t nbits
         while (!block_done) {
             Seg r;
             uint32_t ft;
+            Geo g;
             if (rec != NOREC) {
-                // exact segments from the count pass
+                // exact segments from the count pass, and the round's geometry
                 const SegMeta m = pool.meta[rec];
                 ft = m.ft;
                 r.start = pool.start[(uint64_t)rec * 64 + lane];
@@ -1070,48 +1101,49 @@ ndfl_inflate_emit_wave_kernel(const uint32_t* w, uint64_t nwords, uint64_t nbits
                 r.end = lane < 63 ? nx : m.exit63;
                 r.kind = T_EXIT; r.reason = 0;
                 if ((uint32_t)lane == ft) { r.end = m.end_ft; r.kind = m.kind_ft; r.reason = m.reason_ft; }
+                g = make_geo(in, rs, rs + 1, m.pw);
+                stage_round(in, g, stg, lane);
             } else {
                 uint64_t E = min(next_cand(cands, ncand, rs, ch.end_bit), rs + MAX_SPAN);
                 if (E <= rs) E = rs + 1;
-                round_decode(in, S.t, ed, rs, E, S, lane, r, ft, nslow, nfix, S_ph);
+                round_decode(in, S.t, ed, rs, E, S, stg, lane, r, ft, nslow, nfix, S_ph, g);
             }
             const bool live = (uint32_t)lane <= ft;
             const uint64_t mycnt = live ? r.cnt : 0ull;
             const uint64_t pre = wave_excl_u64(mycnt, lane);
             const uint64_t rsum = wave_sum_u64(mycnt);
             // write pass: every lane runs its segment to the end on its own
-            WLane L;
-            const RB rb = make_rb(in, rs);
-            L.rd.init(rb, (uint32_t)(r.start - rb.base));
-            L.dst0 = base + pre; L.n = 0; L.cnt = mycnt; L.end = (uint32_t)(r.end - rb.base);
-            L.cp_len = 0; L.cp_dist = 0; L.lastb = 0; L.wc = 0; L.wcn = 0;
-            L.q0 = L.q1 = L.q2 = L.q3 = 0; L.qn = 0; L.qaddr = 0; L.lastqw = L.rd.qw;
-            L.kind = r.kind; L.reason = r.reason;
-            L.active = live;
+            const Lv v = make_lv(stg, g, lane);
+            const uint32_t nb = g.nb;
+            uint32_t pos = (uint32_t)(r.start - g.base);
+            uint32_t end = (uint32_t)(r.end - g.base);
+            uint32_t kind = r.kind, rsn = r.reason;
+            const uint64_t dst0 = base + pre;
+            uint64_t n = 0;                 // bytes produced
+            Wr wr;
+            wr.acc = 0; wr.an = 0; wr.dst = dst0;
             uint64_t dfr = ~0ull;           // first deferred byte of this lane (absolute)
             uint64_t lastsrc = 0;           // a byte holding the value of the last output byte
-            while (L.active) {
+            bool active = live;
+            while (active && pos < end) {
                 Tok tk;
-                if (L.rd.pos >= L.end && L.kind == T_EXIT) { L.active = false; break; }
-                next_tok(L.rd, rb, S.t, ed, L.end, tk);
+                if (pos + 48 < end) tok<false>(v, pos, S.t, ed, end, nb, tk);
+                else tok<true>(v, pos, S.t, ed, end, nb, tk);
                 if (tk.kind == K_LIT) {
-                    wputb(L, gout, L.dst0 + L.n, tk.val & 0xFFu);
-                    L.n++;
-                    if (tk.n == 2) { wputb(L, gout, L.dst0 + L.n, tk.val >> 8); L.n++; }
-                    if (L.rd.qw != L.lastqw) { wq_flush(L, gout); L.lastqw = L.rd.qw; }
-                    L.lastb = tk.val >> (tk.n == 2 ? 8 : 0);
-                    lastsrc = L.dst0 + L.n - 1;
+                    wr_lit(wr, gout, tk.val, tk.n);
+                    n += tk.n;
+                    lastsrc = dst0 + n - 1;
                     continue;
                 }
-                if (tk.kind != K_LEN) { L.active = false; break; }     // EOB or error (as verified)
-                if ((uint64_t)tk.dist > L.dst0 + L.n) {
-                    L.kind = T_ERR; L.reason = R_COPY_BEFORE; L.end = L.rd.pos; L.active = false; break;
+                if (tk.kind != K_LEN) break;            // EOB or error (as verified)
+                const uint64_t dst = dst0 + n;
+                if ((uint64_t)tk.dist > dst) {
+                    kind = T_ERR; rsn = R_COPY_BEFORE; end = pos; break;
                 }
-                const uint32_t len = tk.val, dist = tk.dist;
-                const uint64_t dst = L.dst0 + L.n;
+                const uint32_t len = tk.n, dist = tk.dist;
                 const uint64_t src = dst - dist;
                 const uint64_t src_end = src + min(len, dist);          // the copy's bytes before dst
-                bool defer = src < L.dst0;
+                bool defer = src < dst0;
                 if (!defer && src_end > dfr) {
                     // a source at or past our first deferred byte: pending only if its bit is set
                     // (bits of our own range are set by this lane alone, atomically, so an agent-
@@ -1122,14 +1154,14 @@ ndfl_inflate_emit_wave_kernel(const uint32_t* w, uint64_t nwords, uint64_t nbits
                         defer = (__hip_atomic_load(&pend[q], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) & m) != 0;
                     }
                 }
+                wr_flush_word(wr, gout);
                 if (!defer) {
-                    wcopy(L, gout, dst, src, len, dist);                // sources final and our own
+                    wr_copy(gout, dst, len, dist);                  // sources final and our own
                     lastsrc = dst + len - 1;
                 } else {
                     // deferred: back-references (a dist-1 run points at the byte its value comes
                     // from), pending bits; the bytes are written by the resolve rounds
-                    wflush(L, gout, dst);
-                    const uint64_t anchor = dist == 1 ? (L.n > 0 ? lastsrc : src) : 0;
+                    const uint64_t anchor = dist == 1 ? (n > 0 ? lastsrc : src) : 0;
                     for (uint32_t k = 0; k < len; k++) {
                         const uint64_t back = dst + k - anchor;     // a run > 4 GiB falls back to its previous byte
                         ref[dst + k] = dist == 1 ? (back < (1ull << 32) ? (uint32_t)back : 1u) : dist;
@@ -1142,17 +1174,18 @@ ndfl_inflate_emit_wave_kernel(const uint32_t* w, uint64_t nwords, uint64_t nbits
                     if (dist == 1) lastsrc = anchor; else lastsrc = dst + len - 1;
                     dfr = min(dfr, dst);
                 }
-                L.n += len;
+                n += len;
+                wr.dst = dst0 + n;
             }
-            wflush(L, gout, L.dst0 + L.n);
+            wr_flush_exact(wr, gout);
             // the first lane (in stream order) that ended with an error decides
-            const uint64_t em = __ballot(live && L.kind == T_ERR);
+            const uint64_t em = __ballot(live && kind == T_ERR);
             if (em) {
                 const int fl = (int)__builtin_ctzll(em);
                 status = ST_ERROR;
-                reason = __shfl(L.reason, fl, 64);
-                endpos = rb.base + __shfl(L.end, fl, 64);
-                base = __shfl((unsigned long long)(L.dst0 + L.n), fl, 64);
+                reason = __shfl(rsn, fl, 64);
+                endpos = g.base + __shfl(end, fl, 64);
+                base = __shfl((unsigned long long)(dst0 + n), fl, 64);
                 chain_done = true;
                 break;
             }

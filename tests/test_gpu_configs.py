@@ -28,7 +28,10 @@ def ndfl():
 
 @pytest.fixture(scope="module")
 def ctx(ndfl):
-    return ndfl.Context(0)
+    import torch
+    c = ndfl.Context(0)
+    c.set_stream(torch.cuda.current_stream().cuda_stream)     # ordered with torch's kernels
+    return c
 
 
 def test_config2_gzip_64MiB(ndfl, ctx):

@@ -18,8 +18,11 @@ pytestmark = pytest.mark.gpu
 
 @pytest.fixture(scope="module")
 def ctx():
+    import torch
     import ndfl
-    return ndfl.Context(0)
+    c = ndfl.Context(0)
+    c.set_stream(torch.cuda.current_stream().cuda_stream)     # ordered with torch's kernels
+    return c
 
 
 def gpu_inflate(ctx, data):

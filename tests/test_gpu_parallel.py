@@ -17,7 +17,11 @@ pytestmark = pytest.mark.gpu
 def env():
     import torch
     import ndfl
-    return torch, ndfl, ndfl.Context(0)
+    ctx = ndfl.Context(0)
+    # device tensors are written by torch kernels: run the codec on torch's stream (the context's
+    # own stream is non-blocking and would not wait for them)
+    ctx.set_stream(torch.cuda.current_stream().cuda_stream)
+    return torch, ndfl, ctx
 
 
 def test_bits_shift_matches_integer_shift(env):
