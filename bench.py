@@ -8,10 +8,14 @@ step    one round trip over one batch: the rank's 4 GiB shard of the config-4 co
         (RLE_DYNAMIC, 64 KiB blocks, bit-exact with the reference) into one DEFLATE stream, and that
         stream is decompressed again.  Inputs and outputs are resident in HBM (device pointers
         through the C ABI); no host copies inside the timed region.
-N > 1   weak scaling: rank r owns chunks [r*K, (r+1)*K) of ONE global stream.  Ranks exchange the
-        byte before their shard and their compressed bit totals (RCCL all_gather over xGMI), shift
+N > 1   rank r owns chunks [r*K, (r+1)*K) of ONE global stream.  Ranks exchange the bytes before
+        their shard (history) and their compressed bit totals (RCCL all_gather over xGMI), shift
         their bits to the global bit offset on device, and decode their own bit range with the
         previous rank's last 32 KiB of output as the dictionary (RCCL point-to-point).
+        --scaling weak (default): 4 GiB per rank (seed 0xC4 + rank); --scaling strong: config 4 as
+        BASELINE.json defines it, 4 GiB in total split over the ranks, and the step also gathers the
+        global stream onto rank 0 (RCCL point-to-point into its byte offsets, shared bytes ORed on
+        device; --gather adds that to weak scaling too).
 Run: python bench.py [--gpus N --steps K --warmup W]; multi-GPU via torch.distributed.run.
 """
 import argparse
@@ -41,6 +45,9 @@ def main():
     ap.add_argument("--no-cpu", action="store_true")
     ap.add_argument("--no-verify", action="store_true")
     ap.add_argument("--backend", default="nccl", help="nccl (= RCCL over xGMI); gloo only to rehearse N>1 on one GPU")
+    ap.add_argument("--scaling", choices=["weak", "strong"], default="weak",
+                    help="weak: --size bytes per rank; strong: --size bytes in total (config 4), with the gather")
+    ap.add_argument("--gather", action="store_true", help="gather the global stream onto rank 0 in every step")
     args = ap.parse_args()
 
     import torch
@@ -60,8 +67,18 @@ def main():
         else:
             dist.init_process_group(args.backend)
 
-    n = args.size
-    data = corpus.c4_mixed(n, seed=0xC4 + rank, device="cuda")
+    gather = world > 1 and (args.gather or args.scaling == "strong")
+    if args.scaling == "strong" and world > 1:
+        # one global corpus, rank r takes its 64 KiB-aligned share (the last rank the remainder)
+        per = (args.size // world) // 65536 * 65536
+        off = rank * per
+        n = per if rank + 1 < world else args.size - off
+        full = corpus.c4_mixed(args.size, seed=0xC4, device="cuda")
+        data = full[off:off + n].clone()
+        del full
+    else:
+        n = args.size
+        data = corpus.c4_mixed(n, seed=0xC4 + rank, device="cuda")
     torch.cuda.synchronize()
     ctx = ndfl.Context(local)
     L = ndfl._lib.load()
@@ -99,6 +116,8 @@ def main():
             t_c = ctx.timings()["deflate"]
             endbits = part.nbits
             cbytes = (endbits + 7) // 8
+            if gather:
+                state["stream"] = P.gather_stream(codec, dist, torch, part, rank, world)
             r, olen, dl = P.inflate_shard(codec, dist, torch, part, dec, rank, world)
             state["dict_len"] = dl
         if r != 0:
@@ -138,7 +157,12 @@ def main():
         dist.all_reduce(cb)
         c_total = int(cb.item())
 
-    total_in = world * n + c_total       # bytes fed to compress + bytes fed to decompress
+    total_n = n
+    if dist is not None:
+        tn = torch.tensor([n], dtype=torch.int64, device="cpu" if args.backend == "gloo" else "cuda")
+        dist.all_reduce(tn)
+        total_n = int(tn.item())
+    total_in = total_n + c_total         # bytes fed to compress + bytes fed to decompress
     value = total_in / per / MIB
 
     # roofline of the dominant kernel (longest average launch): algorithmic bytes per launch are
@@ -155,7 +179,12 @@ def main():
 
     cpu = None
     if rank == 0 and not args.no_cpu:
-        cpu = cpu_baseline(data, args.cpu_sample, comp if world == 1 else None)
+        # rank 0's shard starts the global stream: its first bits are compared with the oracle's
+        # (on the gathered stream when there is one, else on rank 0's own part)
+        gstream = comp if world == 1 else state.get("stream")
+        if gstream is None and world > 1:
+            gstream = shifted               # rank 0's part sits at bit 0 of its buffer
+        cpu = cpu_baseline(data, args.cpu_sample, gstream)
 
     if rank == 0:
         line = {
@@ -167,14 +196,18 @@ def main():
             "warmup": args.warmup,
             "ms_per_step": round(per * 1e3, 3),
             "higher_is_better": True,
-            "scaling": "weak",
+            "scaling": args.scaling if world > 1 else "weak",
             "vs_baseline": None,
             "dtype": "u8",
-            "data": "synthetic (config-4 Silesia-style mix, seed 0xC4+rank, generated on device)",
+            "data": "synthetic (config-4 Silesia-style mix, generated on device, " +
+                    ("seed 0xC4, one corpus split over the ranks)" if args.scaling == "strong" and world > 1
+                     else "seed 0xC4+rank)"),
             "config": {"workload": "config4: gzip-default (RLE_DYNAMIC, 64 KiB blocks) compress + decompress of a "
-                                   f"{n >> 30} GiB mixed corpus per GPU, bit-exact",
-                       "bytes_per_gpu": n, "compressed_bytes": c_total, "ratio": round(c_total / (world * n), 4),
-                       "parallelism": f"shard-by-block x{world}"},
+                                   + (f"{args.size / 2**30:g} GiB mixed corpus in total" if args.scaling == "strong" and world > 1
+                                      else f"{n / 2**30:g} GiB mixed corpus per GPU") + ", bit-exact",
+                       "bytes_per_gpu": n, "bytes_total": total_n, "compressed_bytes": c_total,
+                       "ratio": round(c_total / total_n, 4), "parallelism": f"shard-by-block x{world}",
+                       "gather_to_rank0": gather},
             "phases_ms": {"deflate_kernel": round(kd, 3), "inflate_find": round(state["t_find"], 3),
                           "inflate_count": round(state["t_count"], 3), "inflate_emit": round(ke, 3),
                           "inflate_device_span": round(state["t_inflate_span"], 3),

@@ -9,7 +9,9 @@ on raw input (D/DeflaterOutputStream.java:119-137).  So rank r 
               (2) all_gather of every shard's bit count and byte count: the seam index;
               (3) each rank moves its bits to its global bit offset mod 8 (ndfl_bits_shift), so
                   the global stream is the concatenation of the shards with the shared boundary
-                  bytes ORed (BitOut's packing, D/DeflaterOutputStream.java:147-156).
+                  bytes ORed (BitOut's packing, D/DeflaterOutputStream.java:147-156);
+              (4) gather_stream: the root receives every part at its byte offset (point to point)
+                  and ORs the shared bytes on device -- one global stream on one GPU.
   decompress  each rank decodes its seam-delimited bit range with a deferred window
               (ndfl_inflate_range + NDFL_DICT_DEFERRED), all ranks in parallel; then the last
               32 KiB of output pass from rank to rank (the reference's dictionary ring,
@@ -185,6 +187,58 @@ def inflate_shard(codec, dist, torch, part, out, rank, world):
     codes = _gather_ints(dist, torch, code, world, codec.device)
     first = next((c for c in codes if c != 0), 0)
     return first, olen, dict_len
+
+
+def gather_stream(codec, dist, torch, part, rank, world, root=0):
+    """Reassemble the global stream on `root` (SURVEY §8e compress step 4): every rank sends its
+    realigned part -- the first byte (shared with the previous shard when the global bit offset is
+    not byte-aligned) and the body -- and the root receives each body straight into its byte offset
+    of the output buffer (point to point over RCCL/xGMI; ncclGather needs equal counts), then ORs the
+    first bytes in: BitOut's byte packing (D/DeflaterOutputStream.java:147-156) across GPUs, on
+    device.  Returns the stream tensor (bytes ceil(total bits / 8)) on the root, None elsewhere."""
+    offs = part.bit_offsets
+    B = [o // 8 for o in offs[:-1]]
+    nb = [(offs[r] % 8 + offs[r + 1] - offs[r] + 7) // 8 for r in range(world)]
+    total = (offs[-1] + 7) // 8
+    staged = _staged(dist, part.buf)
+    if rank == root:
+        out = torch.zeros(max(1, total), dtype=torch.uint8, device=codec.device)
+        firsts = torch.zeros(world, dtype=torch.uint8, device=codec.device)
+        ops = []
+        for r in range(world):
+            if nb[r] == 0:
+                continue
+            if r == rank:
+                out[B[r] + 1:B[r] + nb[r]] = part.buf[1:nb[r]]
+                firsts[r:r + 1] = part.buf[0:1]
+                continue
+            if staged:
+                if nb[r] > 1:
+                    _recv(dist, out[B[r] + 1:B[r] + nb[r]], r)
+                _recv(dist, firsts[r:r + 1], r)
+            else:
+                if nb[r] > 1:
+                    ops.append(dist.P2POp(dist.irecv, out[B[r] + 1:B[r] + nb[r]], r))
+                ops.append(dist.P2POp(dist.irecv, firsts[r:r + 1], r))
+        if ops:
+            for req in dist.batch_isend_irecv(ops):
+                req.wait()
+        for r in range(world):
+            if nb[r]:
+                out[B[r]:B[r] + 1].bitwise_or_(firsts[r:r + 1])
+        return out[:total]
+    if nb[rank]:
+        if staged:
+            if nb[rank] > 1:
+                _send(dist, part.buf[1:nb[rank]], root)
+            _send(dist, part.buf[0:1], root)
+        else:
+            ops = [dist.P2POp(dist.isend, part.buf[0:1].contiguous(), root)]
+            if nb[rank] > 1:
+                ops.insert(0, dist.P2POp(dist.isend, part.buf[1:nb[rank]], root))
+            for req in dist.batch_isend_irecv(ops):
+                req.wait()
+    return None
 
 
 def assemble(parts):

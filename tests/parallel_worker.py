@@ -96,11 +96,15 @@ def main():
     allp = [None] * world
     dist.all_gather_object(allp, mine)
     ok = {}
+    gathered = P.gather_stream(codec, dist, torch, part, rank, world)
     if rank == 0:
         stream = P.assemble(allp)
         ref = O.deflate(data, cfg["strategy"], chunk)
         ok["stream_equal"] = stream == ref
+        ok["gathered_equal"] = bytes(gathered.cpu().numpy()) == ref
         ok["total_bits"] = part.bit_offsets[-1]
+    else:
+        ok["gathered_equal"] = gathered is None
     out = torch.zeros(P.WINDOW + sizes[rank] + 64, dtype=torch.uint8, device=codec.device)
     code, olen, dict_len = P.inflate_shard(codec, dist, torch, part, out, rank, world)
     ok["code"] = code

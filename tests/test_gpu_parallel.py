@@ -148,4 +148,5 @@ def test_sharded_protocol_two_ranks_one_gpu():
     res = run_workers(2, dict(chunk_len=65536, chunks_per_rank=6, last_bytes=300001, seed=9,
                               strategy="RLE_DYNAMIC", seam_run=True, codec="device"))
     assert res[0]["stream_equal"]
+    assert all(r["gathered_equal"] for r in res)      # the device gather onto rank 0
     assert all(r["code"] == 0 and r["decoded_equal"] for r in res)

@@ -39,6 +39,7 @@ def run_workers(world, cfg):
 def test_sharded_stream_roundtrip(world, cfg):
     res = run_workers(world, cfg)
     assert res[0]["stream_equal"], "assembled shards differ from the single-stream encoding"
+    assert all(r["gathered_equal"] for r in res), "the root's gathered stream differs from the oracle's"
     for r in res:
         assert r["code"] == 0
         assert r["decoded_equal"]
