@@ -965,3 +965,5 @@ int ndfl_bits_shift(ndfl_ctx* c, const uint8_t* in, uint64_t nbits, uint32_t shi
 }
 
 }  // extern "C"
+
+#include "ndfl_plugin.cpp"

@@ -19,7 +19,7 @@ import io
 from . import _lib
 from ._lib import IN_DEVICE, OUT_DEVICE, DICT_DEFERRED, IN_PADDED, IN_PAD_BYTES, IN_PARTIAL, NEED_INPUT, NO_END, STRATEGIES, NdflError, check, load, reason_name
 
-__all__ = ["Context", "Reason", "DataFormatException", "Lz77Huffman", "Uncompressed", "MultiStrategy", "BinarySplit", "DeflaterOutputStream", "InflaterInputStream",
+__all__ = ["Context", "Reason", "DataFormatException", "Lz77Huffman", "Uncompressed", "MultiStrategy", "BinarySplit", "DeflaterOutputStream", "InflaterInputStream", "BitOutputStream",
            "GzipMetadata", "GzipOutputStream", "GzipInputStream", "ZlibMetadata", "ZlibOutputStream",
            "ZlibInputStream", "Strategy", "default_context", "compress", "decompress", "crc32_combine"]
 
@@ -95,6 +95,14 @@ class Lz77Huffman:
     def __repr__(self):
         return f"Lz77Huffman({self.useDynamicHuffmanCodes}, {', '.join(map(str, self.params))})"
 
+    def decide(self, b, off, historyLen, dataLen):
+        """Strategy.decide (D/comp/Lz77Huffman.java:42-59), encoded on the GPU (ndfl_decide)."""
+        return self._decide(b, off, historyLen, dataLen)
+
+    def _decide(self, b, off, historyLen, dataLen, context=None):
+        from .plugin import library_decide
+        return library_decide(self, b, off, historyLen, dataLen, context)
+
 
 Lz77Huffman.LITERAL_STATIC = Lz77Huffman(False, 0, 0, 0, 0)
 Lz77Huffman.LITERAL_DYNAMIC = Lz77Huffman(True, 0, 0, 0, 0)
@@ -110,6 +118,14 @@ class _UncompressedType:
     def __repr__(self):
         return "Uncompressed.SINGLETON"
 
+    def decide(self, b, off, historyLen, dataLen):
+        """Strategy.decide (D/comp/Uncompressed.java:22-51)."""
+        return self._decide(b, off, historyLen, dataLen)
+
+    def _decide(self, b, off, historyLen, dataLen, context=None):
+        from .plugin import library_decide
+        return library_decide(self, b, off, historyLen, dataLen, context)
+
 
 class Uncompressed:
     SINGLETON = _UncompressedType()
@@ -117,8 +133,9 @@ class Uncompressed:
 
 class MultiStrategy:
     """MultiStrategy(strats...) (D/comp/MultiStrategy.java:19-57): per chunk and output bit position,
-    the first substrategy giving the fewest bits.  Substrategies: Lz77Huffman or Uncompressed
-    (at most 8 on the GPU path)."""
+    the first substrategy giving the fewest bits.  Substrategies: any Strategy (the library's
+    classes, or a user object with decide()); a flat list of at most 8 Lz77Huffman / Uncompressed
+    runs batched on the GPU (ndfl_deflate_chunks_multi), anything else per chunk (ndfl.plugin)."""
 
     def __init__(self, *strats):
         if strats is None or any(s is None for s in strats):
@@ -126,15 +143,23 @@ class MultiStrategy:
         if len(strats) == 0:
             raise ValueError("Empty list of strategies")
         for st in strats:
-            if not isinstance(st, (Lz77Huffman, _UncompressedType)):
-                raise TypeError(f"unsupported substrategy {st!r}")
+            if not (isinstance(st, Strategy) or hasattr(st, "decide")):
+                raise TypeError(f"not a strategy: {st!r}")
         self.substrategies = tuple(strats)
+
+    def decide(self, b, off, historyLen, dataLen):
+        return self._decide(b, off, historyLen, dataLen)
+
+    def _decide(self, b, off, historyLen, dataLen, context=None):
+        from .plugin import library_decide
+        return library_decide(self, b, off, historyLen, dataLen, context)
 
 
 class BinarySplit:
     """BinarySplit(strat, minBlockLen) (D/comp/BinarySplit.java:15-82): halve each chunk recursively
-    while both halves exceed minBlockLen, keeping a split when it takes fewer bits.  On the GPU path
-    the substrategy must be an Lz77Huffman."""
+    while both halves exceed minBlockLen, keeping a split when it takes fewer bits.  Over an
+    Lz77Huffman the whole stream is batched on the GPU (ndfl_deflate_chunks_binsplit); over any
+    other Strategy it runs per chunk (ndfl.plugin: ndfl_decide for the library's classes)."""
 
     def __init__(self, strat, minBlockLen):
         if strat is None:
@@ -143,6 +168,13 @@ class BinarySplit:
             raise ValueError("Non-positive minimum block length")
         self.substrategy = strat
         self.minimumBlockLength = int(minBlockLen)
+
+    def decide(self, b, off, historyLen, dataLen):
+        return self._decide(b, off, historyLen, dataLen)
+
+    def _decide(self, b, off, historyLen, dataLen, context=None):
+        from .plugin import library_decide
+        return library_decide(self, b, off, historyLen, dataLen, context)
 
 
 def _desc(st):
@@ -308,6 +340,23 @@ class Context:
         return v.value
 
 
+def _ctx_default(context):
+    return context if context is not None else default_context()
+
+
+def _batchable(s):
+    """Strategies the batched GPU calls take whole (ndfl_deflate_chunks / _lz77 / _multi /
+    _binsplit); others go chunk by chunk through the plugin API."""
+    if isinstance(s, (Strategy, str, int, Lz77Huffman, _UncompressedType)):
+        return True
+    if isinstance(s, MultiStrategy):
+        return len(s.substrategies) <= 8 and all(isinstance(x, (Lz77Huffman, _UncompressedType))
+                                                 for x in s.substrategies)
+    if isinstance(s, BinarySplit):
+        return isinstance(s.substrategy, Lz77Huffman)
+    return False
+
+
 def _strategy_id(s):
     if isinstance(s, (Lz77Huffman, MultiStrategy, _UncompressedType, BinarySplit)):
         return s
@@ -345,3 +394,4 @@ def decompress(data):
 
 from .streams import (DeflaterOutputStream, InflaterInputStream, GzipMetadata, GzipOutputStream,  # noqa: E402
                       GzipInputStream, ZlibMetadata, ZlibOutputStream, ZlibInputStream)
+from .plugin import BitOutputStream  # noqa: E402

@@ -37,9 +37,19 @@ EXPORTS = ["ndfl_abi_version", "ndfl_error_string", "ndfl_ctx_create", "ndfl_ctx
            "ndfl_deflate_chunks_lz77", "ndfl_deflate_chunks_multi", "ndfl_deflate_chunks_binsplit",
            "ndfl_deflate_bound",
            "ndfl_inflate", "ndfl_inflate_range", "ndfl_inflate_resolve", "ndfl_bits_shift", "ndfl_crc32", "ndfl_adler32",
-           "ndfl_crc32_combine"]
+           "ndfl_crc32_combine", "ndfl_decide", "ndfl_compress_to", "ndfl_decision_free"]
 
 KIND_LZ77, KIND_UNCOMPRESSED = 0, 1
+
+
+KIND_MULTI, KIND_BINSPLIT = 2, 3
+
+
+class StrategyNode(ctypes.Structure):
+    """ndfl_strategy_node (include/ndfl.h)."""
+    _fields_ = [("kind", ctypes.c_int32), ("dynamic", ctypes.c_int32), ("min_run", ctypes.c_int32),
+                ("max_run", ctypes.c_int32), ("min_dist", ctypes.c_int32), ("max_dist", ctypes.c_int32),
+                ("first_child", ctypes.c_int32), ("n_children", ctypes.c_int32), ("min_block_len", ctypes.c_int32)]
 
 
 class StrategyDesc(ctypes.Structure):
@@ -85,6 +95,10 @@ def load():
     L.ndfl_bits_shift.argtypes = [vp, vp, u64, u32, vp, u64, u32]
     L.ndfl_crc32.argtypes = [vp, ctypes.POINTER(u32), vp, u64, u32]
     L.ndfl_adler32.argtypes = [vp, ctypes.POINTER(u32), vp, u64, u32]
+    L.ndfl_decide.argtypes = [vp, ctypes.POINTER(StrategyNode), u32, u32, vp, u64, u32, u32,
+                              ctypes.POINTER(u64), ctypes.POINTER(vp)]
+    L.ndfl_compress_to.argtypes = [vp, vp, i32, u32, vp, u64, ctypes.POINTER(u64)]
+    L.ndfl_decision_free.argtypes = [vp]
     L.ndfl_crc32_combine.restype = u32
     L.ndfl_crc32_combine.argtypes = [u32, u32, u64]
     _lib = L

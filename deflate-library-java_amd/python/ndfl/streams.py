@@ -27,7 +27,7 @@ class DeflaterOutputStream:
 
     def __init__(self, out, dataLookaheadLimit=64 * 1024, historyLookbehindLimit=32 * 1024, strategy=None,
                  context=None, batch_bytes=64 << 20):
-        from . import Strategy, _strategy_id
+        from . import Strategy, _strategy_id, _batchable
         if out is None:
             raise TypeError("out")
         if (dataLookaheadLimit < 1 or historyLookbehindLimit < 0 or historyLookbehindLimit > 32 * 1024
@@ -36,7 +36,13 @@ class DeflaterOutputStream:
         self._out = out
         self._chunk = dataLookaheadLimit
         self._hist_limit = historyLookbehindLimit
-        self._strategy = _strategy_id(strategy if strategy is not None else Strategy.RLE_DYNAMIC)
+        strategy = strategy if strategy is not None else Strategy.RLE_DYNAMIC
+        # the batched GPU calls take the library's strategies whole; any other Strategy (a user
+        # object with decide(), or trees the batched calls do not cover) runs chunk by chunk
+        # through the plugin API, as Strategy.decide / Decision.compressTo (D/DeflaterOutputStream.java:119-137)
+        self._plugin = None if _batchable(strategy) else strategy
+        self._strategy = _strategy_id(strategy) if self._plugin is None else None
+        self._strategy_obj = strategy
         self._ctx = _ctx(context)
         self._batch = max(batch_bytes, dataLookaheadLimit + 1)
         self._pending = bytearray()
@@ -77,15 +83,29 @@ class DeflaterOutputStream:
             if take == 0:
                 return
         data = bytes(self._pending[:take])
+        if self._plugin is not None:
+            self._flush_plugin(data, final)
+            del self._pending[:take]
+            return
         L = load()
         cap = L.ndfl_deflate_bound(take, self._chunk) + 16
         out = ctypes.create_string_buffer(cap)
         src = ctypes.create_string_buffer(data, max(1, len(data)))
         hist = ctypes.create_string_buffer(self._hist, max(1, len(self._hist)))
-        endbits, crc = self._ctx.deflate_chunks_raw(
-            ctypes.addressof(hist) if self._hist else None, len(self._hist), self._hist_limit,
-            ctypes.addressof(src), take, self._chunk, self._strategy, final, self._bitlen,
-            ctypes.addressof(out), cap, 0, crc=self._crc)
+        try:
+            endbits, crc = self._ctx.deflate_chunks_raw(
+                ctypes.addressof(hist) if self._hist else None, len(self._hist), self._hist_limit,
+                ctypes.addressof(src), take, self._chunk, self._strategy, final, self._bitlen,
+                ctypes.addressof(out), cap, 0, crc=self._crc)
+        except _lib.NdflError as e:
+            if e.code != _lib.E_UNSUPPORTED:
+                raise
+            # a configuration the batched call does not take (e.g. BinarySplit halvings of odd
+            # lengths): the plugin path from here on
+            self._plugin = self._strategy_obj
+            self._flush_plugin(data, final)
+            del self._pending[:take]
+            return
         if self._crc is not None:
             self._crc = crc
         if self._adler is not None and data:
@@ -101,6 +121,32 @@ class DeflaterOutputStream:
         del self._pending[:take]
         if self._hist_limit:
             self._hist = (self._hist + data)[-self._hist_limit:]
+
+    def _flush_plugin(self, data, final):
+        """Chunk by chunk: Strategy.decide(combined, 0, historyLen, dataLen) then
+        Decision.compressTo(bitOut, isFinal) (D/DeflaterOutputStream.java:119-137)."""
+        from .plugin import BitBuffer, decide_any
+        bo = BitBuffer(self._bitlen, self._bitbuf)
+        n = len(data)
+        pos = 0
+        while True:
+            k = min(self._chunk, n - pos)
+            last = final and pos + k == n
+            combined = self._hist + data[pos:pos + k]
+            dec = decide_any(self._plugin, combined, 0, len(self._hist), k, self._ctx)
+            dec.compressTo(bo, last)
+            if self._hist_limit:
+                self._hist = combined[-self._hist_limit:]
+            pos += k
+            if pos >= n:
+                break
+        if self._crc is not None and data:
+            self._crc = self._ctx.crc32(data, self._crc)
+        if self._adler is not None and data:
+            self._adler = self._ctx.adler32(data, self._adler)
+        self._out.write(bo.take_bytes())
+        self._bitlen = bo.nbits & 7
+        self._bitbuf = bo.partial
 
     def finish(self):
         if self._ended:

@@ -155,6 +155,37 @@ int ndfl_deflate_chunks_binsplit(ndfl_ctx* ctx, const uint8_t* hist, uint32_t hi
                                  int32_t min_block_len, int final_flag, uint32_t start_bitpos, uint8_t* out,
                                  uint64_t out_cap, uint64_t* out_end_bits, uint32_t* crc_inout, uint32_t flags);
 
+/*
+ * The compressor plugin API (D/comp/Strategy.java:14, D/comp/Decision.java:16-19): one chunk,
+ * any strategy tree.  A strategy is an array of nodes; node `root` is the strategy:
+ *   NDFL_KIND_LZ77          Lz77Huffman(dynamic, min_run, max_run, min_dist, max_dist)
+ *   NDFL_KIND_UNCOMPRESSED  Uncompressed.SINGLETON
+ *   NDFL_KIND_MULTI         MultiStrategy(nodes[first_child .. first_child + n_children))
+ *   NDFL_KIND_BINSPLIT      BinarySplit(nodes[first_child], min_block_len)
+ * ndfl_decide = Strategy.decide(b, off, historyLen, dataLen) on the GPU encoders: the data is
+ * b[off + history_len, + data_len) (host memory, <= 65536 bytes), preceded by its history;
+ * bit_lengths[i] = Decision.getBitLengths()[i], the block's bits when it starts at bit position
+ * i (mod 8).  The decision keeps a pointer to `b` (as the Java Decision closes over it): keep b
+ * valid until the decision is freed.  NDFL_E_ARG for the constructors' IllegalArgumentExceptions
+ * (Lz77Huffman parameters, empty MultiStrategy, minBlockLen < 1) and malformed trees.
+ * ndfl_compress_to = Decision.compressTo(out, isFinal): writes the block(s) at bit start_bitpos of
+ * out[0] (lower bits kept), *out_end_bits = start_bitpos + bits written.
+ */
+#define NDFL_KIND_MULTI         2
+#define NDFL_KIND_BINSPLIT      3
+typedef struct {
+    int32_t kind;                                        /* NDFL_KIND_* */
+    int32_t dynamic, min_run, max_run, min_dist, max_dist;   /* LZ77 */
+    int32_t first_child, n_children;                     /* MULTI / BINSPLIT (n_children unused) */
+    int32_t min_block_len;                               /* BINSPLIT */
+} ndfl_strategy_node;
+typedef struct ndfl_decision ndfl_decision;
+int ndfl_decide(ndfl_ctx* ctx, const ndfl_strategy_node* nodes, uint32_t n_nodes, uint32_t root, const uint8_t* b,
+                uint64_t off, uint32_t history_len, uint32_t data_len, uint64_t* bit_lengths, ndfl_decision** out);
+int ndfl_compress_to(ndfl_ctx* ctx, const ndfl_decision* dec, int is_final, uint32_t start_bitpos, uint8_t* out,
+                     uint64_t out_cap, uint64_t* out_end_bits);
+int ndfl_decision_free(ndfl_decision* dec);
+
 /* Upper bound of output bytes of ndfl_deflate_chunks for `len` bytes. */
 uint64_t ndfl_deflate_bound(uint64_t len, uint32_t chunk_len);
 

@@ -169,3 +169,18 @@ def test_nversion_binarysplit(sub):
             b = P.deflate_binsplit(data, sub, m, chunk_len, hist)
             assert a == b, (sub, len(data), chunk_len, hist, m)
             assert zlib.decompress(a, -15) == data
+
+
+def test_strategy_ref_pinned_by_oracle():
+    """tests/strategy_ref.py (the checker of the GPU plugin tests) agrees with the oracle's own
+    MultiStrategy / BinarySplit drivers wherever both apply."""
+    import random
+    import strategy_ref as R
+    rng = random.Random(3)
+    data = b"".join(bytes([rng.randrange(3)]) * rng.randrange(1, 400) + rng.randbytes(rng.randrange(0, 300))
+                    for _ in range(600))[:150_000]
+    assert R.stream(data, R.LzLeaf("RLE_DYNAMIC")) == O.deflate(data, "RLE_DYNAMIC")
+    assert R.stream(data, R.Multi(R.LzLeaf("RLE_DYNAMIC"), R.UncLeaf())) == \
+        O.deflate_multi(data, [(1, 3, 258, 1, 1), "UNCOMPRESSED"])
+    assert R.stream(data, R.Split(R.UncLeaf(), 1000)) == O.deflate_binsplit(data, "UNCOMPRESSED", 1000)
+    assert R.stream(data, R.Split(R.LzLeaf("RLE_DYNAMIC"), 2000)) == O.deflate_binsplit(data, (1, 3, 258, 1, 1), 2000)
