@@ -1,0 +1,213 @@
+/*
+ * Drop-in for io.nayuki.deflate.InflaterInputStream (D/InflaterInputStream.java:26-181) on the GPU.
+ * The underlying stream is read in batches of at least inBufLen (default 64 MiB) bytes; each batch
+ * is decoded by ndfl_inflate_range with NDFL_IN_PARTIAL, which stops at the last block boundary the
+ * batch completes -- Open.read's incremental refill (D/decomp/Open.java:137-192) at block
+ * granularity -- and the decode continues from that bit with the last 32 KiB of output as the
+ * window (the reference's dictionary ring, :592-603).  With endExactly the underlying stream is
+ * reset to its mark and skipped to the byte after the final block (Open.finish, :113-124).
+ * Errors: a Reason code raises DataFormatException after the bytes decoded before the error were
+ * served (not sticky); an IOException of the underlying stream is sticky (:152-159).
+ */
+package io.nayuki.deflate.gpu;
+
+import java.io.IOException;
+import java.io.InputStream;
+import java.nio.ByteBuffer;
+import java.util.Objects;
+import io.nayuki.deflate.DataFormatException;
+
+
+public final class InflaterInputStream extends InputStream {
+	
+	static final int BATCH = 64 << 20;
+	private static final int WINDOW = 32768;
+	
+	private InputStream input;
+	private final boolean endExactly;
+	private final int batch;
+	private final NativeCodec codec;
+	private ByteBuffer in;               // unconsumed input (direct); byte 0 holds bit `bit` of the stream
+	private int bit = 0;
+	private boolean eof = false, last = false;
+	private ByteBuffer out;              // window ++ decoded batch (direct)
+	private int outPos = 0, outEnd = 0, windowLen = 0;
+	private DataFormatException error = null;
+	private IOException sticky = null;
+	private boolean closed = false;
+	
+	
+	public InflaterInputStream(InputStream in) throws IOException {
+		this(in, false);
+	}
+	
+	
+	public InflaterInputStream(InputStream in, boolean endExactly) throws IOException {
+		this(in, endExactly, 16 * 1024);
+	}
+	
+	
+	public InflaterInputStream(InputStream in, boolean endExactly, int inBufLen) throws IOException {
+		input = Objects.requireNonNull(in);
+		if (inBufLen <= 0)
+			throw new IllegalArgumentException("Non-positive input buffer size");
+		if (endExactly) {
+			if (!in.markSupported())
+				throw new IllegalArgumentException("Input stream not markable, cannot support detachment");
+			in.mark(Integer.MAX_VALUE);
+		}
+		this.endExactly = endExactly;
+		batch = Math.max(inBufLen, BATCH);
+		codec = new NativeCodec(0);
+		this.in = ByteBuffer.allocateDirect(batch + 256);
+		this.in.limit(0);
+	}
+	
+	
+	@Override public int read() throws IOException {
+		var b = new byte[1];
+		return switch (read(b)) {
+			case  1 -> b[0] & 0xFF;
+			case -1 -> -1;
+			default -> throw new AssertionError("Unreachable value");
+		};
+	}
+	
+	
+	@Override public int read(byte[] b, int off, int len) throws IOException {
+		Objects.requireNonNull(b);
+		Objects.checkFromIndexSize(off, len, b.length);
+		if (closed)
+			throw new IllegalStateException("Stream already closed");
+		if (sticky != null)
+			throw sticky;
+		int result = 0;
+		while (result < len) {
+			if (outPos == outEnd) {
+				if (error != null || last)
+					break;
+				try {
+					fill();
+				} catch (IOException e) {
+					sticky = e;
+					throw e;
+				}
+				continue;
+			}
+			int n = Math.min(len - result, outEnd - outPos);
+			out.get(outPos, b, off + result, n);
+			outPos += n;
+			result += n;
+		}
+		if (result == 0 && len > 0) {
+			if (error != null)
+				throw error;
+			return -1;
+		}
+		return (result > 0 || !last || outPos < outEnd) ? result : -1;
+	}
+	
+	
+	// decode the next batch (D/decomp/Open.java:83-124 over a bounded input buffer)
+	private void fill() throws IOException {
+		// the previous batch is fully served: its last <= 32 KiB become the window
+		if (outEnd > 0) {
+			int keep = Math.min(WINDOW, outEnd);
+			var w = new byte[keep];
+			out.get(outEnd - keep, w);
+			out.put(0, w);
+			windowLen = keep;
+			outPos = outEnd = 0;
+		}
+		int want = batch;
+		while (true) {
+			readMore(want);
+			long inLen = in.limit();
+			long need = windowLen + 4 * inLen + 65536;
+			var res = new long[2];
+			int r;
+			while (true) {
+				prepareOut(need);
+				r = NativeCodec.inflateRange0(codec.handle(), in, inLen, bit, out, windowLen, !eof, res);
+				if (r != NativeCodec.E_CAPACITY)
+					break;
+				need = windowLen + res[0] + 16;
+			}
+			if (r == NativeCodec.NEED_INPUT && res[0] == 0 && res[1] == bit) {
+				want = in.limit() + batch;          // no block completed in this batch: read more
+				continue;
+			}
+			outPos = windowLen;
+			outEnd = windowLen + (int)res[0];
+			long bits = res[1];
+			if (r == NativeCodec.NEED_INPUT) {
+				consume((int)(bits >>> 3));
+				bit = (int)(bits & 7);
+			} else if (r == 0) {
+				last = true;
+				if (endExactly) {
+					// Open.finish: reset to the mark, skip the bytes consumed (a partly used byte counts)
+					int used = (int)((bits + 7) >>> 3);
+					input.reset();
+					input.skipNBytes(consumedBefore + used);
+				}
+			} else {
+				error = new DataFormatException(DataFormatException.Reason.values()[r - 1], "GPU decode: " + r);
+			}
+			return;
+		}
+	}
+	
+	
+	private long consumedBefore = 0;     // input bytes dropped from the front of `in`
+	
+	private void readMore(int want) throws IOException {
+		if (in.capacity() < want + 256) {
+			var bigger = ByteBuffer.allocateDirect(want + 256);
+			bigger.put(in.duplicate().position(0).limit(in.limit())).flip();
+			in = bigger;
+		}
+		var tmp = new byte[65536];
+		while (in.limit() < want && !eof) {
+			int n = input.read(tmp, 0, Math.min(tmp.length, want - in.limit()));
+			if (n == -1)
+				eof = true;
+			else {
+				int p = in.limit();
+				in.limit(p + n);
+				in.put(p, tmp, 0, n);
+			}
+		}
+	}
+	
+	private void consume(int bytes) {
+		var rest = in.duplicate().position(bytes).limit(in.limit()).slice();
+		int n = rest.remaining();
+		var tmp = new byte[n];
+		rest.get(tmp);
+		in.clear();
+		in.put(tmp).flip();
+		consumedBefore += bytes;
+	}
+	
+	private void prepareOut(long need) {
+		if (out == null || out.capacity() < need) {
+			var bigger = ByteBuffer.allocateDirect((int)Math.min(need, Integer.MAX_VALUE - 8));
+			if (out != null && windowLen > 0) {
+				var w = new byte[windowLen];
+				out.get(0, w);
+				bigger.put(0, w);
+			}
+			out = bigger;
+		}
+	}
+	
+	
+	@Override public void close() throws IOException {
+		if (!closed)
+			input.close();
+		closed = true;
+		codec.close();
+	}
+	
+}

@@ -1,0 +1,75 @@
+/*
+ * JNI facade over libndfl.so (include/ndfl.h); the glue is native/ndfl_jni.c.  One codec per stream
+ * object, not thread-safe (the reference's streams are not either).  Built only where a JDK exists:
+ * this image has none, so these sources are compiled by a maintainer, not by our tests.
+ */
+package io.nayuki.deflate.gpu;
+
+import java.io.IOException;
+import java.nio.ByteBuffer;
+
+
+final class NativeCodec implements AutoCloseable {
+	
+	static {
+		System.loadLibrary("ndfl");
+		System.loadLibrary("ndfl_jni");
+	}
+	
+	static final int NEED_INPUT = 64;        // NDFL_NEED_INPUT
+	static final int E_CAPACITY = -3;        // NDFL_E_CAPACITY
+	static final int E_UNSUPPORTED = -2;     // NDFL_E_UNSUPPORTED
+	static final int KIND_LZ77 = 0, KIND_UNCOMPRESSED = 1, KIND_MULTI = 2, KIND_BINSPLIT = 3;
+	
+	private long ctx;
+	
+	
+	NativeCodec(int device) throws IOException {
+		ctx = create(device);
+	}
+	
+	
+	long handle() {
+		if (ctx == 0)
+			throw new IllegalStateException("Codec closed");
+		return ctx;
+	}
+	
+	
+	@Override public void close() {
+		if (ctx != 0) {
+			destroy(ctx);
+			ctx = 0;
+		}
+	}
+	
+	
+	/*---- native entry points (ndfl_jni.c) ----*/
+	
+	static native long create(int device) throws IOException;
+	static native void destroy(long ctx);
+	
+	// end bit in res[0]; returns 0 or a negative code not thrown (NDFL_E_CAPACITY / _UNSUPPORTED)
+	static native int deflateChunks0(long ctx, ByteBuffer hist, int histLen, int histLimit, ByteBuffer data,
+		long len, int chunkLen, int strategy, boolean isFinal, int startBitPos, ByteBuffer out, long[] res, int[] crc);
+	static native int deflateChunksLz770(long ctx, ByteBuffer hist, int histLen, int histLimit, ByteBuffer data,
+		long len, int chunkLen, boolean dynamic, int minRun, int maxRun, int minDist, int maxDist, boolean isFinal,
+		int startBitPos, ByteBuffer out, long[] res, int[] crc);
+	static native int deflateChunksMulti0(long ctx, ByteBuffer hist, int histLen, int histLimit, ByteBuffer data,
+		long len, int chunkLen, int[] subs, boolean isFinal, int startBitPos, ByteBuffer out, long[] res, int[] crc);
+	static native long deflateBound0(long len, int chunkLen);
+	
+	// res[0] = bytes decoded after the window, res[1] = consumed bits
+	static native int inflateRange0(long ctx, ByteBuffer in, long inLen, long startBit, ByteBuffer out, long dictLen,
+		boolean partial, long[] res);
+	
+	static native int crc320(long ctx, int crc, ByteBuffer data, long len);
+	static native int adler320(long ctx, int adler, ByteBuffer data, long len);
+	
+	// the plugin API: strategy tree (9 ints per node) -> decision handle; compressTo -> end bit or -1
+	static native long decide0(long ctx, int[] nodes, int root, byte[] b, int off, int historyLen, int dataLen,
+		long[] bitLengths);
+	static native long compressTo0(long ctx, long dec, boolean isFinal, int startBitPos, byte[] out);
+	static native void freeDecision0(long dec);
+	
+}
