@@ -226,11 +226,13 @@ def main():
 
 
 def pmc_traffic(kernel, n):
-    """HBM bytes per launch of `kernel` from the committed rocprofv3 --pmc summary of this same bench
-    command (profiles/r01_traffic.json, made by scripts/profile_bench.sh + scripts/traffic_summary.py:
+    """HBM bytes per launch of `kernel` from the newest committed rocprofv3 --pmc summary of this same
+    bench command (profiles/rNN_traffic.json, made by scripts/profile_bench.sh + scripts/traffic_summary.py:
     FETCH_SIZE and WRITE_SIZE passes, gfx950 corrections applied).  Counters cannot be read from inside
     the timed run, so the value is the profiled one, quoted only for the default 4 GiB workload."""
-    path = os.path.join(ROOT, "profiles", "r01_traffic.json")
+    import glob
+    found = sorted(glob.glob(os.path.join(ROOT, "profiles", "r[0-9][0-9]_traffic.json")))
+    path = found[-1] if found else os.path.join(ROOT, "profiles", "r01_traffic.json")
     if n != 4 << 30 or not os.path.exists(path):
         return None, None
     tab = json.load(open(path))
@@ -238,7 +240,7 @@ def pmc_traffic(kernel, n):
     if any(r is None for r in recs):
         return None, None
     fb, wb = sum(r["fetch_bytes"] for r in recs), sum(r["write_bytes"] for r in recs)
-    return fb + wb, f"profiles/r01_traffic.json (fetch {fb} B + write {wb} B per launch)"
+    return fb + wb, f"profiles/{os.path.basename(path)} (fetch {fb} B + write {wb} B per launch)"
 
 
 def _cpu_model():

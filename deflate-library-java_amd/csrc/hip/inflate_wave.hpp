@@ -118,7 +118,7 @@ struct Tok {
 #define NDFL_LPW 16
 #endif
 constexpr uint32_t LPW = NDFL_LPW;             // words per lane segment at most (512 bits by default)
-constexpr uint32_t SW = LPW + 4;               // staged words per lane region
+constexpr uint32_t SW = LPW + 4;               // staged words per lane region (+ the tail window)
 constexpr uint64_t RSPAN = 64ull * LPW * 32;   // round span cap (bits)
 
 struct Stage {
@@ -161,9 +161,10 @@ __device__ __forceinline__ void stage_round(const In& in, const Geo& g, Stage& s
     __syncthreads();
 }
 
-// The lane's view of the staged round: 64 bits of input from relative bit `pos`.
+// The lane's view of the staged round: 64 bits of input from relative bit `pos`.  (A cached 128-bit
+// window re-read every two words was measured slower: the selects cost more than the LDS read.)
 struct Lv {
-    const uint32_t* p;     // &st.w[lane] less the region's first word (as a row offset)
+    const uint32_t* p;     // &st.w[lane]
     uint32_t rw;           // region's first word (relative to base)
     __device__ __forceinline__ void win(uint32_t pos, uint32_t& lo, uint32_t& hi) const {
         const uint32_t* q = p + ((pos >> 5) - rw) * 64;
@@ -473,8 +474,9 @@ struct Spec {
     uint32_t cp1, cpc1, cp2, cpc2;
 };
 
-__device__ __forceinline__ void spec_run(const Lv& v, const Tabs& t, bool ed, uint32_t nb, uint32_t st, uint32_t s,
+__device__ __forceinline__ void spec_run(const Lv& v0, const Tabs& t, bool ed, uint32_t nb, uint32_t st, uint32_t s,
                                          uint32_t C1, uint32_t C2, uint32_t e, Spec& o) {
+    const Lv& v = v0;
     uint32_t pos = st, cnt = 0, kind = T_EXIT, reason = 0;
     o.cp1 = NOCP; o.cp2 = NOCP; o.cpc1 = 0; o.cpc2 = 0;
     Tok tk;
@@ -502,9 +504,10 @@ __device__ __forceinline__ void spec_run(const Lv& v, const Tabs& t, bool ed, ui
 // Decode from the true start t0; at C1 compare with phase 0 (registers) and, when nph > 1, phases
 // 1..nph-1 (per-wave slot); at C2 with phase 0 again; on a match take that run's end state,
 // otherwise decode the rest of the segment (authoritative).  Returns true when it synchronised.
-__device__ __forceinline__ bool verify_run(const Lv& v, const Tabs& t, bool ed, uint32_t nb, uint32_t t0, uint32_t s,
+__device__ __forceinline__ bool verify_run(const Lv& v0, const Tabs& t, bool ed, uint32_t nb, uint32_t t0, uint32_t s,
                                            uint32_t C1, uint32_t C2, uint32_t e, const Spec& p0, const PhArr* ph,
                                            int lane, uint32_t nph, SegR& r) {
+    const Lv& v = v0;
     uint32_t pos = t0, c = 0, stage = 0;
     Tok tk;
     r.start = t0;
@@ -641,8 +644,9 @@ static_assert(sizeof(PhMap) <= sizeof(PhArr), "phase map shares the fallback slo
 
 // count run from st to the first token boundary at or past e (or the block end); the first step is
 // a single token whose end and bytes are returned in fb / fbc (fb = NOCP: none)
-__device__ __forceinline__ void phase_run(const Lv& v, const Tabs& t, bool ed, uint32_t nb, uint32_t st, uint32_t e,
+__device__ __forceinline__ void phase_run(const Lv& v0, const Tabs& t, bool ed, uint32_t nb, uint32_t st, uint32_t e,
                                           uint32_t& end, uint32_t& cnt, uint32_t& kr, uint32_t& fb, uint32_t& fbc) {
+    const Lv& v = v0;
     uint32_t pos = st, c = 0;
     kr = T_EXIT << 5; fb = NOCP; fbc = 0;
     Tok tk;
@@ -842,33 +846,40 @@ __device__ __forceinline__ void wr_flush_exact(Wr& w, gu8* out) {
 __device__ __forceinline__ uint64_t ld8(const gu8* p) { return *(const gu64*)p; }
 __device__ __forceinline__ uint32_t ld4(const gu8* p) { return *(const gu32*)p; }
 // out[dst, dst + len) = out[dst - dist, ...), byte-serial semantics; every source byte is final and
-// this lane's own (or the window's)
-__device__ __forceinline__ void wr_copy(gu8* out, uint64_t dst, uint32_t len, uint32_t dist) {
+// this lane's own (or the window's).  `lastb` is the byte at dst - 1 (known to the lane: a dist-1
+// run needs no read back) and is updated to the copy's last byte.
+__device__ __forceinline__ void wr_copy(gu8* out, uint64_t dst, uint32_t len, uint32_t dist, uint32_t& lastb) {
     gu8* d = out + dst;
     const gu8* sp = d - dist;
-    if (dist >= 8) {
-        if (len >= 8) {
-            uint32_t k = 0;
-            for (; k + 8 <= len; k += 8) *(gu64*)(d + k) = ld8(sp + k);
-            if (k < len) *(gu64*)(d + len - 8) = ld8(sp + len - 8);
-            return;
-        }
-    } else if (dist == 1) {
-        const uint32_t v4 = (uint32_t)sp[0] * 0x01010101u;
+    if (dist == 1) {
+        const uint32_t v4 = lastb * 0x01010101u;
         if (len >= 4) {
             uint32_t k = 0;
             for (; k + 4 <= len; k += 4) *(gu32*)(d + k) = v4;
             if (k < len) *(gu32*)(d + len - 4) = v4;
-            return;
+        } else {
+            for (uint32_t k = 0; k < len; k++) d[k] = (uint8_t)lastb;
         }
-    }
-    if (dist >= 4 && len >= 4) {
-        uint32_t k = 0;
-        for (; k + 4 <= len; k += 4) *(gu32*)(d + k) = ld4(sp + k);
-        if (k < len) *(gu32*)(d + len - 4) = ld4(sp + len - 4);
         return;
     }
-    for (uint32_t k = 0; k < len; k++) d[k] = sp[k];
+    if (dist >= 8 && len >= 8) {
+        uint32_t k = 0;
+        uint64_t x = 0;
+        for (; k + 8 <= len; k += 8) { x = ld8(sp + k); *(gu64*)(d + k) = x; }
+        if (k < len) { x = ld8(sp + len - 8); *(gu64*)(d + len - 8) = x; }
+        lastb = (uint32_t)(x >> 56);
+        return;
+    }
+    if (dist >= 4 && len >= 4) {
+        uint32_t k = 0, x = 0;
+        for (; k + 4 <= len; k += 4) { x = ld4(sp + k); *(gu32*)(d + k) = x; }
+        if (k < len) { x = ld4(sp + len - 4); *(gu32*)(d + len - 4) = x; }
+        lastb = x >> 24;
+        return;
+    }
+    uint32_t b = lastb;
+    for (uint32_t k = 0; k < len; k++) { b = sp[k]; d[k] = (uint8_t)b; }
+    lastb = b;
 }
 
 }  // namespace wv
@@ -1030,7 +1041,7 @@ ndfl_inflate_count_wave_kernel(const uint32_t* w, uint64_t nwords, uint64_t nbit
 // and a pending bit, and ndfl_inflate_resolve_kernel rounds resolve them afterwards by pointer
 // jumping.  So every chain decodes in parallel whatever the LZ77 distances.
 #ifndef NDFL_EMIT_WAVES_PER_SIMD
-#define NDFL_EMIT_WAVES_PER_SIMD 2
+#define NDFL_EMIT_WAVES_PER_SIMD 3
 #endif
 extern "C" __global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(NDFL_EMIT_WAVES_PER_SIMD)))
 ndfl_inflate_emit_wave_kernel(const uint32_t* w, uint64_t nwords, uint64_t nbits, const EmitChain* chains,
@@ -1124,6 +1135,8 @@ ndfl_inflate_emit_wave_kernel(const uint32_t* w, uint64_t nwords, uint64_t nbits
             wr.acc = 0; wr.an = 0; wr.dst = dst0;
             uint64_t dfr = ~0ull;           // first deferred byte of this lane (absolute)
             uint64_t lastsrc = 0;           // a byte holding the value of the last output byte
+            uint32_t lastb = 0;             // the last output byte, when it is final (lastok)
+            bool lastok = false;
             bool active = live;
             while (active && pos < end) {
                 Tok tk;
@@ -1133,6 +1146,8 @@ ndfl_inflate_emit_wave_kernel(const uint32_t* w, uint64_t nwords, uint64_t nbits
                     wr_lit(wr, gout, tk.val, tk.n);
                     n += tk.n;
                     lastsrc = dst0 + n - 1;
+                    lastb = tk.val >> (tk.n == 2 ? 8 : 0);
+                    lastok = true;
                     continue;
                 }
                 if (tk.kind != K_LEN) break;            // EOB or error (as verified)
@@ -1155,8 +1170,10 @@ ndfl_inflate_emit_wave_kernel(const uint32_t* w, uint64_t nwords, uint64_t nbits
                     }
                 }
                 wr_flush_word(wr, gout);
+                if (!defer && dist == 1 && !lastok) lastb = gout[dst - 1];    // (not one of our bytes yet)
                 if (!defer) {
-                    wr_copy(gout, dst, len, dist);                  // sources final and our own
+                    wr_copy(gout, dst, len, dist, lastb);           // sources final and our own
+                    lastok = true;
                     lastsrc = dst + len - 1;
                 } else {
                     // deferred: back-references (a dist-1 run points at the byte its value comes
@@ -1173,6 +1190,7 @@ ndfl_inflate_emit_wave_kernel(const uint32_t* w, uint64_t nwords, uint64_t nbits
                     }
                     if (dist == 1) lastsrc = anchor; else lastsrc = dst + len - 1;
                     dfr = min(dfr, dst);
+                    lastok = false;                 // the copy's bytes are pending
                 }
                 n += len;
                 wr.dst = dst0 + n;
