@@ -940,6 +940,13 @@ int ndfl_inflate_range(ndfl_ctx* c, const uint8_t* in, uint64_t in_len, uint64_t
                        consumed_bits, flags, deferred, &c->last_ms, partial);
 }
 
+int ndfl_inflate_sync(ndfl_ctx* c, const uint8_t* in, uint64_t in_len, uint64_t from_bit, uint64_t window_bits,
+                      uint64_t* sync_bit, uint32_t flags) {
+    if (!c || !sync_bit || (!in && in_len) || from_bit > in_len * 8) return NDFL_E_ARG;
+    HIPCHK(hipSetDevice(c->device));
+    return inflate_sync(c->inf, c->stream, in, in_len, from_bit, window_bits, flags, sync_bit, &c->last_ms);
+}
+
 int ndfl_inflate_resolve(ndfl_ctx* c, uint64_t* n_reemitted) {
     if (!c || !n_reemitted) return NDFL_E_ARG;
     HIPCHK(hipSetDevice(c->device));

@@ -341,7 +341,7 @@ __device__ __noinline__ bool strict_stored(const In& in, uint64_t p) {
 #endif
 extern "C" __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(NDFL_FIND_WPE)))
 ndfl_inflate_find_kernel(const uint32_t* w, uint64_t nwords, uint64_t nbits, uint64_t* qlist, uint32_t* qcount,
-                         uint32_t qcap, uint32_t win_words, uint32_t period_words) {
+                         uint32_t qcap, uint32_t win_words, uint32_t period_words, uint64_t w_lo, uint64_t scan_end) {
     using namespace inf;
     __shared__ uint64_t cand[2048];
     __shared__ uint32_t ncand, gbase;
@@ -352,14 +352,16 @@ ndfl_inflate_find_kernel(const uint32_t* w, uint64_t nwords, uint64_t nbits, uin
     In in{w, nwords, nbits};
     for (uint32_t kk = 0; kk < FIND_WPT; kk++) {
     const uint64_t tt = ((uint64_t)blockIdx.x * FIND_WPT + kk) * blockDim.x + threadIdx.x;
-    const uint64_t t = (tt / win_words) * period_words + tt % win_words;     // input word index
+    // input word index; the scan covers bit positions [w_lo * 32, scan_end) of the stream
+    const uint64_t t = w_lo + (tt / win_words) * period_words + tt % win_words;
     const uint64_t p0 = t * 32;
-    if (p0 < nbits) {
+    if (p0 < scan_end) {
         const uint32_t w0 = in.ld(t), w1 = in.ld(t + 1), w2 = in.ld(t + 2), w3 = in.ld(t + 3);
         const uint64_t W = (uint64_t)w0 | ((uint64_t)w1 << 32);
         const uint32_t b1 = (uint32_t)(W >> 1), b2 = (uint32_t)(W >> 2);
         uint32_t valid = 0xFFFFFFFFu;
         if (p0 + 35 > nbits) valid = (nbits >= p0 + 3) ? (uint32_t)((1ull << (nbits - p0 - 2)) - 1) : 0u;
+        if (p0 + 32 > scan_end) valid &= (uint32_t)((1ull << (scan_end - p0)) - 1);
         uint32_t m2 = ~b1 & b2 & valid & kraft_complete_mask(w0, w1, w2, w3);
         // LEN == ~NLEN at byte positions p0 + 8j, j = 1..5; position i pads to j = (i + 10) / 8
         const uint64_t W12 = (uint64_t)w1 | ((uint64_t)w2 << 32);
@@ -797,7 +799,8 @@ static int resolve_rounds(InflateScratch& S, hipStream_t s, uint8_t* d_out, uint
 //             chains) are recorded and re-emitted by inflate_resolve once it is written
 static int inflate_run(InflateScratch& S, hipStream_t s, const uint8_t* in, uint64_t in_len, uint64_t start_bit,
                        uint64_t end_bit, uint8_t* out, uint64_t dict_len, uint64_t out_cap, uint64_t* out_len,
-                       uint64_t* consumed_bits, uint32_t flags, bool deferred, double* last_ms, bool partial = false) {
+                       uint64_t* consumed_bits, uint32_t flags, bool deferred, double* last_ms, bool partial = false,
+                       uint64_t* probe_sync = nullptr) {
     using namespace inf;
     *out_len = 0;
     *consumed_bits = 0;
@@ -833,7 +836,11 @@ static int inflate_run(InflateScratch& S, hipStream_t s, const uint8_t* in, uint
         // sparse windows: chains then span a few blocks (the count pass decodes on through
         // boundaries that are not candidates); every window holds a block start unless blocks
         // are longer than the gap, in which case chains just get longer
-        const uint64_t nw32 = (nbits + 31) / 32;
+        // only the range's own bits are scanned: candidates outside [start_bit, end_bit) are
+        // dropped below anyway (a range decode of one stream shard, or a sync probe)
+        const uint64_t scan_end = std::min(end_bit, nbits);
+        const uint64_t w_lo = start_bit >> 5;
+        const uint64_t nw32 = scan_end > w_lo * 32 ? (scan_end + 31) / 32 - w_lo : 0;
         static const uint32_t env_win = getenv("NDFL_FIND_WIN") ? (uint32_t)atoi(getenv("NDFL_FIND_WIN")) : 0;
         static const uint32_t env_per = getenv("NDFL_FIND_PERIOD") ? (uint32_t)atoi(getenv("NDFL_FIND_PERIOD")) : 0;
         const uint32_t period = env_per ? env_per : FIND_PERIOD_WORDS, win = env_win ? env_win : FIND_WIN_WORDS;
@@ -846,7 +853,8 @@ static int inflate_run(InflateScratch& S, hipStream_t s, const uint8_t* in, uint
         if (nthr) {
             const bool dense = nw32 <= (uint64_t)period;
             hipLaunchKernelGGL(ndfl_inflate_find_kernel, dim3((uint32_t)((nthr + 256 * FIND_WPT - 1) / (256 * FIND_WPT))), dim3(256), 0, s, d_w,
-                               nwords, nbits, d_qlist, d_qcount, qcap, dense ? 1u : win, dense ? 1u : period);
+                               nwords, nbits, d_qlist, d_qcount, qcap, dense ? 1u : win, dense ? 1u : period, w_lo,
+                               scan_end);
             INF_CHK(hipGetLastError());
             static const uint32_t strict_grid = [] {
                 int dev = 0, ncu = 0, per = 0;
@@ -969,6 +977,22 @@ static int inflate_run(InflateScratch& S, hipStream_t s, const uint8_t* in, uint
     S.count_first = true;
     int rc = run_count(starts, res);
     if (rc) return rc;
+    if (probe_sync) {
+        // sync probe: a chain of blocks from a header candidate that ends exactly at another
+        // candidate y has decoded up to y in step with the stream (a decode that starts off a block
+        // boundary re-synchronises inside the block and then ends at its real end-of-block), so y
+        // is a block boundary; y is taken when its own chain links on in turn (or is final)
+        *probe_sync = NONE;
+        auto linked = [&](size_t k) {
+            return res[k].status == ST_BOUNDARY && res[k].next < starts.size() && starts[res[k].next] == res[k].end_bit;
+        };
+        for (size_t k = 1; k < res.size(); k++) {
+            if (!linked(k)) continue;
+            const size_t j = res[k].next;
+            if (j >= 1 && (linked(j) || res[j].status == ST_FINAL)) { *probe_sync = starts[j]; break; }
+        }
+        return 0;
+    }
     {
         float a = 0, b = 0;
         hipEventElapsedTime(&a, S.ev[0], S.ev[1]);
@@ -1145,6 +1169,17 @@ static int inflate_run(InflateScratch& S, hipStream_t s, const uint8_t* in, uint
     *out_len = total;
     *consumed_bits = stop_bit;
     return 0;
+}
+
+// First confirmed block boundary at or past from_bit, looking at most window_bits ahead (NONE if
+// none): the finder and count passes of inflate_run on that window, without the emit.
+static int inflate_sync(InflateScratch& S, hipStream_t s, const uint8_t* in, uint64_t in_len, uint64_t from_bit,
+                        uint64_t window_bits, uint32_t flags, uint64_t* sync_bit, double* last_ms) {
+    uint64_t olen = 0, bits = 0;
+    const uint64_t end = std::min(in_len * 8, from_bit + window_bits);
+    if (from_bit >= end) { *sync_bit = inf::NONE; return 0; }
+    return inflate_run(S, s, in, in_len, from_bit, end, nullptr, 0, 0, &olen, &bits, flags, false, last_ms, false,
+                       sync_bit);
 }
 
 // Second half of a deferred-window range decode: the caller has written the window

@@ -313,6 +313,13 @@ class Context:
                                  out_addr, dict_len, out_cap, ctypes.byref(olen), ctypes.byref(bits), flags)
         return r, olen.value, bits.value
 
+    def inflate_sync_raw(self, in_addr, in_len, from_bit, window_bits, flags):
+        """ndfl_inflate_sync: first confirmed block boundary at or past from_bit (None: none)."""
+        v = ctypes.c_uint64(0)
+        check(load().ndfl_inflate_sync(self._h, in_addr, in_len, from_bit, window_bits, ctypes.byref(v), flags),
+              "ndfl_inflate_sync")
+        return None if v.value == NO_END else v.value
+
     def inflate_resolve(self):
         """Finish a DICT_DEFERRED range decode once the window is written; returns re-emitted chains."""
         n = ctypes.c_uint64(0)

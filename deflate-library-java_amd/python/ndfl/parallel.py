@@ -12,6 +12,9 @@ on raw input (D/DeflaterOutputStream.java:119-137).  So rank r 
                   bytes ORed (BitOut's packing, D/DeflaterOutputStream.java:147-156);
               (4) gather_stream: the root receives every part at its byte offset (point to point)
                   and ORs the shared bytes on device -- one global stream on one GPU.
+  decompress  (seam index, from deflate_shard) inflate_shard, below; (foreign stream, no index)
+              inflate_split: each rank probes for a confirmed block boundary near its share of the
+              bits (ndfl_inflate_sync), the seams are proven by the range decodes themselves.
   decompress  each rank decodes its seam-delimited bit range with a deferred window
               (ndfl_inflate_range + NDFL_DICT_DEFERRED), all ranks in parallel; then the last
               32 KiB of output pass from rank to rank (the reference's dictionary ring,
@@ -75,6 +78,10 @@ class DeviceCodec:
 
     def resolve(self):
         return self.ctx.inflate_resolve()
+
+    def sync(self, src, in_len, from_bit, window_bits):
+        from . import IN_DEVICE
+        return self.ctx.inflate_sync_raw(src.data_ptr(), in_len, from_bit, window_bits, IN_DEVICE)
 
 
 def _staged(dist, t):
@@ -187,6 +194,73 @@ def inflate_shard(codec, dist, torch, part, out, rank, world):
     codes = _gather_ints(dist, torch, code, world, codec.device)
     first = next((c for c in codes if c != 0), 0)
     return first, olen, dict_len
+
+
+SYNC_WINDOW = 8 << 20          # bits a sync probe looks ahead (1 MiB of stream)
+_lib_E_ARG = -1                # NDFL_E_ARG: the range end is no block boundary
+
+
+def inflate_split(codec, dist, torch, stream, in_len, out, rank, world):
+    """Decode ONE stream that carries no seam index (a foreign .gz member, a single-GPU encoding)
+    across the ranks (SURVEY §8e decompress).  Every rank holds the stream.
+
+      (1) rank r > 0 probes for the first confirmed block boundary at or past r * C / N
+          (ndfl_inflate_sync: a header the reference's checks accept whose chain of blocks decodes
+          exactly to the next one) -- all ranks at once; all_gather of the seams;
+      (2) rank r decodes [seam_r, seam_{r+1}) with ndfl_inflate_range and a deferred window.  The
+          range decode's exact-boundary check proves each seam inductively from bit 0: rank r-1,
+          started at a proven boundary, must stop exactly at seam_r;
+      (3) the window chain and the first-error reduction as in inflate_shard.
+    If a seam is not proven (a false candidate, a corrupt stream) or a rank's output is shorter than
+    the 32 KiB window, rank 0 decodes the whole stream alone (the single-GPU result, exact by
+    construction).  out[:32768] is the window slot, the rank's bytes follow.
+    Returns (code, out_len, dict_len, byte_offset) -- code 0 or the Reason+1 of the first error in
+    stream order (the same on every rank); byte_offset = where this rank's bytes start in the output."""
+    nbits = in_len * 8
+    seam = 0
+    if rank > 0:
+        s = codec.sync(stream, in_len, nbits * rank // world, SYNC_WINDOW)
+        seam = nbits if s is None else s
+    seams = _gather_ints(dist, torch, seam, world, codec.device)
+    for r in range(1, world):                   # monotonic: a rank without a seam gets nothing
+        seams[r] = max(seams[r], seams[r - 1])
+    end = seams[rank + 1] if rank + 1 < world and seams[rank + 1] < nbits else None
+    dict_len = WINDOW if rank > 0 else 0
+    empty = seams[rank] >= nbits or (end is not None and end <= seams[rank])
+    if empty:
+        code, olen = 0, 0
+    else:
+        code, olen, consumed = codec.inflate_range(stream, in_len, seams[rank], end, out, dict_len, rank > 0)
+        if code == 0 and end is not None and consumed != end:
+            code = _lib_E_ARG                    # the final block came before the next seam
+    codes = _gather_ints(dist, torch, code, world, codec.device)
+    olens = _gather_ints(dist, torch, olen, world, codec.device)
+    offs = [0]
+    for v in olens:
+        offs.append(offs[-1] + v)
+    # seams proven and windows available: every rank but the last ended exactly at its seam with no
+    # error, and the output before each rank > 0 holds a full window within its predecessor
+    ok = all(c == 0 for c in codes[:-1]) and codes[-1] >= 0 and \
+        all(olens[r - 1] >= WINDOW for r in range(1, world) if seams[r] < nbits)
+    if not ok:
+        # single-GPU fallback: rank 0 decodes everything
+        if rank == 0:
+            code, olen, _ = codec.inflate_range(stream, in_len, 0, None, out, 0, False)
+        else:
+            code, olen = 0, 0
+        code = _gather_ints(dist, torch, code, world, codec.device)[0]
+        if code < 0:
+            raise RuntimeError(f"inflate_range failed: {code}")
+        return code, olen, 0, 0
+    # window chain: rank r-1's last 32 KiB of output -> rank r (ranks with output only)
+    if rank > 0 and not empty:
+        _recv(dist, out[:dict_len], rank - 1)
+        codec.resolve()
+    if rank + 1 < world and seams[rank + 1] < nbits:
+        e = dict_len + olen
+        _send(dist, out[e - WINDOW:e].contiguous(), rank + 1)
+    first = next((c for c in codes if c != 0), 0)
+    return first, olen, dict_len, offs[rank]
 
 
 def gather_stream(codec, dist, torch, part, rank, world, root=0):

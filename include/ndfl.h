@@ -223,6 +223,19 @@ int ndfl_inflate(ndfl_ctx* ctx, const uint8_t* in, uint64_t in_len, uint8_t* out
 int ndfl_inflate_range(ndfl_ctx* ctx, const uint8_t* in, uint64_t in_len, uint64_t start_bit, uint64_t end_bit,
                        uint8_t* out, uint64_t dict_len, uint64_t out_cap, uint64_t* out_len,
                        uint64_t* consumed_bits, uint32_t flags);
+/*
+ * Multi-GPU decode of a stream WITHOUT a seam index (SURVEY §8e decompress): a block boundary
+ * at or past from_bit that the decoder has confirmed -- the end of a chain of blocks, decoded from
+ * a header candidate (the reference's own header checks, D/decomp/Open.java:322-435), that lands
+ * exactly on another candidate whose own chain links on (or is final) -- looking at most
+ * window_bits ahead;
+ * *sync_bit = UINT64_MAX if there is none.  GPU r of N takes [sync(r*C/N), sync((r+1)*C/N)) and
+ * decodes it with ndfl_inflate_range (deferred window); ndfl_inflate_range's exact-boundary
+ * check (NDFL_E_ARG when a block straddles end_bit) proves each seam, starting from bit 0.
+ * flags: NDFL_IN_DEVICE / NDFL_IN_PADDED as for ndfl_inflate.
+ */
+int ndfl_inflate_sync(ndfl_ctx* ctx, const uint8_t* in, uint64_t in_len, uint64_t from_bit, uint64_t window_bits,
+                      uint64_t* sync_bit, uint32_t flags);
 /* Finish the last NDFL_DICT_DEFERRED range decode on this context (NDFL_E_STATE if none). */
 int ndfl_inflate_resolve(ndfl_ctx* ctx, uint64_t* n_reemitted);
 

@@ -50,6 +50,8 @@ class OracleCodec:
         if dec:
             out[dict_len:dict_len + len(dec)] = torch.frombuffer(bytearray(dec), dtype=torch.uint8)
         code = 0 if r is None else O.REASONS.index(r) + 1
+        if code == 0 and end is not None and bits > end:
+            code = -1                    # as ndfl_inflate_range: NDFL_E_ARG when a block straddles end_bit
         return code, len(dec), bits
 
     def inflate_range(self, src, in_len, start, end, out, dict_len, deferred):
@@ -65,11 +67,69 @@ class OracleCodec:
         self.resolved += 1
         return 1
 
+    # the checker knows the true block boundaries of the streams it is given (set by the worker);
+    # `lie` moves one rank's answer off a boundary to exercise the fallback
+    boundaries = []
+    lie = None
+
+    def sync(self, src, in_len, from_bit, window_bits):
+        b = next((x for x in self.boundaries if x >= from_bit), None)
+        if b is not None and b - from_bit > window_bits:
+            b = None
+        if b is not None and self.lie == from_bit:
+            b += 1
+        return b
+
+
+def split_main(rank, world, cfg):
+    """inflate_split: one stream without a seam index decoded across the ranks."""
+    data = mixed_bytes(cfg["n"], cfg["seed"])
+    if cfg["stream"] == "zlib6":
+        import zlib
+        co = zlib.compressobj(6, zlib.DEFLATED, -15)
+        comp = co.compress(data) + co.flush()
+    else:
+        comp = O.deflate(data, cfg["stream"], cfg.get("chunk_len", 65536))
+    if cfg.get("codec") == "device":
+        import ndfl
+        codec = P.DeviceCodec(ndfl.Context(0), torch)
+    else:
+        codec = OracleCodec()
+        bb = O.block_bits(data, cfg["stream"], cfg.get("chunk_len", 65536))
+        acc, bounds = 0, []
+        for v in bb:
+            bounds.append(acc)
+            acc += v
+        OracleCodec.boundaries = bounds
+        if cfg.get("lie"):
+            OracleCodec.lie = len(comp) * 8 * 1 // world
+    src = torch.frombuffer(bytearray(comp + bytes(P_PAD)), dtype=torch.uint8).to(codec.device)
+    out = torch.zeros(P.WINDOW + len(data) + 1024, dtype=torch.uint8, device=codec.device)
+    code, olen, dict_len, off = P.inflate_split(codec, dist, torch, src, len(comp), out, rank, world)
+    mine = bytes(out[dict_len:dict_len + olen].cpu().numpy())
+    allp = [None] * world
+    dist.all_gather_object(allp, (off, mine, code))
+    res = {"code": code}
+    if rank == 0:
+        joined = b"".join(m for _, m, _ in sorted(allp))
+        res["equal"] = joined == data
+        res["split"] = sum(1 for _, m, _ in allp if m) > 1
+    resl = [None] * world
+    dist.all_gather_object(resl, res)
+    if rank == 0:
+        print("RESULT " + json.dumps(resl), flush=True)
+    dist.destroy_process_group()
+
+
+P_PAD = 256          # NDFL_IN_PAD_BYTES after the stream (device buffers are read in place when padded)
+
 
 def main():
     dist.init_process_group("gloo")
     rank, world = dist.get_rank(), dist.get_world_size()
     cfg = json.loads(os.environ["NDFL_PAR_CFG"])
+    if cfg.get("mode") == "split":
+        return split_main(rank, world, cfg)
     chunk = cfg["chunk_len"]
     sizes = [cfg["chunks_per_rank"] * chunk] * (world - 1) + [cfg["last_bytes"]]
     data = mixed_bytes(sum(sizes), cfg["seed"])

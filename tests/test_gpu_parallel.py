@@ -150,3 +150,34 @@ def test_sharded_protocol_two_ranks_one_gpu():
     assert res[0]["stream_equal"]
     assert all(r["gathered_equal"] for r in res)      # the device gather onto rank 0
     assert all(r["code"] == 0 and r["decoded_equal"] for r in res)
+
+
+@pytest.mark.parametrize("stream", ["RLE_DYNAMIC", "zlib6", "FULL_DYNAMIC"])
+def test_split_decode_of_foreign_stream_two_ranks_one_gpu(stream):
+    """inflate_split on the GPU: a stream without a seam index (ours, Python zlib's, LZ77) decoded by
+    2 ranks sharing cuda:0 over gloo from seams found by ndfl_inflate_sync; the joined output equals
+    the data and both ranks took part."""
+    from test_parallel_cpu import run_workers
+    res = run_workers(2, dict(mode="split", n=2_000_000, seed=11, stream=stream, codec="device"))
+    assert res[0]["equal"]
+    assert all(r["code"] == 0 for r in res)
+    assert res[0]["split"]
+
+
+def test_inflate_sync_finds_true_boundaries(env):
+    """ndfl_inflate_sync returns a real block boundary (one of the oracle's chunk seams) at or past
+    the probe point, a few blocks on at most, for probes all over the stream."""
+    torch, ndfl, ctx = env
+    data = mixed_bytes(3_000_000, 21)
+    comp = O.deflate(data)
+    seams, acc = [], 0
+    for v in O.block_bits(data):
+        seams.append(acc)
+        acc += v
+    dev = torch.frombuffer(bytearray(comp + bytes(256)), dtype=torch.uint8).cuda()
+    torch.cuda.synchronize()
+    for frac in (0.1, 0.33, 0.5, 0.77, 0.95):
+        p = int(len(comp) * 8 * frac)
+        s = ctx.inflate_sync_raw(dev.data_ptr(), len(comp), p, 8 << 20, ndfl.IN_DEVICE)
+        assert s is not None and s >= p and s in seams, (frac, p, s)
+        assert s < p + 3 * 65536 * 8            # within a few blocks

@@ -44,3 +44,14 @@ def test_sharded_stream_roundtrip(world, cfg):
         assert r["code"] == 0
         assert r["decoded_equal"]
     assert all(r["resolved"] == 1 for r in res[1:])
+
+
+@pytest.mark.parametrize("world,lie", [(2, False), (3, False), (2, True)])
+def test_split_decode_without_seam_index(world, lie):
+    """inflate_split: one oracle stream decoded across ranks from probed seams (the checker's probe
+    knows the true block boundaries; `lie` moves one seam off a boundary, which the range decodes
+    must catch and answer with the single-rank fallback)."""
+    res = run_workers(world, dict(mode="split", n=600_000, seed=5, stream="RLE_DYNAMIC", lie=lie))
+    assert res[0]["equal"]
+    assert all(r["code"] == 0 for r in res)
+    assert res[0]["split"] == (not lie)
