@@ -457,7 +457,10 @@ __device__ int build_tables(Shared& S, int lane, bool& empty_dist) {
 // speculation and then takes the speculative end state.  Codes whose lengths are (nearly) all
 // multiples of 8 resynchronise slowly or never from a wrong bit phase; when several lanes fail the
 // fallback adds runs from s_j+1 .. s_j+7 (one per phase) compared at C1.
-constexpr uint32_t XCP1 = 128, XCP2 = 1024;
+#ifndef NDFL_XCP1
+#define NDFL_XCP1 128
+#endif
+constexpr uint32_t XCP1 = NDFL_XCP1, XCP2 = 1024;
 constexpr uint32_t NPH = 8;
 constexpr uint32_t NOCP = 0xFFFFFFFFu;
 constexpr uint64_t MAX_SPAN = RSPAN;         // round span cap
