@@ -189,42 +189,49 @@ __device__ __forceinline__ Lv make_lv(const Stage& st, const Geo& g, int lane) {
 template <bool CAREFUL>
 __device__ __forceinline__ void tok(const Lv& v, uint32_t& pos, const Tabs& t, bool empty_dist, uint32_t stop,
                                     uint32_t nb, Tok& tk) {
+    // (the result goes through scalars and is stored into tk once: stores of different fields on
+    // different paths made the compiler keep tk in scratch memory)
+    uint32_t kind, val, n = 1, dist = 0;
     uint32_t lo, hi;
     v.win(pos, lo, hi);
     uint32_t e = t.lit[lo & ((1u << LB) - 1u)];
-    if (e >> 31) {
-        const uint32_t l1 = e & 15, l12 = (e >> 4) & 15;
-        bool two = (e >> 8) & 1;
-        if (CAREFUL) two = two && pos + l1 < stop && pos + l12 <= nb;
-        pos += two ? l12 : l1;
-        if (CAREFUL && pos > nb) { tk.kind = K_BAD; tk.val = R_UEOS; return; }
-        tk.kind = K_LIT; tk.n = two ? 2u : 1u; tk.val = (e >> 9) & (two ? 0xFFFFu : 0xFFu);
-        return;
-    }
-    if (!(e & 31)) e = slow_lit(lo & 0x7FFFu, t);
-    const uint32_t cl = e & 31, k = (e >> 9) & 3;
-    if (k != K_LEN) {
-        pos += cl;
-        if (CAREFUL && pos > nb) { tk.kind = K_BAD; tk.val = R_UEOS; return; }
-        tk.kind = k; tk.n = 1; tk.val = k == K_LIT ? e >> 16 : (uint32_t)R_RESERVED_LEN;
-        return;
-    }
-    const uint32_t xb = (e >> 5) & 15;
-    if (CAREFUL && pos + cl > nb) { pos += cl; tk.kind = K_BAD; tk.val = R_UEOS; return; }
-    const uint32_t run = (e >> 16) + ((lo >> cl) & ((1u << xb) - 1u));
-    const uint32_t sh = cl + xb;
-    if (CAREFUL && pos + sh > nb) { pos += sh; tk.kind = K_BAD; tk.val = R_UEOS; return; }
-    if (empty_dist) { pos += sh; tk.kind = K_BAD; tk.val = R_EMPTY_DIST; return; }
-    const uint32_t dw = __builtin_amdgcn_alignbit(hi, lo, sh);      // 32 bits from the distance code
-    uint32_t d = t.dst[dw & ((1u << DB) - 1u)];
-    if (!(d & 31)) d = slow_dist(dw & 0x7FFFu, t);
-    const uint32_t dl = d & 31, dxb = (d >> 5) & 15;
-    if (CAREFUL && pos + sh + dl > nb) { pos += sh + dl; tk.kind = K_BAD; tk.val = R_UEOS; return; }
-    if (((d >> 9) & 3) == K_BAD) { pos += sh + dl; tk.kind = K_BAD; tk.val = R_RESERVED_DIST; return; }
-    const uint32_t dist = (d >> 16) + ((dw >> dl) & ((1u << dxb) - 1u));
-    pos += sh + dl + dxb;
-    if (CAREFUL && pos > nb) { tk.kind = K_BAD; tk.val = R_UEOS; return; }
-    tk.kind = K_LEN; tk.n = run; tk.dist = dist;
+    do {
+        if (e >> 31) {
+            const uint32_t l1 = e & 15, l12 = (e >> 4) & 15;
+            bool two = (e >> 8) & 1;
+            if (CAREFUL) two = two && pos + l1 < stop && pos + l12 <= nb;
+            pos += two ? l12 : l1;
+            kind = K_LIT; n = two ? 2u : 1u; val = (e >> 9) & (two ? 0xFFFFu : 0xFFu);
+            if (CAREFUL && pos > nb) { kind = K_BAD; val = R_UEOS; n = 1; }
+            break;
+        }
+        if (!(e & 31)) e = slow_lit(lo & 0x7FFFu, t);
+        const uint32_t cl = e & 31, k = (e >> 9) & 3;
+        if (k != K_LEN) {
+            pos += cl;
+            kind = k; val = k == K_LIT ? e >> 16 : (uint32_t)R_RESERVED_LEN;
+            if (CAREFUL && pos > nb) { kind = K_BAD; val = R_UEOS; }
+            break;
+        }
+        kind = K_BAD; val = R_UEOS;
+        const uint32_t xb = (e >> 5) & 15;
+        if (CAREFUL && pos + cl > nb) { pos += cl; break; }
+        const uint32_t run = (e >> 16) + ((lo >> cl) & ((1u << xb) - 1u));
+        const uint32_t sh = cl + xb;
+        if (CAREFUL && pos + sh > nb) { pos += sh; break; }
+        if (empty_dist) { pos += sh; val = R_EMPTY_DIST; break; }
+        const uint32_t dw = __builtin_amdgcn_alignbit(hi, lo, sh);      // 32 bits from the distance code
+        uint32_t d = t.dst[dw & ((1u << DB) - 1u)];
+        if (!(d & 31)) d = slow_dist(dw & 0x7FFFu, t);
+        const uint32_t dl = d & 31, dxb = (d >> 5) & 15;
+        if (CAREFUL && pos + sh + dl > nb) { pos += sh + dl; break; }
+        if (((d >> 9) & 3) == K_BAD) { pos += sh + dl; val = R_RESERVED_DIST; break; }
+        dist = (d >> 16) + ((dw >> dl) & ((1u << dxb) - 1u));
+        pos += sh + dl + dxb;
+        if (CAREFUL && pos > nb) break;
+        kind = K_LEN; n = run; val = 0;
+    } while (false);
+    tk.kind = kind; tk.val = val; tk.n = n; tk.dist = dist;
 }
 
 // Count tokens from pos to the first token boundary at or past `stop` (<= input end) or to a
@@ -1070,6 +1077,11 @@ ndfl_inflate_emit_wave_kernel(const uint32_t* w, uint64_t nwords, uint64_t nbits
     uint64_t endpos = ch.start_bit;
     uint32_t nslow = 0, nfix = 0;
     uint32_t rec = ch.slot < pool.nslot ? pool.head[ch.slot] : NOREC;
+    // the next round's record is loaded one round ahead (its loads overlap this round's decode)
+    SegMeta pm = {};
+    uint64_t pst = 0;
+    uint32_t pcn = 0;
+    if (rec != NOREC) { pm = pool.meta[rec]; pst = pool.start[(uint64_t)rec * 64 + lane]; pcn = pool.cnt[(uint64_t)rec * 64 + lane]; }
     uint64_t bnd_bit = cur, bnd_out = base;     // start of the current block (partial-input decodes)
     for (int blk = 0;; blk++) {
         if (blk > 0 && cur == ch.end_bit) { status = ST_BOUNDARY; endpos = cur; break; }
@@ -1106,11 +1118,12 @@ ndfl_inflate_emit_wave_kernel(const uint32_t* w, uint64_t nwords, uint64_t nbits
             Geo g;
             if (rec != NOREC) {
                 // exact segments from the count pass, and the round's geometry
-                const SegMeta m = pool.meta[rec];
+                const SegMeta m = pm;
                 ft = m.ft;
-                r.start = pool.start[(uint64_t)rec * 64 + lane];
-                r.cnt = pool.cnt[(uint64_t)rec * 64 + lane];
+                r.start = pst;
+                r.cnt = pcn;
                 rec = m.next;
+                if (rec != NOREC) { pm = pool.meta[rec]; pst = pool.start[(uint64_t)rec * 64 + lane]; pcn = pool.cnt[(uint64_t)rec * 64 + lane]; }
                 const uint64_t nx = __shfl_down((unsigned long long)r.start, 1, 64);
                 r.end = lane < 63 ? nx : m.exit63;
                 r.kind = T_EXIT; r.reason = 0;

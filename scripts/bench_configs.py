@@ -1,11 +1,11 @@
 """Measure the other BASELINE.json configurations on one MI355X (bench.py reports config 4).
 
     c1  gzip of 1 MiB of zeros through the stream API (host buffers; plumbing)
-    c2  decompress a 64 MiB .gz of alternating stored + fixed-Huffman (LZ77, dist 1..32768) blocks
-        (generated by the oracle's mixed-strategy driver; device-resident input -> output)
+    c2  decompress a 64 MiB .gz of stored + fixed-Huffman (LZ77, dist 1..32768) blocks
+        (tests/corpus.py c2_gzip; device-resident input -> output)
     c3  FULL_DYNAMIC (LZ77 + dynamic Huffman) compress of 1 GiB enwik-style text, device-resident;
         ratio checked against the oracle on a prefix (bit-exact, so the ratio is the reference's)
-    c5  one GPU's share of the 16 GiB random+repeat round trip (2 GiB, RLE_DYNAMIC), device-resident
+    c5  one GPU's share of the 16 GiB random+repeat round trip (2 GiB, RLE_DYNAMIC; corpus.c5_random_repeat), device-resident
 
 Each config prints one JSON line; the oracle (1 thread) is timed on a bounded sample beside it.
 Run on the GPU box: python scripts/bench_configs.py [c1 c2 c3 c5].
@@ -63,17 +63,10 @@ def c1(ctx):
 
 
 def c2(ctx):
-    rng = np.random.default_rng(0xC2)
-    n = 88 * MIB
-    text = corpus.c3_text(n, seed=0xC2).numpy()
-    rnd = rng.integers(0, 256, n, dtype=np.uint8)
-    # even 64 KiB chunks: random bytes (stored blocks), odd: text (fixed Huffman, LZ77)
-    data = np.where((np.arange(n) // 65536) % 2 == 0, rnd, text).astype(np.uint8).tobytes()
+    # the -m gpu test's corpus (tests/corpus.py c2_gzip: stored + zlib Z_FIXED blocks, seed 0xC2)
     t = time.perf_counter()
-    raw = O.deflate_mixed(data, ["UNCOMPRESSED", "FULL_STATIC"], chunk_len=65536)
+    gz, raw, data = corpus.c2_gzip(64 * MIB)
     gen_s = time.perf_counter() - t
-    meta = ndfl.GzipMetadata("DEFLATE", False, None, 0, "UNIX", None, None, None, False)
-    gz = bytes(meta.header_bytes()) + raw + O.crc32(data).to_bytes(4, "little") + (len(data) & 0xFFFFFFFF).to_bytes(4, "little")
     comp_dev = torch.frombuffer(bytearray(raw), dtype=torch.uint8).cuda()
     out = torch.empty(len(data) + 64, dtype=torch.uint8, device="cuda")
     res = {}
@@ -125,29 +118,9 @@ def c3(ctx):
 
 
 def c5(ctx):
-    rng = np.random.default_rng(0xC5)
+    # the -m gpu test's corpus (tests/corpus.py c5_random_repeat, seed 0xC5): 256 MiB tiled to 2 GiB
     base = 256 * MIB
-    a = np.empty(base, dtype=np.uint8)
-    p = 0
-    while p < base:
-        if rng.random() < 0.5:                      # random span
-            ln = int(rng.integers(64, 4096))
-            a[p:p + ln] = rng.integers(0, 256, min(ln, base - p), dtype=np.uint8)
-        elif rng.random() < 0.2 or p < 32768:        # byte run up to 4 KiB
-            ln = int(rng.integers(3, 4096))
-            a[p:p + ln] = rng.integers(0, 256)
-        else:                                        # repeat: copy from dist U[1, 32768], len geometric 3..258
-            ln = 0
-            for _ in range(int(rng.integers(1, 16))):
-                d = int(rng.integers(1, 32769))
-                ll = min(258, 3 + int(rng.geometric(1 / 20)))
-                q = p + ln
-                if q + ll > base:
-                    break
-                src = a[q - d:q - d + ll] if d >= ll else np.resize(a[q - d:q], ll)
-                a[q:q + ll] = src
-                ln += ll
-        p += max(ln, 1)
+    a = corpus.c5_random_repeat(base)
     n = 2 << 30
     data = torch.from_numpy(np.tile(a, n // base)).cuda()
     cap = ndfl._lib.load().ndfl_deflate_bound(n, 65536) + 64
