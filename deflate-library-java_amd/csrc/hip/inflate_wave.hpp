@@ -32,16 +32,19 @@ constexpr uint32_t DB = 8;                  // distance primary bits
 enum : uint32_t { K_LIT = 0, K_LEN = 1, K_EOB = 2, K_BAD = 3 };
 enum : uint32_t { T_EXIT = 0, T_EOB = 1, T_ERR = 2 };
 
+// Codes longer than the primary: a second-level table per primary prefix when they fit in the
+// extension area (the primary entry then points at it: length 0, [8:5] index bits, [31:16] offset),
+// otherwise the canonical slow path, whose arrays take the extension area instead (primary entry 0).
+constexpr uint32_t LX = 320;                // literal/length extension words
+constexpr uint32_t DX = 64;                 // distance extension words
 struct Tabs {
     uint32_t lit[1u << LB];
     uint32_t dst[1u << DB];
-    // canonical slow path for codes longer than the primary: left-justified 15-bit upper limit of
-    // each length, first code and rank offset per length, and the table entry of every symbol in
-    // canonical order
-    uint32_t llim[16], dlim[16];
-    uint16_t lfirst[16], loff[16], dfirst[16], doff[16];
-    uint32_t lent[288];
-    uint32_t dent[32];
+    // sub-tables, or (fallback) the entry of every symbol in canonical order [0, n), the
+    // left-justified 15-bit upper limit of each length [n, n + 16), first code and rank offset per
+    // length (u16) [n + 16, n + 32)
+    uint32_t lx[LX];
+    uint32_t dx[DX];
 };
 
 struct Shared {
@@ -96,10 +99,21 @@ __device__ __forceinline__ uint32_t slow_entry(uint32_t p15, const uint32_t* lim
     return ent[off[l] + idx];
 }
 __device__ __forceinline__ uint32_t slow_lit(uint32_t p15, const Tabs& t) {
-    return slow_entry<LB>(p15, t.llim, t.lfirst, t.loff, t.lent);
+    return slow_entry<LB>(p15, t.lx + 288, (const uint16_t*)(t.lx + 304), (const uint16_t*)(t.lx + 312), t.lx);
 }
 __device__ __forceinline__ uint32_t slow_dist(uint32_t p15, const Tabs& t) {
-    return slow_entry<DB>(p15, t.dlim, t.dfirst, t.doff, t.dent);
+    return slow_entry<DB>(p15, t.dx + 32, (const uint16_t*)(t.dx + 48), (const uint16_t*)(t.dx + 56), t.dx);
+}
+// entry of a code longer than the primary (e: its primary entry; bits: the window from the code's start)
+__device__ __forceinline__ uint32_t long_lit(uint32_t e, uint32_t bits, const Tabs& t) {
+    const uint32_t sd = (e >> 5) & 15;
+    if (sd) return t.lx[(e >> 16) + ((bits >> LB) & ((1u << sd) - 1u))];
+    return slow_lit(bits & 0x7FFFu, t);
+}
+__device__ __forceinline__ uint32_t long_dist(uint32_t d, uint32_t bits, const Tabs& t) {
+    const uint32_t sd = (d >> 5) & 15;
+    if (sd) return t.dx[(d >> 16) + ((bits >> DB) & ((1u << sd) - 1u))];
+    return slow_dist(bits & 0x7FFFu, t);
 }
 
 struct Tok {
@@ -205,7 +219,7 @@ __device__ __forceinline__ void tok(const Lv& v, uint32_t& pos, const Tabs& t, b
             if (CAREFUL && pos > nb) { kind = K_BAD; val = R_UEOS; n = 1; }
             break;
         }
-        if (!(e & 31)) e = slow_lit(lo & 0x7FFFu, t);
+        if (!(e & 31)) e = long_lit(e, lo, t);
         const uint32_t cl = e & 31, k = (e >> 9) & 3;
         if (k != K_LEN) {
             pos += cl;
@@ -222,7 +236,7 @@ __device__ __forceinline__ void tok(const Lv& v, uint32_t& pos, const Tabs& t, b
         if (empty_dist) { pos += sh; val = R_EMPTY_DIST; break; }
         const uint32_t dw = __builtin_amdgcn_alignbit(hi, lo, sh);      // 32 bits from the distance code
         uint32_t d = t.dst[dw & ((1u << DB) - 1u)];
-        if (!(d & 31)) d = slow_dist(dw & 0x7FFFu, t);
+        if (!(d & 31)) d = long_dist(d, dw, t);
         const uint32_t dl = d & 31, dxb = (d >> 5) & 15;
         if (CAREFUL && pos + sh + dl > nb) { pos += sh + dl; break; }
         if (((d >> 9) & 3) == K_BAD) { pos += sh + dl; val = R_RESERVED_DIST; break; }
@@ -328,10 +342,12 @@ __device__ void parse_hdr(const In& in, uint64_t p, Shared& S) {
 #undef HFAIL
 }
 
-// Canonical code from S.lens[base .. base+n) into a primary table + slow-path arrays (wave).
-// Returns the tree check result of codeLengthsToCodeTree (D/decomp/Open.java:705-756) (uniform).
-__device__ int build_code(Shared& S, uint32_t base, uint32_t n, uint32_t* prim, uint32_t pbits, uint16_t* first,
-                          uint32_t* lim, uint16_t* offv, uint32_t* sorted, bool is_lit, int lane) {
+// Canonical code from S.lens[base .. base+n) into the primary table `prim` (pbits) and the
+// extension area `x` (cap words): second-level tables for the codes longer than the primary when
+// they fit, else the canonical slow-path arrays (wave).  Returns the tree check result of
+// codeLengthsToCodeTree (D/decomp/Open.java:705-756) (uniform).
+__device__ int build_code(Shared& S, uint32_t base, uint32_t n, uint32_t* prim, uint32_t pbits, uint32_t* x,
+                          uint32_t cap, bool is_lit, int lane) {
     for (uint32_t k = (uint32_t)lane; k < (1u << pbits); k += 64) prim[k] = 0;
     uint32_t c[16];
 #pragma unroll
@@ -365,14 +381,53 @@ __device__ int build_code(Shared& S, uint32_t base, uint32_t n, uint32_t* prim, 
             fst[l] = code; off[l] = o; o += c[l];
         }
     }
-    if (lane < 16) {
+    __syncthreads();                            // prim zeroed
+    // the longest code under each primary prefix of the long codes (a canonical code's prefix set
+    // is prefix-free with the short codes, so these entries are free)
+#pragma unroll
+    for (int q = 0; q < 5; q++) {
+        const uint32_t l = mylen[q];
+        if (l <= pbits) continue;
+        uint32_t f = 0;
+#pragma unroll
+        for (int L = 1; L < 16; L++) if (l == (uint32_t)L) f = fst[L];
+        atomicMax(&prim[rev_bits((f + rank[q]) >> (l - pbits), pbits)], l);
+    }
+    __syncthreads();
+    // second-level table offsets: exclusive scan of 2^(longest - pbits) over the primary entries
+    const uint32_t per = (1u << pbits) / 64;
+    uint32_t loc = 0;
+    for (uint32_t i = 0; i < per; i++) {
+        const uint32_t m = prim[(uint32_t)lane * per + i];
+        loc += m ? 1u << (m - pbits) : 0u;
+    }
+    uint32_t incl = loc;
+#pragma unroll
+    for (int o = 1; o < 64; o <<= 1) {
+        const uint32_t y = __shfl_up(incl, o, 64);
+        if (lane >= o) incl += y;
+    }
+    const bool two = __shfl(incl, 63, 64) <= cap;
+    {
+        uint32_t o = incl - loc;
+        for (uint32_t i = 0; i < per; i++) {
+            const uint32_t k = (uint32_t)lane * per + i;
+            const uint32_t m = prim[k];
+            if (m) {
+                prim[k] = two ? ((o << 16) | ((m - pbits) << 5)) : 0u;
+                o += 1u << (m - pbits);
+            }
+        }
+    }
+    if (!two && lane < 16) {
+        uint16_t* first = (uint16_t*)(x + n + 16);
+        uint16_t* offv = first + 16;
         first[lane] = (uint16_t)fst[lane];
         offv[lane] = (uint16_t)off[lane];
-        uint32_t cl = 0, ll = 0;
+        uint32_t ll = 0;
 #pragma unroll
-        for (int L = 1; L < 16; L++) if (lane == L) { cl = c[L]; ll = fst[L] + c[L]; }
-        lim[lane] = lane ? (ll << (15 - lane)) : 0u;
-        (void)cl;
+        for (int L = 1; L < 16; L++) if (lane == L) ll = fst[L] + c[L];
+        x[n + lane] = lane ? (ll << (15 - lane)) : 0u;
     }
     __syncthreads();
 #pragma unroll
@@ -384,10 +439,15 @@ __device__ int build_code(Shared& S, uint32_t base, uint32_t n, uint32_t* prim, 
 #pragma unroll
         for (int L = 1; L < 16; L++) if (l == (uint32_t)L) { f = fst[L]; o = off[L]; }
         const uint32_t ent = is_lit ? lit_entry(s, l) : dist_entry(s, l);
-        sorted[o + rank[q]] = ent;
+        const uint32_t code = f + rank[q];
         if (l <= pbits) {
-            for (uint32_t k = rev_bits(f + rank[q], l); k < (1u << pbits); k += (1u << l)) prim[k] = ent;
+            for (uint32_t k = rev_bits(code, l); k < (1u << pbits); k += (1u << l)) prim[k] = ent;
+        } else if (two) {
+            const uint32_t pe = prim[rev_bits(code >> (l - pbits), pbits)];
+            const uint32_t sb = pe >> 16, sd = (pe >> 5) & 15, r = l - pbits;
+            for (uint32_t k = rev_bits(code & ((1u << r) - 1u), r); k < (1u << sd); k += (1u << r)) x[sb + k] = ent;
         }
+        if (!two) x[o + rank[q]] = ent;
     }
     __syncthreads();
     return 0;
@@ -436,12 +496,12 @@ __device__ int build_tables(Shared& S, int lane, bool& empty_dist) {
     if (S.h_btype == 1) {
         fixed_lens(S, lane);
         __syncthreads();
-        build_code(S, 0, 288, S.t.lit, LB, S.t.lfirst, S.t.llim, S.t.loff, S.t.lent, true, lane);
-        build_code(S, 288, 32, S.t.dst, DB, S.t.dfirst, S.t.dlim, S.t.doff, S.t.dent, false, lane);
+        build_code(S, 0, 288, S.t.lit, LB, S.t.lx, LX, true, lane);
+        build_code(S, 288, 32, S.t.dst, DB, S.t.dx, DX, false, lane);
         return 0;
     }
     const uint32_t numDist = S.h_numdist;
-    int e = build_code(S, 0, 288, S.t.lit, LB, S.t.lfirst, S.t.llim, S.t.loff, S.t.lent, true, lane);
+    int e = build_code(S, 0, 288, S.t.lit, LB, S.t.lx, LX, true, lane);
     if (e) return e;
     group_lits(S.t, lane);
     // distance code: empty (one zero length) or one used code padded at index 31 (:398-425)
@@ -452,7 +512,7 @@ __device__ int build_tables(Shared& S, int lane, bool& empty_dist) {
     __syncthreads();
     if (ones == 1 && other == 0 && lane == 0) S.lens[288 + 31] = 1;
     __syncthreads();
-    return build_code(S, 288, 32, S.t.dst, DB, S.t.dfirst, S.t.dlim, S.t.doff, S.t.dent, false, lane);
+    return build_code(S, 288, 32, S.t.dst, DB, S.t.dx, DX, false, lane);
 }
 
 // ---- segmented speculative decode of one round ------------------------------------------------
