@@ -1084,6 +1084,9 @@ static int inflate_run(InflateScratch& S, hipStream_t s, const uint8_t* in, uint
         fprintf(stderr, "[ndfl] count wave-time (ms x waves, 100 MHz clock): header %.1f spec %.1f verify %.1f phases %.1f "
                 "serial %.1f record %.1f build %.1f phase-mapped %.1f\n", t64[0] * 1e-5, t64[1] * 1e-5, t64[2] * 1e-5, t64[3] * 1e-5,
                 t64[4] * 1e-5, t64[5] * 1e-5, t64[6] * 1e-5, t64[7] * 1e-5);
+        const double span = (double)(t64[9] - ~t64[10]);
+        fprintf(stderr, "[ndfl] count waves %llu: busy %.1f ms x waves, span %.3f ms, occupancy %.3f\n",
+                (unsigned long long)t64[11], t64[8] * 1e-5, span * 1e-5, t64[11] ? t64[8] / (span * t64[11]) : 0.0);
     }
     const uint64_t total = off - dict_len;
     ht[3] = hnow();

@@ -207,14 +207,22 @@ __device__ __forceinline__ Lv make_lv(const Stage& st, const Geo& g, int lane) {
 // CAREFUL = false: the caller guarantees pos + 48 < stop <= nb (no token can reach the stop or the
 // input end), so those checks are dropped.
 template <bool CAREFUL>
+__device__ __forceinline__ void tok_e(uint32_t lo, uint32_t hi, uint32_t e, uint32_t& pos, const Tabs& t,
+                                      bool empty_dist, uint32_t stop, uint32_t nb, Tok& tk);
+template <bool CAREFUL>
 __device__ __forceinline__ void tok(const Lv& v, uint32_t& pos, const Tabs& t, bool empty_dist, uint32_t stop,
                                     uint32_t nb, Tok& tk) {
     // (the result goes through scalars and is stored into tk once: stores of different fields on
     // different paths made the compiler keep tk in scratch memory)
-    uint32_t kind, val, n = 1, dist = 0;
     uint32_t lo, hi;
     v.win(pos, lo, hi);
-    uint32_t e = t.lit[lo & ((1u << LB) - 1u)];
+    tok_e<CAREFUL>(lo, hi, t.lit[lo & ((1u << LB) - 1u)], pos, t, empty_dist, stop, nb, tk);
+}
+// the rest of a token step once its window (lo, hi) and primary entry e are loaded
+template <bool CAREFUL>
+__device__ __forceinline__ void tok_e(uint32_t lo, uint32_t hi, uint32_t e, uint32_t& pos, const Tabs& t,
+                                      bool empty_dist, uint32_t stop, uint32_t nb, Tok& tk) {
+    uint32_t kind, val, n = 1, dist = 0;
     do {
         if (e >> 31) {
             const uint32_t l1 = e & 15, l12 = (e >> 4) & 15;
@@ -711,6 +719,9 @@ __device__ void round_decode(const In& in, const Tabs& t, bool ed, uint64_t rs, 
 // phase whose first token ends at x.  Lane j turns lane j-1's 8 phase ends into a map (phase of
 // lane j-1 -> phase of lane j); a wave prefix scan composes the maps, lane 0 being phase 0.  Only
 // lanes whose entry matches no phase fall back to an in-order decode.
+#ifndef NDFL_PHASE_PAIRS
+#define NDFL_PHASE_PAIRS 1
+#endif
 struct PhMap {
     uint32_t cnt[8][64];                     // bytes of the phase run
     uint32_t fbc[8][64];                     // bytes of its first token
@@ -734,6 +745,59 @@ __device__ __forceinline__ void phase_run(const Lv& v0, const Tabs& t, bool ed, 
             kr = tk.kind == K_EOB ? (T_EOB << 5) : ((T_ERR << 5) | tk.val);
     }
     end = pos; cnt = c;
+}
+
+// Two phase runs at once (starts sa, sb; same results as two phase_run calls).  After each run's
+// first token, the runs step together: both windows and both primary lookups are issued before
+// either position moves, so the two dependent LDS chains overlap; a step that is not a plain literal
+// (or pair) goes through the full token decoder.  Phase-locked codes are literal-dominated.
+struct PhOut { uint32_t end, cnt, kr, fb, fbc; };
+__device__ __forceinline__ void phase_first(const Lv& v, const Tabs& t, bool ed, uint32_t nb, uint32_t st, uint32_t e,
+                                            uint32_t& pos, uint32_t& c, PhOut& o, bool& live) {
+    pos = st; c = 0;
+    o.kr = T_EXIT << 5; o.fb = NOCP; o.fbc = 0;
+    live = false;
+    if (pos < e) {
+        Tok tk;
+        tok<true>(v, pos, t, ed, pos + 1, nb, tk);      // a single token (no pair)
+        if (tk.kind > K_LEN) o.kr = tk.kind == K_EOB ? (T_EOB << 5) : ((T_ERR << 5) | tk.val);
+        else { c = tk.n; o.fb = pos; o.fbc = tk.n; live = true; }
+    }
+}
+__device__ __forceinline__ void phase_pair(const Lv& v, const Tabs& t, bool ed, uint32_t nb, uint32_t sa, uint32_t sb,
+                                           uint32_t e, PhOut& A, PhOut& B) {
+    uint32_t pa, ca, pb, cb;
+    bool la, lb;
+    phase_first(v, t, ed, nb, sa, e, pa, ca, A, la);
+    phase_first(v, t, ed, nb, sb, e, pb, cb, B, lb);
+    for (;;) {
+        const bool fa = la && pa + 48 < e, fb = lb && pb + 48 < e;
+        if (!fa && !fb) break;
+        uint32_t loa, hia, lob, hib;
+        v.win(fa ? pa : pb, loa, hia);
+        v.win(fb ? pb : pa, lob, hib);
+        const uint32_t ea = t.lit[loa & ((1u << LB) - 1u)], eb = t.lit[lob & ((1u << LB) - 1u)];
+        const bool qa = fa && (ea >> 31), qb = fb && (eb >> 31);
+        if (qa) { const bool two = (ea >> 8) & 1; pa += two ? (ea >> 4) & 15 : ea & 15; ca += two ? 2u : 1u; }
+        if (qb) { const bool two = (eb >> 8) & 1; pb += two ? (eb >> 4) & 15 : eb & 15; cb += two ? 2u : 1u; }
+        if (fa && !qa) {
+            Tok tk;
+            tok_e<false>(loa, hia, ea, pa, t, ed, e, nb, tk);
+            if (tk.kind > K_LEN) { la = false; A.kr = tk.kind == K_EOB ? (T_EOB << 5) : ((T_ERR << 5) | tk.val); }
+            else ca += tk.n;
+        }
+        if (fb && !qb) {
+            Tok tk;
+            tok_e<false>(lob, hib, eb, pb, t, ed, e, nb, tk);
+            if (tk.kind > K_LEN) { lb = false; B.kr = tk.kind == K_EOB ? (T_EOB << 5) : ((T_ERR << 5) | tk.val); }
+            else cb += tk.n;
+        }
+    }
+    Tok tk;
+    if (la && run_to(v, pa, t, ed, e, nb, ca, tk)) A.kr = tk.kind == K_EOB ? (T_EOB << 5) : ((T_ERR << 5) | tk.val);
+    if (lb && run_to(v, pb, t, ed, e, nb, cb, tk)) B.kr = tk.kind == K_EOB ? (T_EOB << 5) : ((T_ERR << 5) | tk.val);
+    A.end = pa; A.cnt = ca;
+    B.end = pb; B.cnt = cb;
 }
 
 __device__ __forceinline__ uint32_t sel8(const uint32_t (&v)[8], uint32_t i) {
@@ -777,6 +841,23 @@ __device__ __noinline__ void round_decode_phased(const In& in, const Tabs& t, bo
     PhMap* pm = (PhMap*)ph;
     uint32_t endv[8];
     uint32_t fbl = 0, fbh = 0;
+#if NDFL_PHASE_PAIRS
+#pragma unroll
+    for (uint32_t f = 0; f < 8; f += 2) {
+        PhOut P[2];
+        phase_pair(v, t, ed, nb, s + f, s + f + 1, e, P[0], P[1]);   // (past e: empty, ends at s + f)
+#pragma unroll
+        for (uint32_t h = 0; h < 2; h++) {
+            const uint32_t g = f + h;
+            endv[g] = P[h].end;
+            pm->cnt[g][lane] = P[h].cnt;
+            pm->fbc[g][lane] = P[h].fbc;
+            pm->kr[g][lane] = (uint8_t)P[h].kr;
+            const uint32_t fo = (P[h].fb != NOCP && P[h].fb - s < 255u) ? P[h].fb - s : 255u;
+            if (g < 4) fbl |= fo << (8 * g); else fbh |= fo << (8 * (g - 4));
+        }
+    }
+#else
     for (uint32_t f = 0; f < 8; f++) {
         uint32_t en, cn, kr, fb, fbc;
         phase_run(v, t, ed, nb, s + f, e, en, cn, kr, fb, fbc);      // (past e: empty, ends at s + f)
@@ -788,6 +869,7 @@ __device__ __noinline__ void round_decode_phased(const In& in, const Tabs& t, bo
         const uint32_t fo = (fb != NOCP && fb - s < 255u) ? fb - s : 255u;
         if (f < 4) fbl |= fo << (8 * f); else fbh |= fo << (8 * (f - 4));
     }
+#endif
     // map of lane j: phase of lane j-1 -> phase of lane j
     uint32_t Q = 0;                             // lane 0: always phase 0
 #pragma unroll
@@ -1003,6 +1085,7 @@ ndfl_inflate_count_wave_kernel(const uint32_t* w, uint64_t nwords, uint64_t nbit
     const int lane = threadIdx.x;
     PhArr* ph = ph_all + blockIdx.x;
     const In in{w, nwords, nbits};
+    const uint64_t t_begin = stats ? wall_clock64() : 0;
     for (;;) {
     __syncthreads();
     if (lane == 0) s_ticket = atomicAdd(ticket, 1u);
@@ -1134,6 +1217,14 @@ ndfl_inflate_count_wave_kernel(const uint32_t* w, uint64_t nwords, uint64_t nbit
             atomicAdd(&st64[6], pcl.build); atomicAdd(&st64[7], pcl.phmap);
         }
     }
+    }
+    if (stats && lane == 0) {                   // wave occupancy of the pass: busy sum, first start, last end
+        unsigned long long* st64 = (unsigned long long*)(stats + 32);
+        const uint64_t t_end = wall_clock64();
+        atomicAdd(&st64[8], t_end - t_begin);
+        atomicMax(&st64[9], t_end);
+        atomicMax(&st64[10], ~t_begin);
+        atomicAdd(&st64[11], 1ull);
     }
 }
 
