@@ -723,11 +723,12 @@ struct InflateScratch {
 // Persistent-wave grid of a one-wave-workgroup kernel: what fits on the chip at once (occupancy),
 // at most `cap` waves.
 template <typename K>
-static uint32_t wave_grid(K kernel, uint32_t cap) {
+static uint32_t wave_grid(K kernel, uint32_t cap, const char* env = nullptr) {
     int dev = 0, ncu = 0, per = 0;
     if (hipGetDevice(&dev) != hipSuccess || hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess ||
         hipOccupancyMaxActiveBlocksPerMultiprocessor(&per, kernel, 64, 0) != hipSuccess || ncu <= 0 || per <= 0)
         return cap;
+    if (env && getenv(env)) per = std::max(1, atoi(getenv(env)));     // waves per CU override (tuning)
     return std::min<uint32_t>(cap, (uint32_t)(ncu * per));
 }
 
@@ -959,7 +960,7 @@ static int inflate_run(InflateScratch& S, hipStream_t s, const uint8_t* in, uint
         if (!S.d_cticket) INF_CHK(hipMalloc(&S.d_cticket, 64));
         INF_CHK(hipMemsetAsync(S.d_cticket, 0, 4, s));
         if (S.count_first) INF_CHK(hipEventRecord(S.ev[2], s));
-        static const uint32_t count_grid = wave_grid(ndfl_inflate_count_wave_kernel, COUNT_WAVES);
+        static const uint32_t count_grid = wave_grid(ndfl_inflate_count_wave_kernel, COUNT_WAVES, "NDFL_COUNT_WPC");
         hipLaunchKernelGGL(ndfl_inflate_count_wave_kernel, dim3((uint32_t)std::min<size_t>(n, count_grid)), dim3(64), 0, s,
                            d_w, nwords, nbits,
                            (const uint64_t*)S.d_starts, (const uint64_t*)S.d_stops, (uint32_t)n,
@@ -1117,7 +1118,7 @@ static int inflate_run(InflateScratch& S, hipStream_t s, const uint8_t* in, uint
     hipEvent_t e2 = S.ev[4], e3 = S.ev[5];
     INF_CHK(hipEventRecord(e2, s));
     if (!S.d_ph) INF_CHK(hipMalloc(&S.d_ph, (size_t)std::max(COUNT_WAVES, EMIT_WAVES) * sizeof(wv::PhArr)));
-    static const uint32_t emit_grid = wave_grid(ndfl_inflate_emit_wave_kernel, EMIT_WAVES);
+    static const uint32_t emit_grid = wave_grid(ndfl_inflate_emit_wave_kernel, EMIT_WAVES, "NDFL_EMIT_WPC");
     hipLaunchKernelGGL(ndfl_inflate_emit_wave_kernel, dim3(std::min<uint32_t>(nch, emit_grid)), dim3(64), 0, s, d_w,
                        nwords, nbits, (const EmitChain*)S.d_chains, nch, (uint32_t*)S.d_ticket, d_out,
                        (ChainRes*)S.d_res, (const uint64_t*)S.d_cands, ncand, (uint32_t*)S.d_ref, (uint32_t*)S.d_pend,

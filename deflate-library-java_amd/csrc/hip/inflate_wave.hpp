@@ -51,8 +51,8 @@ struct Shared {
     Tabs t;
     uint8_t lens[320];                       // literal/length 0..287, distance at 288..319
     uint16_t cl_tab[128];                    // code-length code, full 7-bit table: sym | len << 9
-    uint64_t exit_[64];
-    uint32_t kind_[64];
+    uint32_t exit_[64];                      // round-relative lane exits
+    uint8_t kind_[64];
     // header broadcast (lane 0 -> wave)
     uint64_t h_pos, h_d0;
     uint32_t h_err, h_bfinal, h_btype, h_len, h_numlit, h_numdist;
@@ -129,9 +129,9 @@ struct Tok {
 // the image per instruction), so the decode loop carries no prefetch state at all: a token is read
 // from its absolute position with one ds_read2st64 + one ds_read and two funnel shifts.
 #ifndef NDFL_LPW
-#define NDFL_LPW 16
+#define NDFL_LPW 14
 #endif
-constexpr uint32_t LPW = NDFL_LPW;             // words per lane segment at most (512 bits by default)
+constexpr uint32_t LPW = NDFL_LPW;             // words per lane segment at most (448 bits by default)
 constexpr uint32_t SW = LPW + 4;               // staged words per lane region (+ the tail window)
 constexpr uint64_t RSPAN = 64ull * LPW * 32;   // round span cap (bits)
 
