@@ -72,6 +72,19 @@ struct Persist {
     uint32_t crcAcc[NW];
 };
 
+// The split passes (hist, emit) keep no code-construction state: a smaller block of persistent LDS,
+// so that two emit workgroups (bit buffer + this) fit a CU.
+struct PersistS {
+    uint32_t litCode[288];
+    uint32_t distCode[32];
+    uint64_t scan64[NW];
+    uint32_t scan32[NW];
+    uint32_t chunk;
+    uint32_t hdrBits;
+    uint64_t P;
+    uint32_t crcAcc[NW];
+};
+
 struct Args {
     const uint8_t* in;        // data region of this call (device)
     uint64_t n;
@@ -110,6 +123,13 @@ constexpr int HDRW = 80;                  // >= 3 + 14 + 57 + 316 * 7 = 2286 bit
 constexpr int CREC_META = CREC_HDR + HDRW;  // [0] hdrBits
 constexpr int CREC = CREC_META + 16;
 enum { MODE_FUSED = 0, MODE_HIST = 1, MODE_EMIT = 2 };
+// hist pass: HCOPY lane-interleaved histogram copies at a stride of HSTR words (HSTR mod 64 = 20:
+// the copies of a symbol fall in different LDS banks)
+#ifndef NDFL_HCOPY
+#define NDFL_HCOPY 8
+#endif
+constexpr int HCOPY = NDFL_HCOPY;
+constexpr int HSTR = HCOPY > 4 ? 340 : 336;
 
 // Length symbol / extra bits of a run 3..258 (D/comp/Lz77Huffman.java:92-111).
 __device__ __forceinline__ void run_sym(uint32_t run, uint32_t& sym, uint32_t& ne, uint32_t& ex) {
@@ -507,8 +527,8 @@ __device__ __forceinline__ void block_store(const uint32_t* obuf, uint64_t P, ui
 // look-back for the offset); the split pipeline runs it as MODE_HIST (load, CRC, histograms to
 // hist_out) and, after ndfl_deflate_codes_kernel and ndfl_deflate_offsets_kernel, MODE_EMIT (load,
 // code tables and header from the record, token bits at the precomputed offset).
-template <int MODE>
-__device__ __forceinline__ void deflate_chunk(const Args& a, uint32_t* obuf, Persist& ps, uint32_t* hl4 = nullptr,
+template <int MODE, class PS>
+__device__ __forceinline__ void deflate_chunk(const Args& a, uint32_t* obuf, PS& ps, uint32_t* hl4 = nullptr,
                                               uint32_t* ctab = nullptr) {
     char* scr = (char*)obuf;
     uint32_t* hlit = (uint32_t*)(scr + SCR_HLIT);
@@ -529,7 +549,7 @@ __device__ __forceinline__ void deflate_chunk(const Args& a, uint32_t* obuf, Per
         if (tid < 288) hlit[tid] = 0;
         if (tid < 32) hdist[tid] = 0;
     } else if (MODE == MODE_HIST) {
-        for (int k = tid; k < 4 * 336; k += DT) hl4[k] = 0;
+        for (int k = tid; k < HCOPY * HSTR; k += DT) hl4[k] = 0;
         if (a.crc_raw) ctab[tid] = a.crc_tab[tid];          // slicing-by-4 tables to LDS (DT == 1024)
     }
     __syncthreads();
@@ -686,11 +706,11 @@ __device__ __forceinline__ void deflate_chunk(const Args& a, uint32_t* obuf, Per
     }
 
     // ---- 3. histograms (closed-form greedy parse per piece, App. A.2) -------------------------
-    // MODE_HIST counts into 4 lane-interleaved copies (fewer same-address LDS atomics per
-    // instruction; copy stride 336 words puts a symbol's copies in 4 different banks)
+    // MODE_HIST counts into HCOPY lane-interleaved copies (fewer same-address LDS atomics per
+    // instruction; see HCOPY / HSTR)
     uint32_t* hl = hlit;
     uint32_t* hd = hdist;
-    if (MODE == MODE_HIST) { hl = hl4 + (tid & 3) * 336; hd = hl + 288; }
+    if (MODE == MODE_HIST) { hl = hl4 + (tid & (HCOPY - 1)) * HSTR; hd = hl + 288; }
     if (MODE != MODE_EMIT) {
 #define PF_(x) 0u
     NDFL_FOR_PIECES({
@@ -720,14 +740,19 @@ __device__ __forceinline__ void deflate_chunk(const Args& a, uint32_t* obuf, Per
     }
     if (MODE == MODE_HIST) {
         uint32_t* h = a.hist_out + (uint64_t)c * HREC;
-        if (tid < HREC) h[tid] = hl4[tid] + hl4[336 + tid] + hl4[672 + tid] + hl4[1008 + tid];
+        if (tid < HREC) {
+            uint32_t v = 0;
+#pragma unroll
+            for (int k = 0; k < HCOPY; k++) v += hl4[k * HSTR + tid];
+            h[tid] = v;
+        }
         return;
     }
 
     const uint64_t tp2 = wall_clock64();
     // ---- 4. code construction -------------------------------------------------------------------
     uint32_t packedLo = 0, packedHi = 0;
-    if (MODE == MODE_FUSED) {
+    if constexpr (MODE == MODE_FUSED) {
         build_block_codes(a.dynamic != 0, scr, ps, a.prof ? a.prof + (uint64_t)c * 16 + 8 : nullptr);
         packedLo = misc[4]; packedHi = misc[5];
     } else {
@@ -789,7 +814,7 @@ __device__ __forceinline__ void deflate_chunk(const Args& a, uint32_t* obuf, Per
     const uint32_t bit0 = 0;
 
     // ---- 6. emit ------------------------------------------------------------------------------
-    if (MODE == MODE_FUSED) {
+    if constexpr (MODE == MODE_FUSED) {
         emit_block_header(obuf, is_final, a.dynamic != 0, ps, packedLo, packedHi, hdrBits, tokTotal, eobLen);
     } else if (tid == 0) {
         BitPut be; be.init(obuf, bit0 + hdrBits + tokTotal);
@@ -827,7 +852,7 @@ __device__ __forceinline__ void deflate_chunk(const Args& a, uint32_t* obuf, Per
 
     const uint64_t tp5e = wall_clock64();
     // ---- 7. look-back, then store shifted to the global bit offset ---------------------------
-    if (MODE == MODE_FUSED) block_lookback(c, a.base_bit, S, a.status, ps);
+    if constexpr (MODE == MODE_FUSED) block_lookback(c, a.base_bit, S, a.status, ps);
     const uint64_t tp5 = wall_clock64();
     const uint64_t P = MODE == MODE_FUSED ? ps.P : a.chunk_off[c];
     block_store(obuf, P, S, c, a.out, a.edge_w, a.edge_v);
@@ -853,9 +878,9 @@ ndfl_deflate_chunks_kernel(Args a) {
 extern "C" __global__ void __launch_bounds__(DT, 8)
 ndfl_deflate_hist_kernel(Args a) {
     __shared__ __attribute__((aligned(16))) uint32_t obuf[(SCR_LAST + 1024) / 4];
-    __shared__ __attribute__((aligned(16))) uint32_t hl4[4 * 336];
+    __shared__ __attribute__((aligned(16))) uint32_t hl4[HCOPY * HSTR];
     __shared__ uint32_t ctab[1024];
-    __shared__ Persist ps;
+    __shared__ PersistS ps;
     deflate_chunk<MODE_HIST>(a, obuf, ps, hl4, ctab);
 }
 
@@ -863,7 +888,7 @@ ndfl_deflate_hist_kernel(Args a) {
 extern "C" __global__ void __launch_bounds__(DT, 8)
 ndfl_deflate_emit_kernel(Args a) {
     __shared__ __attribute__((aligned(16))) uint32_t obuf[OUTW];
-    __shared__ Persist ps;
+    __shared__ PersistS ps;
     deflate_chunk<MODE_EMIT>(a, obuf, ps);
 }
 
