@@ -23,19 +23,23 @@ struct WScr {
     uint32_t hlit[288];
     uint32_t hdist[32];
     uint32_t hdist0[32];      // distance histogram before the single-code fix-up (token bits)
-    uint32_t key[292];        // padded to a multiple of 4
+    union {
+        uint32_t key[292];        // padded to a multiple of 4 (package-merge input)
+        uint32_t hdr[HDRW];       // header bits: written after the last package-merge
+    };
     uint32_t lf[288];
     uint16_t ls[288];
     uint32_t pf[2][304];
-    uint32_t mf[608];
+    union {
+        uint32_t mf[608];         // package-merge levels
+        uint16_t clOff[320];      // header bit offset of each code-length symbol (after the last one)
+    };
     uint32_t mpk[15 * 20];
     uint32_t lvl[16];
     uint32_t blc[16], nxc[16], mask[16 * 10];
     uint32_t clh[20];
     uint32_t clCode[20];
-    uint32_t hdr[HDRW];
     uint32_t misc[8];
-    uint16_t clOff[320];
     uint8_t clSym[320], clExtra[320];
     uint8_t lens[320];
     uint8_t clLen[32];
@@ -310,6 +314,7 @@ ndfl_deflate_codes_kernel(Args a) {
         __syncthreads();
         wpm_lengths(S.clh, 19, 7, S.clLen, S);
         wcanon(S.clLen, 19, S.clCode, S);
+        for (int i = lane; i < HDRW; i += 64) S.hdr[i] = 0;          // (hdr shares key's LDS)
         // per-symbol header bit offsets (exclusive scan, lane owns [5l, 5l+5))
         uint32_t sb[5], lsum = 0;
 #pragma unroll
