@@ -566,17 +566,18 @@ ndfl_inflate_strict_kernel(const uint32_t* w, uint64_t nwords, uint64_t nbits, c
         n_steps += 64 - nidle;
         if (active) {
             // one code-length symbol (D/decomp/Open.java's dynamic header loop, same checks)
+            // one refill covers the code (<= 7 bits) and its extra bits (<= 7): no branch per symbol kind
             rd.fill(in);
-            const uint32_t x = __builtin_bitreverse32(rd.peek(7)) >> 25;
-            const uint32_t te = tab[x];
-            const uint32_t sym = te & 31u;
-            rd.skip(te >> 5);
-            uint32_t run = 1;
-            bool bad = false;
-            if (sym < 16) runVal = (int)sym;
-            else if (sym == 16) { if (runVal < 0) bad = true; run = rd.get(in, 2) + 3; }
-            else if (sym == 17) { runVal = 0; run = rd.get(in, 3) + 3; }
-            else { runVal = 0; run = rd.get(in, 7) + 11; }
+            const uint32_t b = (uint32_t)rd.bb;
+            const uint32_t te = tab[__builtin_bitreverse32(b) >> 25];
+            const uint32_t sym = te & 31u, cl = te >> 5;
+            const bool s16 = sym == 16, s17 = sym == 17, s18 = sym == 18;
+            const uint32_t nx = s16 ? 2u : s17 ? 3u : s18 ? 7u : 0u;
+            const uint32_t ex = (b >> cl) & ((1u << nx) - 1u);
+            const uint32_t run = sym < 16 ? 1u : ex + (s18 ? 11u : 3u);
+            const bool bad = s16 && runVal < 0;
+            runVal = sym < 16 ? (int)sym : s16 ? runVal : 0;
+            rd.skip(cl + nx);
             if (bad || i + run > total || rd.pos > in.nbits) {
                 active = false;
             } else {
