@@ -578,36 +578,29 @@ ndfl_inflate_strict_kernel(const uint32_t* w, uint64_t nwords, uint64_t nbits, c
             const bool bad = s16 && runVal < 0;
             runVal = sym < 16 ? (int)sym : s16 ? runVal : 0;
             rd.skip(cl + nx);
-            if (bad || i + run > total || rd.pos > in.nbits) {
-                active = false;
-            } else {
-                const uint32_t v = (uint32_t)runVal;
-                const uint32_t en = i + run;
-                if (i < numLit) {
-                    const uint32_t c = min(en, numLit) - i;
-                    if (v) { litK += c * (32768u >> v); if (litK > 32768u) active = false; }
-                    if (i <= 256 && 256 < en) eob = v;
-                }
-                if (en > numLit) {
-                    const uint32_t a0 = max(i, numLit) - numLit, b2 = en - numLit, c = b2 - a0;
-                    if (v) {
-                        distK += c * (32768u >> v);
-                        if (distK > 32768u) active = false;
-                        if (v == 1) ones += c; else other += c;
-                    }
-                    if (a0 == 0) d0 = v;
-                    if (a0 <= 31 && 31 < b2) d31 = v;
-                }
-                i = en;
-                if (active && i >= total) {
-                    active = false;
-                    bool ok;
-                    if (eob == 0 || litK != 32768u) ok = false;
-                    else if (numDist == 1 && d0 == 0) ok = true;
-                    else if (ones == 1 && other == 0) ok = !(numDist == 32 && d31 == 1);
-                    else ok = distK == 32768u;
-                    if (ok) record(p);
-                }
+            // running Kraft sums of the literal/length part [i, min(en, numLit)) and the distance part
+            // (branch-free: the lane's state is only read again if it stays active)
+            const uint32_t en = i + run;
+            const uint32_t v = (uint32_t)runVal;
+            const uint32_t wt = v ? (32768u >> v) : 0u;
+            litK += (min(en, numLit) - min(i, numLit)) * wt;
+            const uint32_t da = max(i, numLit) - numLit, db = max(en, numLit) - numLit, cd = db - da;
+            distK += cd * wt;
+            ones += v == 1 ? cd : 0u;
+            other += v > 1 ? cd : 0u;
+            eob = (i <= 256 && 256 < en) ? v : eob;
+            d0 = (cd && da == 0) ? v : d0;
+            d31 = (da <= 31 && 31 < db) ? v : d31;
+            i = en;
+            const bool go = !(bad || en > total || rd.pos > in.nbits) && litK <= 32768u && distK <= 32768u;
+            active = go && i < total;
+            if (go && i >= total) {
+                bool ok;
+                if (eob == 0 || litK != 32768u) ok = false;
+                else if (numDist == 1 && d0 == 0) ok = true;
+                else if (ones == 1 && other == 0) ok = !(numDist == 32 && d31 == 1);
+                else ok = distK == 32768u;
+                if (ok) record(p);
             }
         }
     }
