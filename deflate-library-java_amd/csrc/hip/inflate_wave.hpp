@@ -719,9 +719,9 @@ __device__ void round_decode(const In& in, const Tabs& t, bool ed, uint64_t rs, 
 // phase whose first token ends at x.  Lane j turns lane j-1's 8 phase ends into a map (phase of
 // lane j-1 -> phase of lane j); a wave prefix scan composes the maps, lane 0 being phase 0.  Only
 // lanes whose entry matches no phase fall back to an in-order decode.
-#ifndef NDFL_PHASE_PAIRS
-#define NDFL_PHASE_PAIRS 1
-#endif
+#ifndef NDFL_PHASE_GROUP
+#define NDFL_PHASE_GROUP 8     // phase runs decoded together (1, 2, 4 or 8; measured 1: 14.6, 2: 13.9,
+#endif                         // 4: 12.9, 8: 12.8 ms count pass)
 struct PhMap {
     uint32_t cnt[8][64];                     // bytes of the phase run
     uint32_t fbc[8][64];                     // bytes of its first token
@@ -747,10 +747,11 @@ __device__ __forceinline__ void phase_run(const Lv& v0, const Tabs& t, bool ed, 
     end = pos; cnt = c;
 }
 
-// Two phase runs at once (starts sa, sb; same results as two phase_run calls).  After each run's
-// first token, the runs step together: both windows and both primary lookups are issued before
-// either position moves, so the two dependent LDS chains overlap; a step that is not a plain literal
-// (or pair) goes through the full token decoder.  Phase-locked codes are literal-dominated.
+// Several phase runs at once (same results as phase_run on each).  After each run's first token,
+// the runs step together: all windows and all primary lookups are issued before any position
+// moves, so the dependent LDS chains of the runs overlap; a step that is not a plain literal (or
+// pair) goes through the full token decoder with the window and entry already loaded.  Phase-locked
+// codes are literal-dominated.
 struct PhOut { uint32_t end, cnt, kr, fb, fbc; };
 __device__ __forceinline__ void phase_first(const Lv& v, const Tabs& t, bool ed, uint32_t nb, uint32_t st, uint32_t e,
                                             uint32_t& pos, uint32_t& c, PhOut& o, bool& live) {
@@ -764,40 +765,42 @@ __device__ __forceinline__ void phase_first(const Lv& v, const Tabs& t, bool ed,
         else { c = tk.n; o.fb = pos; o.fbc = tk.n; live = true; }
     }
 }
-__device__ __forceinline__ void phase_pair(const Lv& v, const Tabs& t, bool ed, uint32_t nb, uint32_t sa, uint32_t sb,
-                                           uint32_t e, PhOut& A, PhOut& B) {
-    uint32_t pa, ca, pb, cb;
-    bool la, lb;
-    phase_first(v, t, ed, nb, sa, e, pa, ca, A, la);
-    phase_first(v, t, ed, nb, sb, e, pb, cb, B, lb);
+
+template <int N>
+__device__ __forceinline__ void phase_multi(const Lv& v, const Tabs& t, bool ed, uint32_t nb, uint32_t s0, uint32_t e,
+                                            PhOut (&O)[N]) {
+    uint32_t p[N], c[N];
+    bool l[N];
+#pragma unroll
+    for (int k = 0; k < N; k++) phase_first(v, t, ed, nb, s0 + k, e, p[k], c[k], O[k], l[k]);
     for (;;) {
-        const bool fa = la && pa + 48 < e, fb = lb && pb + 48 < e;
-        if (!fa && !fb) break;
-        uint32_t loa, hia, lob, hib;
-        v.win(fa ? pa : pb, loa, hia);
-        v.win(fb ? pb : pa, lob, hib);
-        const uint32_t ea = t.lit[loa & ((1u << LB) - 1u)], eb = t.lit[lob & ((1u << LB) - 1u)];
-        const bool qa = fa && (ea >> 31), qb = fb && (eb >> 31);
-        if (qa) { const bool two = (ea >> 8) & 1; pa += two ? (ea >> 4) & 15 : ea & 15; ca += two ? 2u : 1u; }
-        if (qb) { const bool two = (eb >> 8) & 1; pb += two ? (eb >> 4) & 15 : eb & 15; cb += two ? 2u : 1u; }
-        if (fa && !qa) {
-            Tok tk;
-            tok_e<false>(loa, hia, ea, pa, t, ed, e, nb, tk);
-            if (tk.kind > K_LEN) { la = false; A.kr = tk.kind == K_EOB ? (T_EOB << 5) : ((T_ERR << 5) | tk.val); }
-            else ca += tk.n;
-        }
-        if (fb && !qb) {
-            Tok tk;
-            tok_e<false>(lob, hib, eb, pb, t, ed, e, nb, tk);
-            if (tk.kind > K_LEN) { lb = false; B.kr = tk.kind == K_EOB ? (T_EOB << 5) : ((T_ERR << 5) | tk.val); }
-            else cb += tk.n;
+        bool f[N], any = false;
+#pragma unroll
+        for (int k = 0; k < N; k++) { f[k] = l[k] && p[k] + 48 < e; any = any || f[k]; }
+        if (!any) break;
+        uint32_t lo[N], hi[N], en[N];
+#pragma unroll
+        for (int k = 0; k < N; k++) v.win(f[k] ? p[k] : p[0], lo[k], hi[k]);
+#pragma unroll
+        for (int k = 0; k < N; k++) en[k] = t.lit[lo[k] & ((1u << LB) - 1u)];
+#pragma unroll
+        for (int k = 0; k < N; k++) {
+            const bool q = f[k] && (en[k] >> 31);
+            if (q) { const bool two = (en[k] >> 8) & 1; p[k] += two ? (en[k] >> 4) & 15 : en[k] & 15; c[k] += two ? 2u : 1u; }
+            if (f[k] && !q) {
+                Tok tk;
+                tok_e<false>(lo[k], hi[k], en[k], p[k], t, ed, e, nb, tk);
+                if (tk.kind > K_LEN) { l[k] = false; O[k].kr = tk.kind == K_EOB ? (T_EOB << 5) : ((T_ERR << 5) | tk.val); }
+                else c[k] += tk.n;
+            }
         }
     }
-    Tok tk;
-    if (la && run_to(v, pa, t, ed, e, nb, ca, tk)) A.kr = tk.kind == K_EOB ? (T_EOB << 5) : ((T_ERR << 5) | tk.val);
-    if (lb && run_to(v, pb, t, ed, e, nb, cb, tk)) B.kr = tk.kind == K_EOB ? (T_EOB << 5) : ((T_ERR << 5) | tk.val);
-    A.end = pa; A.cnt = ca;
-    B.end = pb; B.cnt = cb;
+#pragma unroll
+    for (int k = 0; k < N; k++) {
+        Tok tk;
+        if (l[k] && run_to(v, p[k], t, ed, e, nb, c[k], tk)) O[k].kr = tk.kind == K_EOB ? (T_EOB << 5) : ((T_ERR << 5) | tk.val);
+        O[k].end = p[k]; O[k].cnt = c[k];
+    }
 }
 
 __device__ __forceinline__ uint32_t sel8(const uint32_t (&v)[8], uint32_t i) {
@@ -841,13 +844,14 @@ __device__ __noinline__ void round_decode_phased(const In& in, const Tabs& t, bo
     PhMap* pm = (PhMap*)ph;
     uint32_t endv[8];
     uint32_t fbl = 0, fbh = 0;
-#if NDFL_PHASE_PAIRS
+#if NDFL_PHASE_GROUP > 1
+    constexpr uint32_t G = NDFL_PHASE_GROUP >= 8 ? 8 : NDFL_PHASE_GROUP >= 4 ? 4 : 2;
 #pragma unroll
-    for (uint32_t f = 0; f < 8; f += 2) {
-        PhOut P[2];
-        phase_pair(v, t, ed, nb, s + f, s + f + 1, e, P[0], P[1]);   // (past e: empty, ends at s + f)
+    for (uint32_t f = 0; f < 8; f += G) {
+        PhOut P[G];
+        phase_multi<G>(v, t, ed, nb, s + f, e, P);       // (past e: empty, ends at s + f)
 #pragma unroll
-        for (uint32_t h = 0; h < 2; h++) {
+        for (uint32_t h = 0; h < G; h++) {
             const uint32_t g = f + h;
             endv[g] = P[h].end;
             pm->cnt[g][lane] = P[h].cnt;
