@@ -719,6 +719,9 @@ __device__ void round_decode(const In& in, const Tabs& t, bool ed, uint64_t rs, 
 // phase whose first token ends at x.  Lane j turns lane j-1's 8 phase ends into a map (phase of
 // lane j-1 -> phase of lane j); a wave prefix scan composes the maps, lane 0 being phase 0.  Only
 // lanes whose entry matches no phase fall back to an in-order decode.
+#ifndef NDFL_PHASE_SWITCH
+#define NDFL_PHASE_SWITCH 48   // lanes of a round that failed to synchronise before the block's next
+#endif                         // rounds are phase-mapped
 #ifndef NDFL_PHASE_GROUP
 #define NDFL_PHASE_GROUP 8     // phase runs decoded together (1, 2, 4 or 8; measured 1: 14.6, 2: 13.9,
 #endif                         // 4: 12.9, 8: 12.8 ms count pass)
@@ -1159,7 +1162,7 @@ ndfl_inflate_count_wave_kernel(const uint32_t* w, uint64_t nwords, uint64_t nbit
             } else {
                 const uint32_t ns0 = nslow;
                 round_decode(in, S.t, ed, rs, E, S, stg, lane, r, ft, nslow, nfix, ph, g, pc);
-                if (nslow - ns0 > 32) phased = true;    // phase-locked code: map the next rounds
+                if (nslow - ns0 > NDFL_PHASE_SWITCH) phased = true;    // phase-locked code: map the next rounds
             }
             if (pc) tb = wall_clock64();
             if (recording) {
