@@ -721,7 +721,8 @@ __device__ void round_decode(const In& in, const Tabs& t, bool ed, uint64_t rs, 
 // lanes whose entry matches no phase fall back to an in-order decode.
 #ifndef NDFL_PHASE_SWITCH
 #define NDFL_PHASE_SWITCH 48   // lanes of a round that failed to synchronise before the block's next
-#endif                         // rounds are phase-mapped
+#endif                         // rounds are phase-mapped (measured: 4-16 much slower; 32 -> 48: config 2
+                               // count 16.9 -> 9.5 ms, fixed-Huffman text resyncs through the 8-phase verify)
 #ifndef NDFL_PHASE_GROUP
 #define NDFL_PHASE_GROUP 8     // phase runs decoded together (1, 2, 4 or 8; measured 1: 14.6, 2: 13.9,
 #endif                         // 4: 12.9, 8: 12.8 ms count pass)
