@@ -660,21 +660,29 @@ __device__ __forceinline__ void deflate_chunk(const Args& a, uint32_t* obuf, PS&
         if (gpos == 0) return (has_prev0 && prev0 == v) ? 0u : 1u;
         return 1u;
     };
-    // pieces of length 1 (the next byte starts a piece, or the chunk ends) are exactly one literal
-    // whatever their lead; they take the fast path below
-    uint64_t S1 = 0;
+    // Piece classes per lane, over its 64 bytes (F bit i: a piece starts at byte i).  A
+    // piece of length plen with lead literal `lead` is R = plen - lead bytes of matches; R < 3 means
+    // it is plen literals of one value, whatever its lead (:62-90).  So a start is
+    //   mR1: 1 literal (plen 1), mR2: 2 literals (plen 2), mR3: 3 literals (plen 3, lead 1),
+    //   mLG: a run with a length token (R >= 3) -- the only class that needs the closed-form parse.
+    // plen comes from the next start: the lane's own starts, then nextStart as a marker bit (the
+    // chunk end is one).  Only the chunk's first byte can have lead 0 (its value continues the
+    // history), where plen 3 is R = 3: a run.
+    // The classes are formed per 8-byte group from F and the marker position mp (bit 31 of mpx: the
+    // chunk's first piece has lead 0), so only F and one word stay live across the loops.
+    uint32_t mpx = 0xFFFFu;
     if (vcnt > 0) {
-        const uint64_t nxt = (F >> 1) | (nextStart == t0 + 64 ? (1ull << 63) : 0ull);
-        const uint64_t beyond = vcnt >= 64 ? 0ull : (~0ull << (vcnt - 1));
-        S1 = F & (nxt | beyond);
+        mpx = nextStart - t0;
+        if (a.rle && tid == 0 && (F & 1) && lead_of(0, w[0] & 0xFFu) == 0) mpx |= 1u << 31;
     }
-    // visit this lane's pieces in order: BODY sees (gpos, v, pend, single) and pfv = PF_(v), which is
-    // evaluated for all 8 bytes of a group before the per-byte branches (independent LDS reads in
-    // flight instead of one exposed latency per byte).  Outer loop over 8-byte
-    // groups (select tree on the uniform group index: a dynamic register index would put w[] in
-    // scratch memory), inner loop unrolled: byte extraction is a constant shift.  A macro rather than
-    // a lambda: capturing w[] by reference also demotes it to scratch.
-#define NDFL_FOR_PIECES(...)                                                                           \
+    // visit this lane's bytes in order, 8 at a time.  Outer loop over 8-byte groups (select tree on
+    // the uniform group index: a dynamic register index would put w[] in scratch memory), inner loop
+    // unrolled by the caller: byte extraction is a constant shift.  BODY sees the group's bytes
+    // (gw0_, gw1_), its class masks (r1g_: >= 1 literal, r2g_: >= 2, r3g_: 3, lgg_: run) and whether
+    // any lane of the wave has a 2/3-literal piece (any2_) or a run (anyL_) in it, so the per-byte
+    // work of plain literal bytes is branch-free.  A macro rather than a lambda: capturing w[] by
+    // reference also demotes it to scratch.
+#define NDFL_FOR_GROUPS(...)                                                                           \
     _Pragma("unroll 1") for (int o_ = 0; o_ < 8; o_++) {                                               \
         const uint32_t g_ = (uint32_t)(F >> (8 * o_)) & 0xFFu;                                        \
         if (!__any(g_ != 0)) continue;                                                                 \
@@ -685,24 +693,28 @@ __device__ __forceinline__ void deflate_chunk(const Args& a, uint32_t* obuf, PS&
         const uint32_t b2_ = o1_ ? w[11] : w[9], b3_ = o1_ ? w[15] : w[13];                            \
         const uint32_t gw0_ = o4_ ? (o2_ ? a3_ : a2_) : (o2_ ? a1_ : a0_);                             \
         const uint32_t gw1_ = o4_ ? (o2_ ? b3_ : b2_) : (o2_ ? b1_ : b0_);                             \
-        uint32_t pf_[8];                                                                               \
-        _Pragma("unroll") for (int j_ = 0; j_ < 8; j_++)                                               \
-            pf_[j_] = PF_(((j_ < 4 ? gw0_ : gw1_) >> (8 * (j_ & 3))) & 0xFFu);                         \
-        _Pragma("unroll") for (int j_ = 0; j_ < 8; j_++) {                                             \
-            if ((g_ >> j_) & 1) {                                                                      \
-                const int i_ = 8 * o_ + j_;                                                            \
-                const uint32_t v = ((j_ < 4 ? gw0_ : gw1_) >> (8 * (j_ & 3))) & 0xFFu;                 \
-                const uint32_t pfv = pf_[j_];                                                          \
-                const bool single = (S1 >> i_) & 1;                                                    \
-                const uint32_t gpos = t0 + (uint32_t)i_;                                               \
-                uint32_t pend = gpos + 1;                                                              \
-                if (!single) {                                                                         \
-                    const uint64_t rest_ = i_ < 63 ? (F >> (i_ + 1)) : 0ull;                           \
-                    pend = rest_ ? gpos + 1 + (uint32_t)__builtin_ctzll(rest_) : nextStart;            \
-                }                                                                                      \
-                __VA_ARGS__                                                                            \
-            }                                                                                          \
-        }                                                                                              \
+        const uint32_t mq_ = (mpx & 0xFFFFu) - 8u * (uint32_t)o_;                                      \
+        const uint32_t win_ = (uint32_t)(F >> (8 * o_)) | (mq_ < 32u ? (1u << mq_) : 0u);              \
+        const uint32_t e1_ = win_ >> 1, e2_ = win_ >> 2, e3_ = win_ >> 3;                              \
+        uint32_t r3g_ = g_ & ~e1_ & ~e2_ & e3_;                                                        \
+        uint32_t lgg_ = g_ & ~(e1_ | e2_ | e3_);                                                       \
+        if (o_ == 0 && (mpx >> 31) && (r3g_ & 1u)) { r3g_ &= ~1u; lgg_ |= 1u; }                        \
+        const uint32_t r2g_ = (g_ & ~e1_ & e2_) | r3g_;                                                \
+        const uint32_t r1g_ = (g_ & e1_) | r2g_;                                                       \
+        const bool any2_ = __any(r2g_ != 0), anyL_ = __any(lgg_ != 0);                                 \
+        (void)r1g_; (void)any2_;                                                                       \
+        __VA_ARGS__                                                                                    \
+    }
+#define NDFL_BYTE(j) ((((j) < 4 ? gw0_ : gw1_) >> (8 * ((j) & 3))) & 0xFFu)
+    // a run starting at group byte j: its value v, start gpos and end pend (next start)
+#define NDFL_RUN(j, ...)                                                                               \
+    if (anyL_ && ((lgg_ >> (j)) & 1)) {                                                                \
+        const int i_ = 8 * o_ + (j);                                                                   \
+        const uint32_t v = NDFL_BYTE(j);                                                               \
+        const uint32_t gpos = t0 + (uint32_t)i_;                                                       \
+        const uint64_t rest_ = i_ < 63 ? (F >> (i_ + 1)) : 0ull;                                       \
+        const uint32_t pend = rest_ ? gpos + 1 + (uint32_t)__builtin_ctzll(rest_) : nextStart;         \
+        __VA_ARGS__                                                                                    \
     }
 
     // ---- 3. histograms (closed-form greedy parse per piece, App. A.2) -------------------------
@@ -712,26 +724,30 @@ __device__ __forceinline__ void deflate_chunk(const Args& a, uint32_t* obuf, PS&
     uint32_t* hd = hdist;
     if (MODE == MODE_HIST) { hl = hl4 + (tid & (HCOPY - 1)) * HSTR; hd = hl + 288; }
     if (MODE != MODE_EMIT) {
-#define PF_(x) 0u
-    NDFL_FOR_PIECES({
-        (void)pfv;
-        if (single || !a.rle) { atomicAdd(&hl[v], 1u); continue; }
-        const uint32_t plen = pend - gpos;
-        const uint32_t lead = lead_of(gpos, v);
-        const uint32_t R = plen - lead;
-        const uint32_t n258 = R / 258, m = R % 258;
-        uint32_t nlit = lead + (m < 3 ? m : 0);
-        if (nlit) atomicAdd(&hl[v], nlit);
-        if (n258) atomicAdd(&hl[285], n258);
-        uint32_t nd = n258;
-        if (m >= 3) {
-            uint32_t sym, ne, ex; run_sym(m, sym, ne, ex);
-            atomicAdd(&hl[sym], 1u);
-            nd++;
+    NDFL_FOR_GROUPS({
+_Pragma("unroll")
+        for (int j = 0; j < 8; j++) {
+            const uint32_t v = NDFL_BYTE(j);
+            uint32_t rep = (r1g_ >> j) & 1;
+            if (any2_) rep += ((r2g_ >> j) & 1) + ((r3g_ >> j) & 1);
+            if (rep) atomicAdd(&hl[v], rep);
+            NDFL_RUN(j, {
+                const uint32_t lead = lead_of(gpos, v);
+                const uint32_t R = pend - gpos - lead;
+                const uint32_t n258 = R / 258, m = R % 258;
+                const uint32_t nlit = lead + (m < 3 ? m : 0);
+                if (nlit) atomicAdd(&hl[v], nlit);
+                if (n258) atomicAdd(&hl[285], n258);
+                uint32_t nd = n258;
+                if (m >= 3) {
+                    uint32_t sym, ne, ex; run_sym(m, sym, ne, ex);
+                    atomicAdd(&hl[sym], 1u);
+                    nd++;
+                }
+                if (nd) atomicAdd(&hd[0], nd);
+            })
         }
-        if (nd) atomicAdd(&hd[0], nd);
     })
-#undef PF_
     if (tid == 0) {
         atomicAdd(&hl[256], 1u);                          // end of block (:131-132)
         if (a.dynamic && len_c == 0) atomicAdd(&hl[0], 1u);  // (:146-147)
@@ -742,7 +758,7 @@ __device__ __forceinline__ void deflate_chunk(const Args& a, uint32_t* obuf, PS&
         uint32_t* h = a.hist_out + (uint64_t)c * HREC;
         if (tid < HREC) {
             uint32_t v = 0;
-#pragma unroll
+_Pragma("unroll")
             for (int k = 0; k < HCOPY; k++) v += hl4[k * HSTR + tid];
             h[tid] = v;
         }
@@ -768,22 +784,29 @@ __device__ __forceinline__ void deflate_chunk(const Args& a, uint32_t* obuf, PS&
     const uint32_t d0 = ps.distCode[0];
     const uint32_t c285 = ps.litCode[285];
     uint32_t mybits = 0;
-#define PF_(x) ps.litCode[x]
-    NDFL_FOR_PIECES({
-        const uint32_t lv = pfv >> 16;
-        if (single || !a.rle) { mybits += lv; continue; }
-        const uint32_t lead = lead_of(gpos, v);
-        const uint32_t R = pend - gpos - lead;
-        const uint32_t n258 = R / 258, m = R % 258;
-        mybits += lead * lv + n258 * ((c285 >> 16) + (d0 >> 16));
-        if (m >= 3) {
-            uint32_t sym, ne, ex; run_sym(m, sym, ne, ex);
-            mybits += (ps.litCode[sym] >> 16) + ne + (d0 >> 16);
-        } else {
-            mybits += m * lv;
+    NDFL_FOR_GROUPS({
+        uint32_t pf[8];
+_Pragma("unroll")
+        for (int j = 0; j < 8; j++) pf[j] = ps.litCode[NDFL_BYTE(j)];
+_Pragma("unroll")
+        for (int j = 0; j < 8; j++) {
+            const uint32_t lv = pf[j] >> 16;
+            const uint32_t rep = ((r1g_ >> j) & 1) + ((r2g_ >> j) & 1) + ((r3g_ >> j) & 1);
+            mybits += rep * lv;
+            NDFL_RUN(j, {
+                const uint32_t lead = lead_of(gpos, v);
+                const uint32_t R = pend - gpos - lead;
+                const uint32_t n258 = R / 258, m = R % 258;
+                mybits += lead * lv + n258 * ((c285 >> 16) + (d0 >> 16));
+                if (m >= 3) {
+                    uint32_t sym, ne, ex; run_sym(m, sym, ne, ex);
+                    mybits += (ps.litCode[sym] >> 16) + ne + (d0 >> 16);
+                } else {
+                    mybits += m * lv;
+                }
+            })
         }
     })
-#undef PF_
     const uint64_t tp3a = wall_clock64();
     uint32_t tokTotal;
     const uint32_t myoff = block_excl_scan<uint32_t, NW>(mybits, ps.scan32, tokTotal);
@@ -826,26 +849,37 @@ __device__ __forceinline__ void deflate_chunk(const Args& a, uint32_t* obuf, PS&
         const uint32_t d0c = d0 & 0xFFFF, d0l = d0 >> 16;
         const uint32_t m258 = (c285 & 0xFFFF) | (d0c << (c285 >> 16));
         const uint32_t m258l = (c285 >> 16) + d0l;
-#define PF_(x) ps.litCode[x]
-        NDFL_FOR_PIECES({
-            const uint32_t lc = pfv;
-            if (single || !a.rle) { bp.put(lc & 0xFFFF, lc >> 16); continue; }
-            const uint32_t lead = lead_of(gpos, v);
-            const uint32_t R = pend - gpos - lead;
-            const uint32_t n258 = R / 258, m = R % 258;
-            if (lead) bp.put(lc & 0xFFFF, lc >> 16);
-            for (uint32_t k = 0; k < n258; k++) bp.put(m258, m258l);
-            if (m >= 3) {
-                uint32_t sym, ne, ex; run_sym(m, sym, ne, ex);
-                const uint32_t sc = ps.litCode[sym];
-                bp.put(sc & 0xFFFF, sc >> 16);
-                bp.put(ex, ne);
-                bp.put(d0c, d0l);
-            } else {
-                for (uint32_t k = 0; k < m; k++) bp.put(lc & 0xFFFF, lc >> 16);
+        NDFL_FOR_GROUPS({
+            uint32_t pf[8];
+_Pragma("unroll")
+            for (int j = 0; j < 8; j++) pf[j] = ps.litCode[NDFL_BYTE(j)];
+_Pragma("unroll")
+            for (int j = 0; j < 8; j++) {
+                const uint32_t lc = pf[j];
+                const bool r1 = (r1g_ >> j) & 1;
+                bp.put(r1 ? (lc & 0xFFFF) : 0u, r1 ? (lc >> 16) : 0u);
+                if (any2_ && ((r2g_ >> j) & 1)) {
+                    bp.put(lc & 0xFFFF, lc >> 16);
+                    if ((r3g_ >> j) & 1) bp.put(lc & 0xFFFF, lc >> 16);
+                }
+                NDFL_RUN(j, {
+                    const uint32_t lead = lead_of(gpos, v);
+                    const uint32_t R = pend - gpos - lead;
+                    const uint32_t n258 = R / 258, m = R % 258;
+                    if (lead) bp.put(lc & 0xFFFF, lc >> 16);
+                    for (uint32_t k = 0; k < n258; k++) bp.put(m258, m258l);
+                    if (m >= 3) {
+                        uint32_t sym, ne, ex; run_sym(m, sym, ne, ex);
+                        const uint32_t sc = ps.litCode[sym];
+                        bp.put(sc & 0xFFFF, sc >> 16);
+                        bp.put(ex, ne);
+                        bp.put(d0c, d0l);
+                    } else {
+                        for (uint32_t k = 0; k < m; k++) bp.put(lc & 0xFFFF, lc >> 16);
+                    }
+                })
             }
         })
-#undef PF_
         bp.flush();
     }
     __syncthreads();
