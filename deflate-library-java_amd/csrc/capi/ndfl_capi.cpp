@@ -430,7 +430,7 @@ int ndfl_deflate_chunks_lz77(ndfl_ctx* c, const uint8_t* hist, uint32_t hist_len
         const uint64_t P0 = LZ_DS + x0, P1 = LZ_DS + x1;
         if (P1 > P0) {
             const uint64_t L0 = std::max<uint64_t>(la.vstart, P0 - LZ_SEG);
-            hipLaunchKernelGGL(ndfl_lz_links_kernel, dim3((uint32_t)((P1 - L0 + LZ_SEG - 1) / LZ_SEG)), dim3(64), 0, s,
+            hipLaunchKernelGGL(ndfl_lz_links_kernel, dim3((uint32_t)((P1 - L0 + LZ_SEG - 1) / LZ_SEG)), dim3(1024), 0, s,
                                (const uint8_t*)buf, total, la.vstart, L0, P1, c->d_link.as<uint16_t>());
             HIPCHK(hipGetLastError());
             la.L0 = L0; la.p_begin = P0; la.p_end = P1;

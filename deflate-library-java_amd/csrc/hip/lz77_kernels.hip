@@ -6,7 +6,7 @@
 // (:71-84).  Only candidates whose run reaches minRun (>= 3) can be chosen, and those share the
 // 3-byte prefix, so walking every earlier position with the same 3-byte prefix nearest-first and
 // keeping strictly longer runs is the same search.  Three launches per batch:
-//   1. ndfl_lz_links_kernel   one wave per 32 KiB segment: link[q] = distance to the previous
+//   1. ndfl_lz_links_kernel   one workgroup per 32 KiB segment: link[q] = distance to the previous
 //                             position whose 3-byte prefix hashes like q's (0 if none within
 //                             32 KiB); head table in LDS, in-wave duplicates resolved by readlane.
 //   2. ndfl_lz_match_kernel   one 1024-thread workgroup per 8 KiB tile: the tile's 32 KiB window
@@ -51,61 +51,59 @@ struct LzArgs {
 // ---- 1. hash-chain links ---------------------------------------------------------------------
 // Segment s covers positions [L0 + 32K s, +32K) ∩ [.., L1).  The head table is first filled from
 // the 32 KiB before the segment (those are the only positions a link can reach), then the
-// segment's positions are linked in order, 64 at a time: lane l's predecessor is the highest lane
-// below it with the same bucket, else the head entry; the last lane of each bucket updates it.
-extern "C" __global__ void __launch_bounds__(64)
+// segment's positions are linked in order, 1024 at a time by one workgroup: every wave finds, for
+// its 64 positions, the highest lane below each with the same bucket (all 16 waves at once); then
+// the waves take turns on the head table in position order -- a lane with no predecessor in its
+// wave reads the head entry, the last lane of each bucket updates it.
+extern "C" __global__ void __launch_bounds__(1024)
 ndfl_lz_links_kernel(const uint8_t* buf, uint64_t total, uint64_t vstart, uint64_t L0, uint64_t L1, uint16_t* link) {
     __shared__ __attribute__((aligned(16))) uint16_t head[1 << LZ_HBITS];
     __shared__ __attribute__((aligned(16))) uint32_t bb[(1024 + 16) / 4];    // one 1 KiB block + lookahead
-    const int lane = threadIdx.x;
+    const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
     const uint64_t s0 = L0 + (uint64_t)blockIdx.x * LZ_SEG;
     const uint64_t s1 = min(s0 + LZ_SEG, L1);
     const uint64_t seed0 = max(vstart, s0 >= (uint64_t)LZ_SEG ? s0 - LZ_SEG : 0ull);
-    for (int k = lane; k < (1 << LZ_HBITS) / 8; k += 64) ((u32x4*)head)[k] = u32x4{~0u, ~0u, ~0u, ~0u};
+    for (int k = tid; k < (1 << LZ_HBITS) / 8; k += 1024) ((u32x4*)head)[k] = u32x4{~0u, ~0u, ~0u, ~0u};
     // bytes are staged 1 KiB at a time, the next block's loads in flight while this one is linked
     // (the staging buffer has 64 zero bytes after `total`)
     auto load16 = [&](uint64_t g) -> u32x4 {
         return g + 16 <= total + 64 ? *(const u32x4*)(buf + g) : u32x4{0u, 0u, 0u, 0u};
     };
     const uint64_t a0 = seed0 & ~15ull;
-    u32x4 nx = load16(a0 + 16 * (uint64_t)lane);
-    u32x4 nx2 = lane == 0 ? load16(a0 + 1024) : u32x4{0u, 0u, 0u, 0u};
+    u32x4 nx = tid < 65 ? load16(a0 + 16 * (uint64_t)tid) : u32x4{0u, 0u, 0u, 0u};
     for (uint64_t q0 = a0; q0 < s1; q0 += 1024) {
         __syncthreads();
-        ((u32x4*)bb)[lane] = nx;
-        if (lane == 0) ((u32x4*)bb)[64] = nx2;
+        if (tid < 65) ((u32x4*)bb)[tid] = nx;
         __syncthreads();
-        if (q0 + 1024 < s1) {
-            nx = load16(q0 + 1024 + 16 * (uint64_t)lane);
-            if (lane == 0) nx2 = load16(q0 + 2048);
-        }
-        for (int it = 0; it < 16; it++) {
-            const uint32_t r = (uint32_t)(it * 64 + lane);
-            const uint64_t q = q0 + r;
-            const bool valid = q >= seed0 && q < s1 && q + 2 < total;
-            uint32_t h = 0x10000u + (uint32_t)lane;   // distinct non-bucket for invalid lanes
-            if (valid) h = lz_hash(__builtin_amdgcn_alignbyte(bb[(r >> 2) + 1], bb[r >> 2], r & 3) & 0xFFFFFFu);
-            int prevLane = -1;
-            bool last = true;
+        if (q0 + 1024 < s1 && tid < 65) nx = load16(q0 + 1024 + 16 * (uint64_t)tid);
+        const uint32_t r = (uint32_t)tid;
+        const uint64_t q = q0 + r;
+        const bool valid = q >= seed0 && q < s1 && q + 2 < total;
+        uint32_t h = 0x10000u + (uint32_t)lane;   // distinct non-bucket for invalid lanes
+        if (valid) h = lz_hash(__builtin_amdgcn_alignbyte(bb[(r >> 2) + 1], bb[r >> 2], r & 3) & 0xFFFFFFu);
+        int prevLane = -1;
+        bool last = true;
 #pragma unroll 8
-            for (int k = 0; k < 64; k++) {
-                const uint32_t hk = __builtin_amdgcn_readlane(h, k);
-                const bool eq = hk == h;
-                if (eq && k < lane) prevLane = k;
-                if (eq && k > lane) last = false;
-            }
-            const uint32_t off = (uint32_t)(q - seed0);   // < 65536; 0xFFFF is written only by the
-            uint32_t d = 0;                               // segment's last position and never read
-            if (valid) {
-                if (prevLane >= 0) d = (uint32_t)(lane - prevLane);
-                else {
+        for (int k = 0; k < 64; k++) {
+            const uint32_t hk = __builtin_amdgcn_readlane(h, k);
+            const bool eq = hk == h;
+            if (eq && k < lane) prevLane = k;
+            if (eq && k > lane) last = false;
+        }
+        const uint32_t off = (uint32_t)(q - seed0);   // < 65536; 0xFFFF is written only by the
+        uint32_t d = 0;                               // segment's last position and never read
+        if (valid && prevLane >= 0) d = (uint32_t)(lane - prevLane);
+        for (int g = 0; g < 16; g++) {
+            if (wid == g && valid) {
+                if (prevLane < 0) {
                     const uint32_t hv = head[h];
                     if (hv != 0xFFFFu) { d = off - hv; if (d > (uint32_t)LZ_SEG) d = 0; }
                 }
+                if (last) head[h] = (uint16_t)off;   // one wave: its LDS ops stay in program order
             }
-            if (valid && last) head[h] = (uint16_t)off;   // one wave: LDS ops stay in program order
-            if (q >= s0 && q < s1) link[q - L0] = (uint16_t)d;
+            __syncthreads();
         }
+        if (q >= s0 && q < s1) link[q - L0] = (uint16_t)d;
     }
 }
 
@@ -144,6 +142,11 @@ ndfl_lz_match_kernel(LzArgs a) {
     }
     __syncthreads();
     const uint32_t minRun = a.min_run, maxRun = a.max_run;
+    // chunk and parent chunk of the tile's first position (wave-uniform); later positions of the
+    // tile step from them with 32-bit divisions (a claim runs beside other lanes' hops, so it must
+    // be cheap: no 64-bit division per position)
+    const uint64_t cs0 = LZ_DS + ((p0 - LZ_DS) / a.chunk_len) * a.chunk_len;
+    const uint64_t pps0 = LZ_DS + ((p0 - LZ_DS) / a.parent_len) * a.parent_len;
     uint32_t st_pos = 0, st_hop = 0, st_hit = 0, st_cmp = 0;
     // Each lane searches positions one hop per iteration and takes the tile's next unclaimed position
     // (LDS counter) as soon as it finishes one: chain lengths vary by orders of magnitude, so static
@@ -155,12 +158,11 @@ ndfl_lz_match_kernel(LzArgs a) {
     for (;;) {
         if (!have) {
             while (i < p1) {
-                const uint64_t x = i - LZ_DS;                  // data index
-                const uint64_t c = x / a.chunk_len;
-                const uint64_t cs = LZ_DS + c * a.chunk_len;
+                // i - cs0 < LZ_TILE + chunk_len < 2^32
+                const uint64_t cs = cs0 + (uint64_t)(((uint32_t)(i - cs0) / a.chunk_len) * a.chunk_len);
                 const uint64_t e = min(cs + a.chunk_len, a.total);
                 maxlen = (uint32_t)min((uint64_t)maxRun, e - i);
-                const uint64_t ps = LZ_DS + (x / a.parent_len) * a.parent_len;   // parent chunk start
+                const uint64_t ps = pps0 + (uint64_t)(((uint32_t)(i - pps0) / a.parent_len) * a.parent_len);
                 const uint64_t off = ps - min((uint64_t)a.hist_limit, ps - a.vstart);
                 const int64_t lo = max((int64_t)i - (int64_t)a.max_dist, (int64_t)off);
                 const int64_t hi = (int64_t)i - (int64_t)a.min_dist;
