@@ -781,8 +781,8 @@ _Pragma("unroll")
 
     const uint64_t tp3 = wall_clock64();
     // ---- 5. token bits per lane, chunk size, decoupled look-back ------------------------------
-    const uint32_t d0 = ps.distCode[0];
-    const uint32_t c285 = ps.litCode[285];
+    const uint32_t d0 = __builtin_amdgcn_readfirstlane(ps.distCode[0]);       // workgroup-uniform: SGPRs
+    const uint32_t c285 = __builtin_amdgcn_readfirstlane(ps.litCode[285]);
     uint32_t mybits = 0;
     NDFL_FOR_GROUPS({
         uint32_t pf[8];
@@ -811,8 +811,8 @@ _Pragma("unroll")
     uint32_t tokTotal;
     const uint32_t myoff = block_excl_scan<uint32_t, NW>(mybits, ps.scan32, tokTotal);
     const uint64_t tp3b = wall_clock64();
-    const uint32_t eobLen = ps.litCode[256] >> 16;
-    const uint32_t hdrBits = ps.hdrBits;
+    const uint32_t eobLen = __builtin_amdgcn_readfirstlane(ps.litCode[256] >> 16);
+    const uint32_t hdrBits = __builtin_amdgcn_readfirstlane(ps.hdrBits);
     const uint64_t S = (uint64_t)hdrBits + tokTotal + eobLen;
     // publish this chunk's size now; the look-back runs after the chunk is emitted at local bit 0,
     // so predecessors get the emit time to publish theirs
@@ -850,12 +850,15 @@ _Pragma("unroll")
         const uint32_t m258 = (c285 & 0xFFFF) | (d0c << (c285 >> 16));
         const uint32_t m258l = (c285 >> 16) + d0l;
         NDFL_FOR_GROUPS({
-            uint32_t pf[8];
+            // codes looked up 4 bytes ahead (8 would spill: the bit buffer state, the chunk's 16
+            // words and the lookups share 64 VGPRs)
+            uint32_t pf[4];
 _Pragma("unroll")
-            for (int j = 0; j < 8; j++) pf[j] = ps.litCode[NDFL_BYTE(j)];
+            for (int j = 0; j < 4; j++) pf[j] = ps.litCode[NDFL_BYTE(j)];
 _Pragma("unroll")
             for (int j = 0; j < 8; j++) {
-                const uint32_t lc = pf[j];
+                const uint32_t lc = pf[j & 3];
+                if (j < 4) pf[j] = ps.litCode[NDFL_BYTE(j + 4)];
                 const bool r1 = (r1g_ >> j) & 1;
                 bp.put(r1 ? (lc & 0xFFFF) : 0u, r1 ? (lc >> 16) : 0u);
                 if (any2_ && ((r2g_ >> j) & 1)) {
