@@ -263,6 +263,13 @@ int ndfl_deflate_chunks(ndfl_ctx* c, const uint8_t* hist, uint32_t hist_len, uin
     const bool prof = getenv("NDFL_DEFLATE_PROFILE") != nullptr;
     if (prof) { HIPCHK(hipMalloc(&a.prof, (size_t)nch * 128)); HIPCHK(hipMemsetAsync(a.prof, 0, (size_t)nch * 128, s)); }
     a.hist_out = nullptr; a.codes = nullptr; a.chunk_off = nullptr;
+    {
+        // next generation of resident split-pass workgroups: 2 per CU (1024 threads, <= 75 KB LDS)
+        static int ncu = 0;
+        if (!ncu && hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, c->device) != hipSuccess) ncu = 0;
+        const char* pe = getenv("NDFL_DEFLATE_PF");        // A/B knob: 0 turns the L2 touch off
+        a.pf_dist = (pe && atoi(pe) == 0) ? 0u : 2u * (uint32_t)ncu;
+    }
     // split pipeline by default (deflate_split.hip); NDFL_DEFLATE_FUSED=1 selects the one-kernel encoder
     const char* fenv = getenv("NDFL_DEFLATE_FUSED");      // read per call (tests switch it)
     const bool fused = fenv != nullptr && atoi(fenv) != 0;

@@ -112,6 +112,8 @@ struct Args {
     uint32_t* hist_out;       // [nchunks][HREC] histograms: literal/length [0,288), distance [288,320)
     const uint32_t* codes;    // [nchunks][CREC] code records
     const uint64_t* chunk_off;// [nchunks] global bit offset of each chunk
+    uint32_t pf_dist;         // split passes: touch chunk c + pf_dist (the next wave of resident
+                              // workgroups on this XCD) into L2 while chunk c is processed; 0: off
 };
 
 // Split pipeline record layouts.
@@ -632,6 +634,19 @@ __device__ __forceinline__ void deflate_chunk(const Args& a, uint32_t* obuf, PS&
     }
 
     const uint64_t tp1 = wall_clock64();
+    // The split passes read their chunk once, at the start, and every workgroup of a generation
+    // waits on HBM at the same time.  One byte per 128-byte line of the chunk the next generation
+    // takes on this XCD (c + pf_dist, dispatch is round-robin over the XCDs) is loaded here, after
+    // the pass's last dependent global load, and consumed at the end, so that chunk is in L2 when
+    // its workgroup starts.
+    uint32_t pfv = 0;
+    auto prefetch_next = [&]() {
+        const uint64_t cn = (uint64_t)c + a.pf_dist;
+        if (a.pf_dist && cn < a.nchunks && tid < 512) {
+            const uint64_t off = cn * a.chunk_len + (uint64_t)tid * 128;
+            if (off < a.n) pfv = a.in[off];
+        }
+    };
     // ---- 2. run pieces ------------------------------------------------------------------------
     // a block inside its parent chunk always has the parent's earlier bytes as history
     const bool has_prev0 = (cs % a.parent_len != 0) ? true : (c > 0) ? (a.hist_enabled != 0) : (a.prev_byte >= 0);
@@ -642,13 +657,17 @@ __device__ __forceinline__ void deflate_chunk(const Args& a, uint32_t* obuf, PS&
         if (!a.rle) {
             F = vcnt == 64 ? ~0ull : ((1ull << vcnt) - 1);
         } else {
+            // four bytes per step: x = word ^ (word shifted by one byte) is nonzero exactly in the
+            // bytes that differ from the byte before them; their high bits are gathered into 4 bits
+            // by one multiply (bits 0, 8, 16, 24 land on 21..24 with no carries)
 #pragma unroll
-            for (int i = 0; i < 64; i++) {
-                uint32_t b = (w[i >> 2] >> ((i & 3) * 8)) & 0xFF;
-                bool st = (i == 0 && tid == 0) || b != prev;
-                if (i < vcnt && st) F |= 1ull << i;
-                prev = b;
+            for (int k = 0; k < 16; k++) {
+                const uint32_t x = w[k] ^ ((w[k] << 8) | (k ? (w[k - 1] >> 24) : prev));
+                const uint32_t hb = ((((x & 0x7F7F7F7Fu) + 0x7F7F7F7Fu) | x) & 0x80808080u) >> 7;
+                F |= (uint64_t)(((hb * 0x00204081u) >> 21) & 0xFu) << (4 * k);
             }
+            if (tid == 0) F |= 1ull;
+            if (vcnt < 64) F &= (1ull << vcnt) - 1;
         }
     }
     const uint32_t firstStart = F ? t0 + (uint32_t)__builtin_ctzll(F) : 0xFFFFFFFFu;
@@ -723,6 +742,10 @@ __device__ __forceinline__ void deflate_chunk(const Args& a, uint32_t* obuf, PS&
     uint32_t* hl = hlit;
     uint32_t* hd = hdist;
     if (MODE == MODE_HIST) { hl = hl4 + (tid & (HCOPY - 1)) * HSTR; hd = hl + 288; }
+    if (MODE == MODE_HIST) {
+        asm volatile("" :: "v"(prev0));    // its load is waited for here, not behind the prefetch
+        prefetch_next();
+    }
     if (MODE != MODE_EMIT) {
     NDFL_FOR_GROUPS({
 _Pragma("unroll")
@@ -762,6 +785,7 @@ _Pragma("unroll")
             for (int k = 0; k < HCOPY; k++) v += hl4[k * HSTR + tid];
             h[tid] = v;
         }
+        asm volatile("" :: "v"(pfv));
         return;
     }
 
@@ -780,6 +804,7 @@ _Pragma("unroll")
     __syncthreads();
 
     const uint64_t tp3 = wall_clock64();
+    if (MODE == MODE_EMIT) prefetch_next();
     // ---- 5. token bits per lane, chunk size, decoupled look-back ------------------------------
     const uint32_t d0 = __builtin_amdgcn_readfirstlane(ps.distCode[0]);       // workgroup-uniform: SGPRs
     const uint32_t c285 = __builtin_amdgcn_readfirstlane(ps.litCode[285]);
@@ -902,6 +927,7 @@ _Pragma("unroll")
         }
     }
     (void)is_final; (void)packedLo; (void)packedHi;
+    asm volatile("" :: "v"(pfv));
 }
 
 extern "C" __global__ void __launch_bounds__(DT, 8)
