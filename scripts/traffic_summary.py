@@ -10,12 +10,15 @@ import csv
 import json
 import sys
 
-WIDE_READ = {"ndfl_deflate_chunks_kernel": True, "ndfl_deflate_hist_kernel": True, "ndfl_deflate_emit_kernel": True}
+WIDE_READ = {"ndfl_deflate_chunks_kernel": True}
 NOTES = {
     "ndfl_deflate_chunks_kernel": "16-B/lane streaming loads (x2 applied) and 16-B/lane interior stores: calibrated",
-    "ndfl_deflate_hist_kernel": "16-B/lane streaming loads (x2 applied); writes: the 1.25 KiB histogram per chunk",
-    "ndfl_deflate_emit_kernel": "16-B/lane streaming loads (x2 applied to all reads, incl. the 4-B code-record "
-                                "loads, ~1.7 KiB per chunk) and 4-B/lane coalesced interior stores",
+    "ndfl_deflate_hist_kernel": "raw: the chunk arrives partly through the previous generation's L2 touch (1-B "
+                                "loads, one per 128-B line: counted in full) and partly through 16-B/lane loads "
+                                "(counted half), so no single correction applies; raw = N (0.5 + 0.5 p) gives the "
+                                "touched share p, and the actual fetch is about N; writes: 1.25 KiB per chunk",
+    "ndfl_deflate_emit_kernel": "raw, as for hist (L2 touch + 16-B/lane loads; the 4-B code-record loads add "
+                                "~1.7 KiB per chunk); 4-B/lane coalesced interior stores",
     "ndfl_inflate_emit_wave_kernel": "reads are 16-B prefetch per chain (uncalibrated, raw); stores are 4-B per lane "
                                      "at 64 independent chain cursors: partial lines leave L2 before they fill",
 }
