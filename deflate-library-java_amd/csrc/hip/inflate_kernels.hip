@@ -353,7 +353,8 @@ ndfl_inflate_find_kernel(const uint32_t* w, uint64_t nwords, uint64_t nbits, uin
     for (uint32_t kk = 0; kk < FIND_WPT; kk++) {
     const uint64_t tt = ((uint64_t)blockIdx.x * FIND_WPT + kk) * blockDim.x + threadIdx.x;
     // input word index; the scan covers bit positions [w_lo * 32, scan_end) of the stream
-    const uint64_t t = w_lo + (tt / win_words) * period_words + tt % win_words;
+    const uint64_t t = win_words == period_words ? w_lo + tt    // every position (the default): no division
+                                                 : w_lo + (tt / win_words) * period_words + tt % win_words;
     const uint64_t p0 = t * 32;
     if (p0 < scan_end) {
         const uint32_t w0 = in.ld(t), w1 = in.ld(t + 1), w2 = in.ld(t + 2), w3 = in.ld(t + 3);
