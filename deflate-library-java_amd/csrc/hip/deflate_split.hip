@@ -92,26 +92,36 @@ __device__ void wpm_lengths(const uint32_t* hist, int n, int L, uint8_t* lens, W
     for (int it = 0; it < L; it++) {
         const uint32_t m = np + nl;
         const uint32_t* pf = S.pf[cur];
-        // item t lands at t + (# items of the other list before it): a package counts leaves with
-        // freq < f, a leaf counts packages with freq <= f.  (Measured: stepping a lane's <= 9
-        // searches together, branchy or branch-free, ran slower than this plain loop.)
-        for (uint32_t t = (uint32_t)lane; t < m; t += 64) {
-            uint32_t f, pos;
-            const bool isp = t < np;
-            if (isp) {
-                f = pf[t];
-                uint32_t lo = 0, hi = nl;
-                while (lo < hi) { const uint32_t mid = (lo + hi) >> 1; if (S.lf[mid] < f) lo = mid + 1; else hi = mid; }
-                pos = t + lo;
-            } else {
-                const uint32_t r = t - np;
-                f = S.lf[r];
-                uint32_t lo = 0, hi = np;
-                while (lo < hi) { const uint32_t mid = (lo + hi) >> 1; if (pf[mid] <= f) lo = mid + 1; else hi = mid; }
-                pos = r + lo;
+        // merged order: package i before leaf j iff pf[i] <= lf[j] (packages first on equal freq).
+        // Lane l writes merged positions [k0, k1): one merge-path search for how many packages
+        // precede k0, then a sequential merge (one dependent LDS read per output instead of one
+        // binary search per item).
+        {
+            const uint32_t per = (m + 63) >> 6;
+            const uint32_t k0 = min(m, (uint32_t)lane * per), k1 = min(m, k0 + per);
+            uint32_t lo = k0 > nl ? k0 - nl : 0u, hi = min(k0, np);
+            while (lo < hi) {
+                const uint32_t mid = (lo + hi) >> 1;
+                if (pf[mid] <= S.lf[k0 - mid - 1]) lo = mid + 1; else hi = mid;
             }
-            S.mf[pos] = f;
-            if (isp) atomicOr(&S.mpk[it * 20 + (pos >> 5)], 1u << (pos & 31));
+            uint32_t i = lo, j = k0 - lo;
+            uint32_t pv = i < np ? pf[i] : 0u, lv = j < nl ? S.lf[j] : 0u;
+            const uint32_t wb = k0 & ~31u;
+            uint64_t bits = 0;
+            for (uint32_t pos = k0; pos < k1; pos++) {
+                const bool takeP = i < np && (j >= nl || pv <= lv);
+                S.mf[pos] = takeP ? pv : lv;
+                if (takeP) {
+                    bits |= 1ull << (pos - wb);
+                    i++;
+                    pv = i < np ? pf[i] : 0u;
+                } else {
+                    j++;
+                    lv = j < nl ? S.lf[j] : 0u;
+                }
+            }
+            if ((uint32_t)bits) atomicOr(&S.mpk[it * 20 + (wb >> 5)], (uint32_t)bits);
+            if ((uint32_t)(bits >> 32)) atomicOr(&S.mpk[it * 20 + (wb >> 5) + 1], (uint32_t)(bits >> 32));
         }
         __syncthreads();
         const uint32_t np2 = m >> 1;
