@@ -16,7 +16,13 @@ N > 1   rank r owns chunks [r*K, (r+1)*K) of ONE global stream.  Ranks exchange 
         BASELINE.json defines it, 4 GiB in total split over the ranks, and the step also gathers the
         global stream onto rank 0 (RCCL point-to-point into its byte offsets, shared bytes ORed on
         device; --gather adds that to weak scaling too).
-Run: python bench.py [--gpus N --steps K --warmup W]; multi-GPU via torch.distributed.run.
+Run: python bench.py [--gpus N --steps K --warmup W].  With --gpus N > 1 and no WORLD_SIZE in the
+environment, bench.py starts N ranks itself (torch.distributed.run on 127.0.0.1, before anything
+touches the GPU) and exits with their status; under torch.distributed.run it is one rank.
+N > 1 gathers the global stream onto rank 0 in every step by default (north_star: "RCCL gather over
+xGMI to reassemble the output stream"; --no-gather leaves it out).
+bit_exact: every rank compares its WHOLE shard's stream with the oracle's (chunk-parallel on the
+host, outside the timed region), and the flag is the AND over ranks.
 """
 import argparse
 import ctypes
@@ -47,14 +53,22 @@ def main():
     ap.add_argument("--backend", default="nccl", help="nccl (= RCCL over xGMI); gloo only to rehearse N>1 on one GPU")
     ap.add_argument("--scaling", choices=["weak", "strong"], default="weak",
                     help="weak: --size bytes per rank; strong: --size bytes in total (config 4), with the gather")
-    ap.add_argument("--gather", action="store_true", help="gather the global stream onto rank 0 in every step")
+    ap.add_argument("--gather", action="store_true", help="(default for N > 1) gather the global stream onto rank 0")
+    ap.add_argument("--no-gather", action="store_true", help="N > 1: leave the gather to rank 0 out of the step")
+    ap.add_argument("--verify-threads", type=int, default=0, help="host threads of the full-stream oracle check "
+                    "(0: min(16, cpus / ranks))")
     args = ap.parse_args()
+
+    if args.gpus > 1 and "WORLD_SIZE" not in os.environ:
+        sys.exit(launch_ranks(args.gpus))
 
     import torch
     import ndfl
     import corpus
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
+    if world != args.gpus:
+        raise SystemExit(f"bench.py: WORLD_SIZE={world} but --gpus {args.gpus}")
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
     local = local % max(1, torch.cuda.device_count())
@@ -67,7 +81,7 @@ def main():
         else:
             dist.init_process_group(args.backend)
 
-    gather = world > 1 and (args.gather or args.scaling == "strong")
+    gather = world > 1 and not args.no_gather
     if args.scaling == "strong" and world > 1:
         # one global corpus, rank r takes its 64 KiB-aligned share (the last rank the remainder)
         per = (args.size // world) // 65536 * 65536
@@ -113,11 +127,12 @@ def main():
             # one global stream: history halo + seam index + realignment, then range decode with the
             # window chain (ndfl/parallel.py)
             part = P.deflate_shard(codec, dist, torch, data, rank, world, work=comp, out=shifted)
+            state["hist"] = part.hist
             t_c = ctx.timings()["deflate"]
             endbits = part.nbits
             cbytes = (endbits + 7) // 8
             if gather:
-                state["stream"] = P.gather_stream(codec, dist, torch, part, rank, world)
+                state["stream"] = P.gather_stream(codec, dist, torch, part, rank, world, out=state.get("stream"))
             r, olen, dl = P.inflate_shard(codec, dist, torch, part, dec, rank, world)
             state["dict_len"] = dl
         if r != 0:
@@ -177,14 +192,25 @@ def main():
     achieved = alg / (kms / 1e3)
     traffic, traffic_src = pmc_traffic(dom, n)
 
+    # bit-exactness of the whole shard: `comp` holds this rank's stream at bit 0 (the single-GPU
+    # stream, or the shard before its realignment), compared with the oracle's encoding of the same
+    # chunks with the same history and final flag
+    exact = None
+    if not args.no_cpu:
+        threads = args.verify_threads or max(1, min(16, (os.cpu_count() or 1) // world))
+        hist = state.get("hist")
+        exact = verify_stream(data, None if hist is None else hist.cpu().numpy().tobytes(), rank == world - 1,
+                              comp, state["endbits"], threads)
+        if dist is not None:
+            f = torch.tensor([1 if exact["bit_exact"] else 0], dtype=torch.int64,
+                             device="cpu" if args.backend == "gloo" else "cuda")
+            dist.all_reduce(f, op=dist.ReduceOp.MIN)
+            exact["all_ranks"] = bool(f.item())
     cpu = None
     if rank == 0 and not args.no_cpu:
-        # rank 0's shard starts the global stream: its first bits are compared with the oracle's
-        # (on the gathered stream when there is one, else on rank 0's own part)
-        gstream = comp if world == 1 else state.get("stream")
-        if gstream is None and world > 1:
-            gstream = shifted               # rank 0's part sits at bit 0 of its buffer
-        cpu = cpu_baseline(data, args.cpu_sample, gstream)
+        cpu = cpu_baseline(data, args.cpu_sample)
+        cpu["bit_exact"] = exact["all_ranks"] if world > 1 else exact["bit_exact"]
+        cpu["verify"] = exact
 
     if rank == 0:
         line = {
@@ -223,6 +249,20 @@ def main():
         print(json.dumps(line), flush=True)
     if dist is not None:
         dist.destroy_process_group()
+
+
+def launch_ranks(n):
+    """bench.py --gpus N without a launcher: run N ranks under torch.distributed.run (one process
+    per GPU, rendezvous on 127.0.0.1) as a child process and return its exit status.  Nothing here
+    touches the GPU, so the ranks are the only processes that do."""
+    import socket
+    import subprocess
+    with socket.socket() as so:
+        so.bind(("127.0.0.1", 0))
+        port = so.getsockname()[1]
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", f"--nproc-per-node={n}",
+           "--master-addr", "127.0.0.1", "--master-port", str(port), os.path.abspath(__file__)] + sys.argv[1:]
+    return subprocess.call(cmd)
 
 
 def pmc_traffic(kernel, n):
@@ -264,14 +304,58 @@ def _append_final_empty_block(comp, nbits):
     return bytes(b[:(nbits + 10 + 7) // 8])
 
 
-def cpu_baseline(data_dev, sample_bytes, gpu_comp=None):
+def verify_stream(data_dev, hist, final, comp_dev, nbits, threads):
+    """Whole-stream bit-exactness: the oracle (C restatement of the reference encoder) compresses
+    the shard chunk-parallel -- `threads` pieces of whole 64 KiB chunks, each with its own 32 KiB of
+    raw history, as the reference's blocks depend only on raw input -- and every
+    piece's bits are compared with the GPU stream at that piece's bit offset.  The GPU stream's
+    SHA-256 and bit count are reported beside the flag."""
+    import hashlib
+    import numpy as np
+    import oracle_lib as O
+    from concurrent.futures import ThreadPoolExecutor
+    t0 = time.perf_counter()
+    n = data_dev.numel()
+    host = data_dev.cpu().numpy().tobytes()
+    nb = (nbits + 7) // 8
+    g = np.frombuffer(comp_dev[:nb + 1].cpu().numpy().tobytes(), dtype=np.uint8)
+    nch = max(1, -(-n // 65536))
+    per = -(-nch // threads)
+    pieces = []
+    for k in range(0, nch, per):
+        a, b = k * 65536, min(n, (k + per) * 65536)
+        h = (hist or b"")[-32768:] if a == 0 else host[max(0, a - 32768):a]
+        pieces.append((h, a, b, final and b == n))
+    with ThreadPoolExecutor(threads) as ex:
+        outs = list(ex.map(lambda p: O.deflate_chunks(p[0], host[p[1]:p[2]], final=p[3]), pieces))
+    t1 = time.perf_counter()
+    ok = sum(o[1] for o in outs) == nbits
+    off = 0
+    for pb, pbits in outs:
+        if not ok:
+            break
+        s, q = off % 8, off // 8
+        m = (pbits + 7) // 8
+        seg = g[q:q + m + 1].astype(np.uint16)
+        if len(seg) < m + 1:
+            seg = np.concatenate([seg, np.zeros(m + 1 - len(seg), np.uint16)])
+        x = ((seg[:-1] >> s) | (seg[1:] << (8 - s))).astype(np.uint8)
+        if pbits % 8:
+            x[-1] &= (1 << (pbits % 8)) - 1
+        ok = x.tobytes() == pb[:m]
+        off += pbits
+    sha = hashlib.sha256(g[:nb].tobytes()).hexdigest()
+    return {"bit_exact": bool(ok), "bits_compared": int(nbits), "bytes_in": n, "pieces": len(pieces),
+            "threads": threads, "oracle_s": round(t1 - t0, 2), "total_s": round(time.perf_counter() - t0, 2),
+            "sha256": sha}
+
+
+def cpu_baseline(data_dev, sample_bytes):
     """The oracle (C restatement of the reference algorithm) on a bounded sample of the same
     workload: compress the first `sample_bytes` of the corpus as the first chunks of the stream
     (non-final, exactly what the GPU wrote for them), decompress that (closed by an empty final
-    block); same metric.  1 thread; beside it the compress leg chunk-parallel on all the box's cores
-    (threads over 64 KiB-aligned pieces, each with its 32 KiB history).  The GPU stream's first
-    bits are compared with the oracle's: `bit_exact`."""
-    import hashlib
+    block); same metric.  1 thread; beside it the compress leg chunk-parallel on 16 host threads
+    (threads over 64 KiB-aligned pieces, each with its 32 KiB history)."""
     import oracle_lib as O
     from concurrent.futures import ThreadPoolExecutor
     m = min(sample_bytes, data_dev.numel())
@@ -284,12 +368,6 @@ def cpu_baseline(data_dev, sample_bytes, gpu_comp=None):
     reason, out, bits = O.inflate(stream, out_cap=m + 64)
     t2 = time.perf_counter()
     assert reason is None and out == host and bits == nbits + 10
-    exact = None
-    if gpu_comp is not None:
-        nb = nbits // 8
-        g = gpu_comp[:nb + 1].cpu().numpy().tobytes()
-        tail_mask = (1 << (nbits % 8)) - 1
-        exact = g[:nb] == comp[:nb] and (g[nb] & tail_mask) == (comp[nb] & tail_mask if nbits % 8 else 0)
     cores = max(1, min(16, os.cpu_count() or 1))          # the GPU box's CPU share is 16
     step = max(65536, (m // cores) // 65536 * 65536)
     pieces = [(max(0, o - 32768), o, min(m, o + step)) for o in range(0, m, step)]
@@ -305,9 +383,7 @@ def cpu_baseline(data_dev, sample_bytes, gpu_comp=None):
             "all_cores": {"cores": cores, "compress_MiBps": round(m / (tp1 - tp0) / MIB, 2),
                           "note": "chunk-parallel oracle compress (threads over 64 KiB-aligned pieces with their "
                                   "32 KiB history); a single DEFLATE stream decodes serially on the CPU"},
-            "host": {"nproc": os.cpu_count(), "cpu_model": _cpu_model()},
-            "bit_exact": exact, "bits_compared": nbits,
-            "sha256_prefix": hashlib.sha256(comp[:nbits // 8]).hexdigest()}
+            "host": {"nproc": os.cpu_count(), "cpu_model": _cpu_model()}}
 
 
 if __name__ == "__main__":

@@ -63,7 +63,8 @@ struct ndfl_ctx {
     int device = 0;
     hipStream_t own = nullptr;
     hipStream_t stream = nullptr;
-    hipEvent_t ev0 = nullptr, ev1 = nullptr;
+    bool user_stream = false;       // ndfl_ctx_set_stream named the caller's stream
+    hipEvent_t ev0 = nullptr, ev1 = nullptr, ev_order = nullptr;
     double last_ms = 0;
     double deflate_ms = 0;
     DevBuf d_in, d_out, d_status, d_ticket, d_edge_w, d_edge_v, d_crc, d_crc1, d_tabs, d_hostio;
@@ -77,6 +78,21 @@ struct ndfl_ctx {
 };
 
 #define HIPCHK(x) do { hipError_t _e = (x); if (_e != hipSuccess) return NDFL_E_DEVICE; } while (0)
+
+// The ordering contract of include/ndfl.h: unless the caller named its stream (ndfl_ctx_set_stream),
+// a call's device work starts only after everything queued before the call on the device's default
+// stream -- e.g. the torch kernel that produced an NDFL_IN_DEVICE buffer, or the torch kernel still
+// using a block the caching allocator has just handed out again as an NDFL_OUT_DEVICE buffer.  (The
+// context's own stream is also a blocking stream, which the null stream orders implicitly; the
+// event makes the wait explicit.)  Every call synchronizes its stream before returning, so results
+// are complete when the call returns.
+static hipStream_t ordered_stream(ndfl_ctx* c) {
+    if (!c->user_stream) {
+        hipEventRecord(c->ev_order, nullptr);
+        hipStreamWaitEvent(c->stream, c->ev_order, 0);
+    }
+    return c->stream;
+}
 
 // Raw CRC of `len` bytes from the raw CRCs of its consecutive parts of `part_len` bytes into *out.
 static hipError_t launch_crc_combine(ndfl_ctx* c, hipStream_t s, const uint32_t* parts, uint32_t nparts,
@@ -125,10 +141,11 @@ int ndfl_ctx_create(ndfl_ctx** out, int device, uint32_t flags) {
     init_host_tables();
     ndfl_ctx* c = new ndfl_ctx();
     c->device = device;
-    if (hipStreamCreateWithFlags(&c->own, hipStreamNonBlocking) != hipSuccess) { delete c; return NDFL_E_DEVICE; }
+    if (hipStreamCreateWithFlags(&c->own, hipStreamDefault) != hipSuccess) { delete c; return NDFL_E_DEVICE; }
     c->stream = c->own;
     hipEventCreate(&c->ev0);
     hipEventCreate(&c->ev1);
+    if (hipEventCreateWithFlags(&c->ev_order, hipEventDisableTiming) != hipSuccess) { delete c; return NDFL_E_DEVICE; }
     if (c->d_tabs.ensure(sizeof(host_crc_tab) + sizeof(host_crc_x) + sizeof(host_crc_p2)) != hipSuccess) { delete c; return NDFL_E_DEVICE; }
     hipMemcpy(c->d_tabs.p, host_crc_tab, sizeof(host_crc_tab), hipMemcpyHostToDevice);
     hipMemcpy((char*)c->d_tabs.p + sizeof(host_crc_tab), host_crc_x, sizeof(host_crc_x), hipMemcpyHostToDevice);
@@ -152,6 +169,7 @@ int ndfl_ctx_destroy(ndfl_ctx* c) {
     if (c->h_pinned) hipHostFree(c->h_pinned);
     if (c->ev0) hipEventDestroy(c->ev0);
     if (c->ev1) hipEventDestroy(c->ev1);
+    if (c->ev_order) hipEventDestroy(c->ev_order);
     if (c->own) hipStreamDestroy(c->own);
     delete c;
     return NDFL_OK;
@@ -160,6 +178,7 @@ int ndfl_ctx_destroy(ndfl_ctx* c) {
 int ndfl_ctx_set_stream(ndfl_ctx* c, void* s) {
     if (!c) return NDFL_E_ARG;
     c->stream = s ? (hipStream_t)s : c->own;
+    c->user_stream = s != nullptr;
     return NDFL_OK;
 }
 
@@ -213,7 +232,7 @@ int ndfl_deflate_chunks(ndfl_ctx* c, const uint8_t* hist, uint32_t hist_len, uin
     const uint64_t nch64 = final_flag ? (len == 0 ? 1 : (len + chunk_len - 1) / chunk_len) : len / chunk_len;
     if (nch64 > 0xFFFFFFFFull) return NDFL_E_UNSUPPORTED;
     const uint32_t nch = (uint32_t)nch64;
-    hipStream_t s = c->stream;
+    hipStream_t s = ordered_stream(c);
 
     // input
     const uint8_t* d_data = data;
@@ -382,7 +401,7 @@ int ndfl_deflate_chunks_lz77(ndfl_ctx* c, const uint8_t* hist, uint32_t hist_len
     const uint64_t nch64 = final_flag ? (len == 0 ? 1 : (len + chunk_len - 1) / chunk_len) : len / chunk_len;
     if (nch64 > 0xFFFFFFFFull) return NDFL_E_UNSUPPORTED;
     const uint32_t nch = (uint32_t)nch64;
-    hipStream_t s = c->stream;
+    hipStream_t s = ordered_stream(c);
 
     // staging buffer: data at LZ_DS, the history right before it
     const uint64_t total = LZ_DS + len;
@@ -513,7 +532,7 @@ int ndfl_deflate_chunks_multi(ndfl_ctx* c, const uint8_t* hist, uint32_t hist_le
             return NDFL_E_ARG;
     }
     HIPCHK(hipSetDevice(c->device));
-    hipStream_t s = c->stream;
+    hipStream_t s = ordered_stream(c);
     const uint64_t nch64 = final_flag ? (len == 0 ? 1 : (len + chunk_len - 1) / chunk_len) : len / chunk_len;
     if (nch64 > 0xFFFFFFFFull) return NDFL_E_UNSUPPORTED;
     const uint32_t nch = (uint32_t)nch64;
@@ -651,7 +670,7 @@ int ndfl_deflate_chunks_binsplit(ndfl_ctx* c, const uint8_t* hist, uint32_t hist
             return NDFL_E_ARG;
     }
     HIPCHK(hipSetDevice(c->device));
-    hipStream_t s = c->stream;
+    hipStream_t s = ordered_stream(c);
     const uint32_t M = (uint32_t)min_block_len;
     // device copy [hist | data]
     HIPCHK(c->d_mdata.ensure(len + hist_len + 16));
@@ -863,7 +882,7 @@ int ndfl_crc32(ndfl_ctx* c, uint32_t* crc_inout, const uint8_t* data, uint64_t l
     if (!c || !crc_inout || (!data && len)) return NDFL_E_ARG;
     if (len == 0) return NDFL_OK;
     HIPCHK(hipSetDevice(c->device));
-    hipStream_t s = c->stream;
+    hipStream_t s = ordered_stream(c);
     const uint8_t* d = data;
     if (!(flags & NDFL_IN_DEVICE)) {
         HIPCHK(c->d_in.ensure(len));
@@ -896,7 +915,7 @@ int ndfl_adler32(ndfl_ctx* c, uint32_t* adler_inout, const uint8_t* data, uint64
     if (!c || !adler_inout || (!data && len)) return NDFL_E_ARG;
     if (len == 0) return NDFL_OK;
     HIPCHK(hipSetDevice(c->device));
-    hipStream_t s = c->stream;
+    hipStream_t s = ordered_stream(c);
     const uint8_t* d = data;
     if (!(flags & NDFL_IN_DEVICE)) {
         HIPCHK(c->d_in.ensure(len));
@@ -929,7 +948,7 @@ int ndfl_inflate(ndfl_ctx* c, const uint8_t* in, uint64_t in_len, uint8_t* out, 
                  uint64_t* out_len, uint64_t* consumed_bits, uint32_t flags) {
     if (!c || !out_len || !consumed_bits || (!in && in_len)) return NDFL_E_ARG;
     HIPCHK(hipSetDevice(c->device));
-    return inflate_run(c->inf, c->stream, in, in_len, 0, inf::NONE, out, 0, out_cap, out_len, consumed_bits,
+    return inflate_run(c->inf, ordered_stream(c), in, in_len, 0, inf::NONE, out, 0, out_cap, out_len, consumed_bits,
                        flags, false, &c->last_ms);
 }
 
@@ -943,7 +962,7 @@ int ndfl_inflate_range(ndfl_ctx* c, const uint8_t* in, uint64_t in_len, uint64_t
     if (deferred && !(flags & NDFL_OUT_DEVICE)) return NDFL_E_ARG;
     if (partial && (deferred || end_bit != UINT64_MAX)) return NDFL_E_ARG;
     HIPCHK(hipSetDevice(c->device));
-    return inflate_run(c->inf, c->stream, in, in_len, start_bit, end_bit, out, dict_len, out_cap, out_len,
+    return inflate_run(c->inf, ordered_stream(c), in, in_len, start_bit, end_bit, out, dict_len, out_cap, out_len,
                        consumed_bits, flags, deferred, &c->last_ms, partial);
 }
 
@@ -951,13 +970,13 @@ int ndfl_inflate_sync(ndfl_ctx* c, const uint8_t* in, uint64_t in_len, uint64_t 
                       uint64_t* sync_bit, uint32_t flags) {
     if (!c || !sync_bit || (!in && in_len) || from_bit > in_len * 8) return NDFL_E_ARG;
     HIPCHK(hipSetDevice(c->device));
-    return inflate_sync(c->inf, c->stream, in, in_len, from_bit, window_bits, flags, sync_bit, &c->last_ms);
+    return inflate_sync(c->inf, ordered_stream(c), in, in_len, from_bit, window_bits, flags, sync_bit, &c->last_ms);
 }
 
 int ndfl_inflate_resolve(ndfl_ctx* c, uint64_t* n_reemitted) {
     if (!c || !n_reemitted) return NDFL_E_ARG;
     HIPCHK(hipSetDevice(c->device));
-    return inflate_resolve(c->inf, c->stream, n_reemitted);
+    return inflate_resolve(c->inf, ordered_stream(c), n_reemitted);
 }
 
 int ndfl_bits_shift(ndfl_ctx* c, const uint8_t* in, uint64_t nbits, uint32_t shift, uint8_t* out, uint64_t out_cap,
@@ -971,7 +990,7 @@ int ndfl_bits_shift(ndfl_ctx* c, const uint8_t* in, uint64_t nbits, uint32_t shi
     if (nout == 0) return NDFL_OK;
     HIPCHK(hipSetDevice(c->device));
     const uint64_t nthr = (nout + 3) / 4;
-    hipLaunchKernelGGL(ndfl_bits_shift_kernel, dim3((uint32_t)((nthr + 255) / 256)), dim3(256), 0, c->stream, in,
+    hipLaunchKernelGGL(ndfl_bits_shift_kernel, dim3((uint32_t)((nthr + 255) / 256)), dim3(256), 0, ordered_stream(c), in,
                        nbits, shift, out, nout);
     HIPCHK(hipGetLastError());
     HIPCHK(hipStreamSynchronize(c->stream));

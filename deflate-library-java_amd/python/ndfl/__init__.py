@@ -15,6 +15,7 @@ kernels; this module only buffers bytes, writes container headers and raises exc
 import ctypes
 import enum
 import io
+import sys
 
 from . import _lib
 from ._lib import IN_DEVICE, OUT_DEVICE, DICT_DEFERRED, IN_PADDED, IN_PAD_BYTES, IN_PARTIAL, NEED_INPUT, NO_END, STRATEGIES, NdflError, check, load, reason_name
@@ -200,7 +201,13 @@ def _ptr(obj):
 
 
 class Context:
-    """One device context (HIP stream + device scratch).  Not reentrant."""
+    """One device context (HIP stream + device scratch).  Not reentrant.
+
+    Stream ordering: unless set_stream() named a stream, every call that touches device memory
+    runs on torch's current stream of this device when torch has initialised the GPU (so a
+    tensor a torch kernel is still producing, or a block the caching allocator reuses, is ordered
+    like any torch op), else after the device's default stream (the C ABI's own rule,
+    include/ndfl.h)."""
 
     def __init__(self, device=0):
         L = load()
@@ -208,6 +215,20 @@ class Context:
         check(L.ndfl_ctx_create(ctypes.byref(h), device, 0), "ndfl_ctx_create")
         self._h = h
         self.device = device
+        self._explicit_stream = False
+        self._bound = None
+
+    def _order(self):
+        """Bind torch's current stream (see the class docstring) before a device call."""
+        if self._explicit_stream:
+            return
+        torch = sys.modules.get("torch")
+        if torch is None or not torch.cuda.is_initialized():
+            return
+        h = torch.cuda.current_stream(self.device).cuda_stream
+        if h != self._bound:
+            check(load().ndfl_ctx_set_stream(self._h, ctypes.c_void_p(h)))
+            self._bound = h
 
     def close(self):
         if getattr(self, "_h", None):
@@ -221,7 +242,10 @@ class Context:
             pass
 
     def set_stream(self, stream_handle):
+        """Run this context's calls on the caller's HIP stream (None / 0: the default rule)."""
         check(load().ndfl_ctx_set_stream(self._h, ctypes.c_void_p(stream_handle)))
+        self._explicit_stream = bool(stream_handle)
+        self._bound = stream_handle
 
     def last_kernel_ms(self):
         return load().ndfl_ctx_last_kernel_ms(self._h)
@@ -238,6 +262,7 @@ class Context:
     def deflate_chunks_raw(self, hist_addr, hist_len, hist_limit, data_addr, n, chunk_len, strategy, final,
                            start_bitpos, out_addr, out_cap, flags, crc=None):
         L = load()
+        self._order()
         endbits = ctypes.c_uint64(0)
         crcv = ctypes.c_uint32(crc if crc is not None else 0)
         crcp = ctypes.byref(crcv) if crc is not None else None
@@ -282,6 +307,7 @@ class Context:
     def inflate_raw(self, in_addr, in_len, out_addr, out_cap, flags):
         """Returns (code, out_len, consumed_bits); code = 0 / reason+1 / <0 error."""
         L = load()
+        self._order()
         olen = ctypes.c_uint64(0)
         bits = ctypes.c_uint64(0)
         r = L.ndfl_inflate(self._h, in_addr, in_len, out_addr, out_cap, ctypes.byref(olen), ctypes.byref(bits),
@@ -307,6 +333,7 @@ class Context:
         """ndfl_inflate_range: decode bits [start_bit, end_bit) into out_addr + dict_len, with the
         dict_len bytes at out_addr as the window.  Returns (code, out_len, consumed_bits)."""
         L = load()
+        self._order()
         olen = ctypes.c_uint64(0)
         bits = ctypes.c_uint64(0)
         r = L.ndfl_inflate_range(self._h, in_addr, in_len, start_bit, NO_END if end_bit is None else end_bit,
@@ -315,6 +342,7 @@ class Context:
 
     def inflate_sync_raw(self, in_addr, in_len, from_bit, window_bits, flags):
         """ndfl_inflate_sync: first confirmed block boundary at or past from_bit (None: none)."""
+        self._order()
         v = ctypes.c_uint64(0)
         check(load().ndfl_inflate_sync(self._h, in_addr, in_len, from_bit, window_bits, ctypes.byref(v), flags),
               "ndfl_inflate_sync")
@@ -322,16 +350,19 @@ class Context:
 
     def inflate_resolve(self):
         """Finish a DICT_DEFERRED range decode once the window is written; returns re-emitted chains."""
+        self._order()
         n = ctypes.c_uint64(0)
         check(load().ndfl_inflate_resolve(self._h, ctypes.byref(n)), "ndfl_inflate_resolve")
         return n.value
 
     def bits_shift_raw(self, in_addr, nbits, shift, out_addr, out_cap):
         """ndfl_bits_shift on device buffers: in's first nbits bits placed at bit `shift` of out."""
+        self._order()
         check(load().ndfl_bits_shift(self._h, in_addr, nbits, shift, out_addr, out_cap, IN_DEVICE | OUT_DEVICE),
               "ndfl_bits_shift")
 
     def crc32(self, data, crc=0, flags=0):
+        self._order()
         addr, keep = _ptr(data)
         n = data.numel() * data.element_size() if hasattr(data, "numel") else len(data)
         v = ctypes.c_uint32(crc)
@@ -340,6 +371,7 @@ class Context:
 
 
     def adler32(self, data, adler=1, flags=0):
+        self._order()
         addr, keep = _ptr(data)
         n = data.numel() * data.element_size() if hasattr(data, "numel") else len(data)
         v = ctypes.c_uint32(adler)

@@ -37,6 +37,7 @@ class Part:
     shift: int                  # global bit offset mod 8
     bit_offsets: list = field(default_factory=list)    # seam index: global bit offset per rank (+ total)
     byte_offsets: list = field(default_factory=list)   # uncompressed byte offset per rank (+ total)
+    hist: object = None         # the raw bytes before the shard the encoder used as history
 
     @property
     def nbytes(self):
@@ -165,7 +166,7 @@ def deflate_shard(codec, dist, torch, shard, rank, world, *, strategy="RLE_DYNAM
     shift = bit_offsets[rank] % 8
     out = out if out is not None else codec.empty(cap + 1)
     codec.bits_shift(work, nbits, shift, out)
-    return Part(out, nbits, shift, bit_offsets, byte_offsets)
+    return Part(out, nbits, shift, bit_offsets, byte_offsets, hist if prev_h else None)
 
 
 def inflate_shard(codec, dist, torch, part, out, rank, world):
@@ -263,20 +264,29 @@ def inflate_split(codec, dist, torch, stream, in_len, out, rank, world):
     return first, olen, dict_len, offs[rank]
 
 
-def gather_stream(codec, dist, torch, part, rank, world, root=0):
+def gather_stream(codec, dist, torch, part, rank, world, root=0, out=None):
     """Reassemble the global stream on `root` (SURVEY §8e compress step 4): every rank sends its
     realigned part -- the first byte (shared with the previous shard when the global bit offset is
     not byte-aligned) and the body -- and the root receives each body straight into its byte offset
     of the output buffer (point to point over RCCL/xGMI; ncclGather needs equal counts), then ORs the
     first bytes in: BitOut's byte packing (D/DeflaterOutputStream.java:147-156) across GPUs, on
-    device.  Returns the stream tensor (bytes ceil(total bits / 8)) on the root, None elsewhere."""
+    device.  Returns the stream tensor (bytes ceil(total bits / 8)) on the root, None elsewhere.
+    `out`: an optional preallocated root buffer of at least that many bytes (its old contents do not
+    matter: only the bytes every part's first byte is ORed into are cleared)."""
     offs = part.bit_offsets
     B = [o // 8 for o in offs[:-1]]
     nb = [(offs[r] % 8 + offs[r + 1] - offs[r] + 7) // 8 for r in range(world)]
     total = (offs[-1] + 7) // 8
     staged = _staged(dist, part.buf)
     if rank == root:
-        out = torch.zeros(max(1, total), dtype=torch.uint8, device=codec.device)
+        if out is None or out.numel() < max(1, total):
+            out = torch.empty(max(1, total), dtype=torch.uint8, device=codec.device)
+        # every byte is either inside some part's body or a part's first byte: only the first bytes
+        # need a defined value before the OR (a part's last byte, shared with the next part's first,
+        # arrives with the body)
+        firsts_at = [B[r] for r in range(world) if nb[r]]
+        if firsts_at:
+            out[torch.tensor(firsts_at, dtype=torch.int64, device=codec.device)] = 0
         firsts = torch.zeros(world, dtype=torch.uint8, device=codec.device)
         ops = []
         for r in range(world):

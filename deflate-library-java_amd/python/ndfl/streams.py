@@ -245,16 +245,26 @@ class InflaterInputStream:
         self._on_batch = None         # container hook: called with every decoded batch (CRC / Adler)
 
     def _read_more(self, want):
+        """Read until `want` bytes are buffered or the stream ends -- or until a read returns fewer
+        bytes than asked for (a pipe or socket with nothing more available yet): then what is
+        buffered is decoded first, as Open decodes from whatever its fill returned
+        (D/decomp/Open.java:181-192), so a peer that waits for our output is not deadlocked."""
+        rd = getattr(self._in, "read1", None) or self._in.read
         try:
             while len(self._ibuf) < want and not self._eof:
-                b = self._in.read(want - len(self._ibuf))
+                ask = want - len(self._ibuf)
+                b = rd(ask)
                 if not b:
                     self._eof = True
                 else:
                     self._ibuf += b
+                    if len(b) < ask:
+                        break
         except OSError as e:
             self._sticky = e
             raise
+
+    MAX_BATCH_OUT = 1 << 30       # output bytes per decoded batch before the input is cut shorter
 
     def _fill(self):
         """Decode the next batch into self._buf (empty only at end of stream or on an error)."""
@@ -262,20 +272,44 @@ class InflaterInputStream:
         want = self._batch
         while True:
             self._read_more(want)
-            flags = 0 if self._eof else _lib.IN_PARTIAL
-            n = len(self._ibuf)
-            src = ctypes.create_string_buffer(bytes(self._ibuf), max(1, n))
+            n_all = len(self._ibuf)
+            n = n_all
             wl = len(self._window)
-            cap = wl + 4 * n + 65536
             while True:
-                out = ctypes.create_string_buffer(self._window, max(1, cap))
-                r, olen, bits = self._ctx.inflate_range_raw(ctypes.addressof(src), n, self._bit, None,
-                                                            ctypes.addressof(out), wl, cap, flags)
+                # a prefix of the buffered input (the whole of it unless its output would exceed
+                # MAX_BATCH_OUT): IN_PARTIAL unless it is all of a finished stream
+                flags = 0 if (self._eof and n == n_all) else _lib.IN_PARTIAL
+                src = ctypes.create_string_buffer(bytes(self._ibuf[:n]), max(1, n))
+                room = 4 * n + 65536                      # bytes after the window (out_cap)
+                while True:
+                    out = ctypes.create_string_buffer(self._window, max(1, wl + room))
+                    r, olen, bits = self._ctx.inflate_range_raw(ctypes.addressof(src), n, self._bit, None,
+                                                                ctypes.addressof(out), wl, room, flags)
+                    if r == _lib.E_CAPACITY and (olen <= self.MAX_BATCH_OUT or n <= 1):
+                        room = olen + 16
+                        continue
+                    break
                 if r == _lib.E_CAPACITY:
-                    cap = wl + olen + 16
+                    n = max(1, n // 2)                    # too much output for one batch: less input
                     continue
+                if r == _lib.NEED_INPUT and olen == 0 and bits == self._bit and n < n_all:
+                    # the shorter prefix completes no block: take the whole output of the full input
+                    n = n_all
+                    flags = 0 if self._eof else _lib.IN_PARTIAL
+                    src = ctypes.create_string_buffer(bytes(self._ibuf), max(1, n))
+                    room = 4 * n + 65536
+                    while True:
+                        out = ctypes.create_string_buffer(self._window, max(1, wl + room))
+                        r, olen, bits = self._ctx.inflate_range_raw(ctypes.addressof(src), n, self._bit, None,
+                                                                    ctypes.addressof(out), wl, room, flags)
+                        if r == _lib.E_CAPACITY:
+                            room = olen + 16
+                            continue
+                        break
                 break
             if r == _lib.NEED_INPUT and olen == 0 and bits == self._bit:
+                if self._eof:
+                    check(_lib.E_INTERNAL, "ndfl_inflate_range")   # unreachable: no IN_PARTIAL at EOF
                 want = len(self._ibuf) + self._batch        # no block completed: read more
                 continue
             if r < 0 or (r > len(_lib.REASONS) and r != _lib.NEED_INPUT):

@@ -74,7 +74,16 @@ const char* ndfl_error_string(int code);
 /* Create a context on HIP device `device`.  Fails with NDFL_E_DEVICE if no GPU. */
 int ndfl_ctx_create(ndfl_ctx** out, int device, uint32_t flags);
 int ndfl_ctx_destroy(ndfl_ctx* ctx);
-/* Use the caller's hipStream_t (NULL restores the context's own stream). */
+/*
+ * Stream ordering (every call that reads or writes device memory: NDFL_IN_DEVICE / NDFL_OUT_DEVICE
+ * buffers, ndfl_bits_shift, the deferred-window resolve).  By default a call's device work is
+ * ordered after all work queued earlier on the device's default (NULL) stream, so a buffer just
+ * produced there -- or a freed block a caching allocator hands out again while a kernel on that
+ * stream still uses it -- is safe to pass without a host synchronize.  A caller that works on
+ * another stream names it with ndfl_ctx_set_stream: the calls then run on that stream, in order
+ * with the caller's own work (NULL restores the default).  Every call completes its device work
+ * before it returns, so its outputs may be used right away on any stream.
+ */
 int ndfl_ctx_set_stream(ndfl_ctx* ctx, void* hip_stream);
 /* Average device time (ms) of the last call's dominant kernel, measured with HIP events. */
 double ndfl_ctx_last_kernel_ms(ndfl_ctx* ctx);

@@ -203,3 +203,50 @@ def c5_random_repeat(n, seed=0xC5):
                 ln += ll
         p += ln
     return a[:n]
+
+
+def c5_device(n, seed=0xC5, device="cuda", batch=256 << 20):
+    """Config 5 at its defined size (16 GiB), generated on the device: the same span mix as
+    c5_random_repeat -- 50 % random-byte spans (64..4095 B), ~10 % byte runs (3..4096 B), ~40 %
+    copies of earlier data (dist U[1, 32768], length 3 + geometric(1/20), capped at 258; overlapping
+    copies repeat their period) -- drawn per 256 MiB batch with a torch generator (seed + batch
+    index).  A copy's source is resolved by pointer jumping over the batch (copies of copies), and a
+    copy never reaches before its batch.  Deterministic per (seed, device type); not tiled."""
+    out = torch.empty(n, dtype=torch.uint8, device=device)
+    for b0 in range(0, n, batch):
+        m = min(batch, n - b0)
+        g = torch.Generator(device=device).manual_seed(seed * 1000003 + b0 // batch)
+        k = m // 300 + 1024                              # spans (mean length ~ 700 B, with slack)
+        while True:
+            u = torch.rand(k, generator=g, device=device)
+            kind = torch.where(u < 0.5, 0, torch.where(u < 0.6, 1, 2))          # random / run / copy
+            lr = torch.randint(64, 4096, (k,), generator=g, device=device)
+            lrun = torch.randint(3, 4097, (k,), generator=g, device=device)
+            gu = torch.rand(k, generator=g, device=device).clamp_(min=1e-12)
+            lcopy = (3 + torch.floor(torch.log(gu) / math.log(1 - 1 / 20.0)).long()).clamp_(max=258)
+            ln = torch.where(kind == 0, lr, torch.where(kind == 1, lrun, lcopy))
+            if int(ln.sum()) >= m:
+                break
+            k *= 2
+        starts = torch.cumsum(ln, 0) - ln
+        span = torch.repeat_interleave(torch.arange(k, device=device), ln)[:m]
+        pos = torch.arange(m, device=device)
+        sk = kind[span]
+        rnd = torch.randint(0, 256, (m,), generator=g, device=device, dtype=torch.uint8)
+        runv = torch.randint(0, 256, (k,), generator=g, device=device, dtype=torch.uint8)
+        val = torch.where(sk == 1, runv[span], rnd)
+        # copies: distance per span, U[1, min(32768, span start)]; the first 64 bytes are random
+        dmax = starts.clamp(min=1, max=32768)
+        d = (torch.rand(k, generator=g, device=device) * dmax).long() + 1
+        d = torch.minimum(d, dmax)
+        is_copy = (sk == 2) & (pos >= 64)
+        src = torch.where(is_copy, pos - d[span], pos)
+        del span, sk, rnd, runv
+        for _ in range(40):                              # pointer jumping: sources of sources
+            nxt = src[src]
+            if torch.equal(nxt, src):
+                break
+            src = nxt
+        out[b0:b0 + m] = val[src]
+        del src, val, pos, is_copy
+    return out
