@@ -26,23 +26,24 @@ public final class DeflaterOutputStream extends OutputStream {
 	private OutputStream output;
 	private final int dataLookaheadLimit, historyLookbehindLimit;
 	private final Strategy strategy;
-	private final NativeCodec codec;
+	private NativeCodec codec;           // created on first use (the constructors do no I/O)
 	private ByteBuffer pending;          // staged data (direct)
 	private final ByteBuffer history;    // last <= historyLookbehindLimit raw bytes (direct)
 	private ByteBuffer outBuf;           // compressed staging (direct)
 	private int bitPos = 0;              // BitOut bits pending (0..7)
 	private int bitByte = 0;             // the pending partial byte
 	private int[] crc = null;            // GzipOutputStream asks for the CRC pass fused into the encoder
+	private long written = 0;            // bytes written so far
 	private boolean ended = false;
 	
 	
-	public DeflaterOutputStream(OutputStream out) throws IOException {
+	public DeflaterOutputStream(OutputStream out) {
 		this(out, 64 * 1024, 32 * 1024, Lz77Huffman.RLE_DYNAMIC);
 	}
 	
 	
 	public DeflaterOutputStream(OutputStream out, int dataLookaheadLimit, int historyLookbehindLimit,
-			Strategy strat) throws IOException {
+			Strategy strat) {
 		output = Objects.requireNonNull(out);
 		strategy = Objects.requireNonNull(strat);
 		if (dataLookaheadLimit < 1 || historyLookbehindLimit < 0 || historyLookbehindLimit > 32 * 1024
@@ -50,21 +51,39 @@ public final class DeflaterOutputStream extends OutputStream {
 			throw new IllegalArgumentException("Invalid capacities");
 		this.dataLookaheadLimit = dataLookaheadLimit;
 		this.historyLookbehindLimit = historyLookbehindLimit;
-		codec = new NativeCodec(0);
 		pending = ByteBuffer.allocateDirect(Math.max(BATCH, dataLookaheadLimit) + dataLookaheadLimit + 1);
 		history = ByteBuffer.allocateDirect(Math.max(historyLookbehindLimit, 1));
 		history.limit(0);
 	}
 	
 	
+	// D/DeflaterOutputStream.java:69-73 (package-private there too; the gpu Gzip/Zlib streams use it)
 	OutputStream getUnderlyingStream() {
+		if (output == null)
+			throw new IllegalStateException("Stream already closed");
 		return output;
 	}
 	
-	void enableCrc() {
-		crc = new int[]{0};
+	
+	private NativeCodec codec() throws IOException {
+		if (codec == null)
+			codec = new NativeCodec(0);
+		return codec;
 	}
 	
+	
+	// GzipOutputStream: fuse the CRC-32 of the data into the encoder (ndfl_deflate_chunks crc_inout).
+	// Only before the first write, so the CRC covers exactly the bytes written through the gzip stream;
+	// returns false otherwise (the caller keeps its own java.util.zip.CRC32).
+	boolean enableCrc() {
+		if (written != 0 || crc != null)
+			return false;
+		crc = new int[]{0};
+		return true;
+	}
+	
+	
+	// the CRC-32 of everything written; valid after finish()
 	int crc() {
 		return crc[0];
 	}
@@ -79,6 +98,7 @@ public final class DeflaterOutputStream extends OutputStream {
 		if (ended)
 			throw new IllegalStateException("Stream already ended");
 		Objects.checkFromIndexSize(off, len, b.length);
+		written += len;
 		while (len > 0) {
 			if (!pending.hasRemaining())
 				flush(false);
@@ -104,10 +124,14 @@ public final class DeflaterOutputStream extends OutputStream {
 	
 	
 	@Override public void close() throws IOException {
+		if (output == null)
+			return;
 		if (!ended)
 			finish();
 		output.close();
-		codec.close();
+		output = null;
+		if (codec != null)
+			codec.close();
 	}
 	
 	
@@ -145,9 +169,9 @@ public final class DeflaterOutputStream extends OutputStream {
 	}
 	
 	
-	private int batched(ByteBuffer data, int take, boolean isFinal, long[] res) {
+	private int batched(ByteBuffer data, int take, boolean isFinal, long[] res) throws IOException {
 		int histLen = history.limit();
-		long ctx = codec.handle();
+		long ctx = codec().handle();
 		if (strategy instanceof Lz77Huffman lz) {
 			return NativeCodec.deflateChunksLz770(ctx, history, histLen, historyLookbehindLimit, data, take,
 				dataLookaheadLimit, lz.useDynamicHuffmanCodes(), lz.searchMinimumRunLength(), lz.searchMaximumRunLength(),
@@ -172,7 +196,7 @@ public final class DeflaterOutputStream extends OutputStream {
 			data.get(pos, combined, hl, k);
 			strategy.decide(combined, 0, hl, k).compressTo(bo, isFinal && pos + k == take);
 			if (crc != null)
-				crc[0] = NativeCodec.crc320(codec.handle(), crc[0], ByteBuffer.allocateDirect(k).put(0, combined, hl, k), k);
+				crc[0] = NativeCodec.crc320(codec().handle(), crc[0], ByteBuffer.allocateDirect(k).put(0, combined, hl, k), k);
 			int nh = Math.min(historyLookbehindLimit, hl + k);
 			System.arraycopy(combined, hl + k - nh, combined, 0, nh);
 			hl = nh;

@@ -22,11 +22,12 @@ public final class InflaterInputStream extends InputStream {
 	
 	static final int BATCH = 64 << 20;
 	private static final int WINDOW = 32768;
+	private static final long MAX_OUT = Integer.MAX_VALUE - 8;   // largest direct buffer
 	
 	private InputStream input;
 	private final boolean endExactly;
 	private final int batch;
-	private final NativeCodec codec;
+	private NativeCodec codec;           // created on first use (the constructors do no I/O)
 	private ByteBuffer in;               // unconsumed input (direct); byte 0 holds bit `bit` of the stream
 	private int bit = 0;
 	private boolean eof = false, last = false;
@@ -37,17 +38,17 @@ public final class InflaterInputStream extends InputStream {
 	private boolean closed = false;
 	
 	
-	public InflaterInputStream(InputStream in) throws IOException {
+	public InflaterInputStream(InputStream in) {
 		this(in, false);
 	}
 	
 	
-	public InflaterInputStream(InputStream in, boolean endExactly) throws IOException {
+	public InflaterInputStream(InputStream in, boolean endExactly) {
 		this(in, endExactly, 16 * 1024);
 	}
 	
 	
-	public InflaterInputStream(InputStream in, boolean endExactly, int inBufLen) throws IOException {
+	public InflaterInputStream(InputStream in, boolean endExactly, int inBufLen) {
 		input = Objects.requireNonNull(in);
 		if (inBufLen <= 0)
 			throw new IllegalArgumentException("Non-positive input buffer size");
@@ -58,7 +59,6 @@ public final class InflaterInputStream extends InputStream {
 		}
 		this.endExactly = endExactly;
 		batch = Math.max(inBufLen, BATCH);
-		codec = new NativeCodec(0);
 		this.in = ByteBuffer.allocateDirect(batch + 256);
 		this.in.limit(0);
 	}
@@ -119,21 +119,36 @@ public final class InflaterInputStream extends InputStream {
 			windowLen = keep;
 			outPos = outEnd = 0;
 		}
+		if (codec == null)
+			codec = new NativeCodec(0);
 		int want = batch;
 		while (true) {
 			readMore(want);
-			long inLen = in.limit();
-			long need = windowLen + 4 * inLen + 65536;
+			final long all = in.limit();
+			long inLen = all;
 			var res = new long[2];
 			int r;
 			while (true) {
-				prepareOut(need);
-				r = NativeCodec.inflateRange0(codec.handle(), in, inLen, bit, out, windowLen, !eof, res);
+				// decode a prefix of the buffered input: all of it, unless its output would not fit in
+				// one direct buffer -- then a shorter prefix, which stops at an earlier block boundary
+				long need = windowLen + 4 * inLen + 65536;
+				boolean partial = !eof || inLen < all;
+				while (true) {
+					prepareOut(Math.min(need, MAX_OUT));
+					r = NativeCodec.inflateRange0(codec.handle(), in, inLen, bit, out, windowLen, partial, res);
+					if (r != NativeCodec.E_CAPACITY || windowLen + res[0] + 16 > MAX_OUT)
+						break;
+					need = windowLen + res[0] + 16;
+				}
 				if (r != NativeCodec.E_CAPACITY)
 					break;
-				need = windowLen + res[0] + 16;
+				if (inLen <= 1)
+					throw new IOException("A single DEFLATE block decodes to more than " + MAX_OUT + " bytes");
+				inLen /= 2;
 			}
 			if (r == NativeCodec.NEED_INPUT && res[0] == 0 && res[1] == bit) {
+				if (inLen < all)                    // the shorter prefix completes no block
+					throw new IOException("A single DEFLATE block decodes to more than " + MAX_OUT + " bytes");
 				want = in.limit() + batch;          // no block completed in this batch: read more
 				continue;
 			}
@@ -167,15 +182,21 @@ public final class InflaterInputStream extends InputStream {
 			bigger.put(in.duplicate().position(0).limit(in.limit())).flip();
 			in = bigger;
 		}
+		// read until `want` bytes are buffered, the stream ends, or a read returns short (a pipe or
+		// socket with nothing more available yet): what is buffered is decoded first, as Open
+		// decodes from whatever its fill returned (D/decomp/Open.java:181-192)
 		var tmp = new byte[65536];
 		while (in.limit() < want && !eof) {
-			int n = input.read(tmp, 0, Math.min(tmp.length, want - in.limit()));
+			int ask = Math.min(tmp.length, want - in.limit());
+			int n = input.read(tmp, 0, ask);
 			if (n == -1)
 				eof = true;
 			else {
 				int p = in.limit();
 				in.limit(p + n);
 				in.put(p, tmp, 0, n);
+				if (n < ask && in.limit() > 0)
+					break;
 			}
 		}
 	}
@@ -207,7 +228,8 @@ public final class InflaterInputStream extends InputStream {
 		if (!closed)
 			input.close();
 		closed = true;
-		codec.close();
+		if (codec != null)
+			codec.close();
 	}
 	
 }

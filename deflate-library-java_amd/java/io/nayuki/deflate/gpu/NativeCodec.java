@@ -66,6 +66,33 @@ final class NativeCodec implements AutoCloseable {
 	static native int crc320(long ctx, int crc, ByteBuffer data, long len);
 	static native int adler320(long ctx, int adler, ByteBuffer data, long len);
 	
+	
+	static final int GPU_CHECKSUM_MIN = 1 << 20;   // smaller arrays: a host loop beats a launch + copy
+	private ByteBuffer staging;
+	
+	// java.util.zip.Adler32.update continued from `adler` (the zlib streams' checksum,
+	// D/ZlibOutputStream.java:48, D/ZlibInputStream.java:57): large arrays on the GPU (ndfl_adler32),
+	// small ones on the host
+	int adler32(int adler, byte[] b, int off, int len) {
+		if (len >= GPU_CHECKSUM_MIN) {
+			if (staging == null || staging.capacity() < len)
+				staging = ByteBuffer.allocateDirect(len);
+			staging.put(0, b, off, len);
+			return adler320(handle(), adler, staging, len);
+		}
+		long s1 = adler & 0xFFFF, s2 = adler >>> 16;
+		for (int i = 0; i < len; ) {
+			int end = Math.min(len, i + 5552);       // no overflow before the reduction
+			for (; i < end; i++) {
+				s1 += b[off + i] & 0xFF;
+				s2 += s1;
+			}
+			s1 %= 65521;
+			s2 %= 65521;
+		}
+		return (int)((s2 << 16) | s1);
+	}
+	
 	// the plugin API: strategy tree (9 ints per node) -> decision handle; compressTo -> end bit or -1
 	static native long decide0(long ctx, int[] nodes, int root, byte[] b, int off, int historyLen, int dataLen,
 		long[] bitLengths);

@@ -166,6 +166,13 @@ JNIEXPORT jlong JNICALL Java_io_nayuki_deflate_gpu_NativeCodec_decide0(JNIEnv* e
         jintArray nodes, jint root, jbyteArray b, jint off, jint historyLen, jint dataLen, jlongArray bitLengths) {
     (void)k;
     const jsize nn = (*env)->GetArrayLength(env, nodes) / 9;
+    const jsize blen = (*env)->GetArrayLength(env, b);
+    /* b[off, off + historyLen + dataLen) must lie inside the array (Strategy.decide's contract) */
+    if (off < 0 || historyLen < 0 || dataLen < 0 || (jlong)off + historyLen + dataLen > (jlong)blen) {
+        jclass c = (*env)->FindClass(env, "java/lang/IndexOutOfBoundsException");
+        if (c) (*env)->ThrowNew(env, c, "Range out of bounds");
+        return 0;
+    }
     ndfl_strategy_node* nd = (ndfl_strategy_node*)malloc(sizeof(ndfl_strategy_node) * (nn ? nn : 1));
     jint* v = (jint*)malloc(sizeof(jint) * 9 * (nn ? nn : 1));
     jdec* jd = (jdec*)calloc(1, sizeof(jdec));
@@ -183,6 +190,10 @@ JNIEXPORT jlong JNICALL Java_io_nayuki_deflate_gpu_NativeCodec_decide0(JNIEnv* e
         nd[i].first_child = v[9 * i + 6]; nd[i].n_children = v[9 * i + 7]; nd[i].min_block_len = v[9 * i + 8];
     }
     (*env)->GetByteArrayRegion(env, b, off, total, (jbyte*)copy);
+    if ((*env)->ExceptionCheck(env)) {               /* nothing is kept: free and return */
+        free(nd); free(v); free(jd); free(copy);
+        return 0;
+    }
     uint64_t bl[8];
     int r = ndfl_decide(CTX(ctx), nd, (uint32_t)nn, (uint32_t)root, copy, 0, (uint32_t)historyLen, (uint32_t)dataLen,
                         bl, &jd->dec);

@@ -5,7 +5,8 @@
         (tests/corpus.py c2_gzip; device-resident input -> output)
     c3  FULL_DYNAMIC (LZ77 + dynamic Huffman) compress of 1 GiB enwik-style text, device-resident;
         ratio checked against the oracle on a prefix (bit-exact, so the ratio is the reference's)
-    c5  one GPU's share of the 16 GiB random+repeat round trip (2 GiB, RLE_DYNAMIC; corpus.c5_random_repeat), device-resident
+    c5  the 16 GiB random+repeat round trip on one GPU (RLE_DYNAMIC; corpus.c5_device), device-resident,
+        the whole stream checked against the oracle
 
 Each config prints one JSON line; the oracle (1 thread) is timed on a bounded sample beside it.
 Run on the GPU box: python scripts/bench_configs.py [c1 c2 c3 c5].
@@ -18,6 +19,7 @@ import sys
 import time
 
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, ROOT)
 sys.path.insert(0, os.path.join(ROOT, "deflate-library-java_amd", "python"))
 sys.path.insert(0, os.path.join(ROOT, "tests"))
 import numpy as np  # noqa: E402
@@ -117,31 +119,45 @@ def c3(ctx):
             "round_trip_ok": rt, "cpu_oracle_MiBps": round(pre / tc / MIB, 2)}
 
 
-def c5(ctx):
-    # the -m gpu test's corpus (tests/corpus.py c5_random_repeat, seed 0xC5): 256 MiB tiled to 2 GiB
-    base = 256 * MIB
-    a = corpus.c5_random_repeat(base)
-    n = 2 << 30
-    data = torch.from_numpy(np.tile(a, n // base)).cuda()
+def c5(ctx, n=16 << 30):
+    """Config 5 as BASELINE.json defines it: a 16 GiB random+repeat stream (corpus.c5_device, seed
+    0xC5, generated on the device, not tiled), RLE_DYNAMIC compress then inflate on one GPU
+    (288 GB HBM holds input, stream, output and the decoder's scratch).  bit_exact: the whole
+    stream against the oracle (chunk-parallel on 16 host threads, bench.verify_stream)."""
+    from bench import verify_stream
+    t0 = time.perf_counter()
+    data = corpus.c5_device(n, device="cuda")
+    torch.cuda.synchronize()
+    gen_s = time.perf_counter() - t0
     cap = ndfl._lib.load().ndfl_deflate_bound(n, 65536) + 64
-    comp = torch.empty(cap, dtype=torch.uint8, device="cuda")
+    comp = torch.empty(cap + ndfl.IN_PAD_BYTES, dtype=torch.uint8, device="cuda")
     dec = torch.empty(n + 64, dtype=torch.uint8, device="cuda")
     st = {}
 
     def run():
+        t = time.perf_counter()
         eb, _ = ctx.deflate_chunks_raw(None, 0, 32768, data.data_ptr(), n, 65536, 3, True, 0, comp.data_ptr(), cap, DEV)
+        t1 = time.perf_counter()
         st["td"] = ctx.timings()["deflate"]
         cb = (eb + 7) // 8
-        r, olen, _ = ctx.inflate_raw(comp.data_ptr(), cb, dec.data_ptr(), dec.numel(), DEV)
-        st.update(cb=cb, r=r, olen=olen, ti=ctx.timings()["inflate_span"])
-    dt = timed(run, 3)
+        comp[cb:cb + ndfl.IN_PAD_BYTES].zero_()
+        r, olen, _ = ctx.inflate_raw(comp.data_ptr(), cb, dec.data_ptr(), dec.numel(), DEV | ndfl.IN_PADDED)
+        t2 = time.perf_counter()
+        st.update(eb=eb, cb=cb, r=r, olen=olen, ti=ctx.timings()["inflate_span"], wc=t1 - t, wi=t2 - t1)
+    dt = timed(run, 2)
     ok = st["r"] == 0 and st["olen"] == n and torch.equal(dec[:n], data)
-    return {"config": "c5 (one GPU's share): RLE_DYNAMIC round trip of 2 GiB random+repeat (device-resident)",
-            "round_trip_ok": ok, "ratio": round(st["cb"] / n, 4), "ms_per_round_trip": round(dt * 1e3, 2),
-            "input_MiBps": round((n + st["cb"]) / dt / MIB, 1),
-            "compress_ms": round(st["td"], 2), "inflate_span_ms": round(st["ti"], 2),
-            "compress_frac_hbm": round((n + st["cb"]) / (st["td"] / 1e3) / 8e12, 4),
-            "decompress_frac_hbm": round((n + st["cb"]) / (st["ti"] / 1e3) / 8e12, 4)}
+    v = verify_stream(data, None, True, comp, st["eb"], 16)
+    cb = st["cb"]
+    return {"config": "c5: RLE_DYNAMIC round trip of 16 GiB random+repeat (device-resident, one GPU)",
+            "bytes": n, "round_trip_ok": ok, "bit_exact": v["bit_exact"], "verify": v,
+            "ratio": round(cb / n, 4), "ms_per_round_trip": round(dt * 1e3, 2),
+            "input_MiBps": round((n + cb) / dt / MIB, 1),
+            "compress_ms": round(st["td"], 2), "compress_wall_ms": round(st["wc"] * 1e3, 2),
+            "inflate_span_ms": round(st["ti"], 2), "inflate_wall_ms": round(st["wi"] * 1e3, 2),
+            "compress_frac_hbm": round((n + cb) / (st["td"] / 1e3) / 8e12, 4),
+            "decompress_frac_hbm": round((n + cb) / (st["ti"] / 1e3) / 8e12, 4),
+            "decompress_read_frac_hbm": round(cb / (st["ti"] / 1e3) / 8e12, 4),
+            "round_trip_frac_hbm": round(2 * (n + cb) / dt / 8e12, 4), "corpus_gen_s": round(gen_s, 1)}
 
 
 def main():
