@@ -71,6 +71,7 @@ static_assert((60 + 1) * 4 <= IN_PAD, "round staging clamp must stay inside the 
 // header finder scan pattern (32-bit words): FIND_WIN_WORDS of every FIND_PERIOD_WORDS.  Dense
 // (every position) by default: sparse windows make chains span several blocks, which costs more
 // in the count/emit passes' load balance than it saves here.
+constexpr uint32_t PART_EXPENSIVE = 1u << 30;     // partitioned finder: expensive first block (state flag)
 constexpr uint32_t FIND_WIN_WORDS = 32768;
 constexpr uint32_t FIND_PERIOD_WORDS = 32768;
 #ifndef NDFL_FIND_WPT
@@ -339,6 +340,66 @@ __device__ __noinline__ bool strict_stored(const In& in, uint64_t p) {
 #ifndef NDFL_STRICT_WPE
 #define NDFL_STRICT_WPE 4
 #endif
+namespace inf {
+// Stage-1 test of the 32 bit positions of input word t below scan_end; survivors go to the
+// workgroup's LDS list (bit 63 set: dynamic header, clear: stored).
+__device__ __forceinline__ void find_word(const In& in, uint64_t t, uint64_t scan_end, uint64_t* cand,
+                                          uint32_t* ncand) {
+    const uint64_t nbits = in.nbits;
+    const uint64_t p0 = t * 32;
+    if (p0 >= scan_end) return;
+    const uint32_t w0 = in.ld(t), w1 = in.ld(t + 1), w2 = in.ld(t + 2), w3 = in.ld(t + 3);
+    const uint64_t W = (uint64_t)w0 | ((uint64_t)w1 << 32);
+    const uint32_t b1 = (uint32_t)(W >> 1), b2 = (uint32_t)(W >> 2);
+    uint32_t valid = 0xFFFFFFFFu;
+    if (p0 + 35 > nbits) valid = (nbits >= p0 + 3) ? (uint32_t)((1ull << (nbits - p0 - 2)) - 1) : 0u;
+    if (p0 + 32 > scan_end) valid &= (uint32_t)((1ull << (scan_end - p0)) - 1);
+    uint32_t m2 = ~b1 & b2 & valid & kraft_complete_mask(w0, w1, w2, w3);
+    // LEN == ~NLEN at byte positions p0 + 8j, j = 1..5; position i pads to j = (i + 10) / 8
+    const uint64_t W12 = (uint64_t)w1 | ((uint64_t)w2 << 32);
+    const uint32_t x1 = (uint32_t)(W >> 8), x2 = (uint32_t)(W >> 16), x3 = (uint32_t)(W >> 24), x4 = w1,
+                   x5 = (uint32_t)(W12 >> 8);
+#define NDFL_LENOK(x) ((((x) ^ ((x) >> 16)) & 0xFFFFu) == 0xFFFFu)
+    const uint32_t okm = (NDFL_LENOK(x1) ? 0x0000003Fu : 0u) | (NDFL_LENOK(x2) ? 0x00003FC0u : 0u) |
+                         (NDFL_LENOK(x3) ? 0x003FC000u : 0u) | (NDFL_LENOK(x4) ? 0x3FC00000u : 0u) |
+                         (NDFL_LENOK(x5) ? 0xC0000000u : 0u);
+#undef NDFL_LENOK
+    uint32_t m0 = ~b1 & ~b2 & valid & okm;
+    while (m2) {
+        const uint32_t o = __builtin_ctz(m2);
+        m2 &= m2 - 1;
+        const uint32_t nf3 = 3 * (((uint32_t)(W >> (o + 13)) & 15u) + 4);
+        if (p0 + o + 17 + nf3 <= nbits) {
+            uint32_t k = atomicAdd(ncand, 1u);
+            if (k < 2048) cand[k] = (p0 + o) | (1ull << 63);
+        }
+    }
+    while (m0) {
+        const uint32_t o = __builtin_ctz(m0);
+        m0 &= m0 - 1;
+        const uint32_t q = o + 3, al = (q + 7) & ~7u;            // al <= 40
+        const uint32_t pad = al > q ? (uint32_t)(W >> q) & ((1u << (al - q)) - 1u) : 0u;
+        if (pad) continue;
+        const uint32_t ln = (al < 32 ? (uint32_t)(W >> al) : (uint32_t)(W12 >> (al - 32))) & 0xFFFFu;
+        if (p0 + al + 32 + 8ull * ln <= nbits) {
+            uint32_t k = atomicAdd(ncand, 1u);
+            if (k < 2048) cand[k] = p0 + o;
+        }
+    }
+}
+
+// the workgroup's LDS survivors -> the global survivor list (one global atomic)
+__device__ __forceinline__ void find_flush(const uint64_t* cand, const uint32_t* ncand, uint32_t* gbase,
+                                           uint64_t* qlist, uint32_t* qcount, uint32_t qcap) {
+    __syncthreads();
+    const uint32_t nc = min(*ncand, 2048u);
+    if (threadIdx.x == 0) *gbase = nc ? atomicAdd(qcount, nc) : 0u;
+    __syncthreads();
+    for (uint32_t k = threadIdx.x; k < nc; k += blockDim.x)
+        if (*gbase + k < qcap) qlist[*gbase + k] = cand[k];
+}
+}  // namespace inf
+
 extern "C" __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(NDFL_FIND_WPE)))
 ndfl_inflate_find_kernel(const uint32_t* w, uint64_t nwords, uint64_t nbits, uint64_t* qlist, uint32_t* qcount,
                          uint32_t qcap, uint32_t win_words, uint32_t period_words, uint64_t w_lo, uint64_t scan_end) {
@@ -351,61 +412,95 @@ ndfl_inflate_find_kernel(const uint32_t* w, uint64_t nwords, uint64_t nbits, uin
     // (FIND_WPT words per thread, so that one group's survivors cost one global atomic)
     In in{w, nwords, nbits};
     for (uint32_t kk = 0; kk < FIND_WPT; kk++) {
-    const uint64_t tt = ((uint64_t)blockIdx.x * FIND_WPT + kk) * blockDim.x + threadIdx.x;
-    // input word index; the scan covers bit positions [w_lo * 32, scan_end) of the stream
-    const uint64_t t = win_words == period_words ? w_lo + tt    // every position (the default): no division
-                                                 : w_lo + (tt / win_words) * period_words + tt % win_words;
-    const uint64_t p0 = t * 32;
-    if (p0 < scan_end) {
-        const uint32_t w0 = in.ld(t), w1 = in.ld(t + 1), w2 = in.ld(t + 2), w3 = in.ld(t + 3);
-        const uint64_t W = (uint64_t)w0 | ((uint64_t)w1 << 32);
-        const uint32_t b1 = (uint32_t)(W >> 1), b2 = (uint32_t)(W >> 2);
-        uint32_t valid = 0xFFFFFFFFu;
-        if (p0 + 35 > nbits) valid = (nbits >= p0 + 3) ? (uint32_t)((1ull << (nbits - p0 - 2)) - 1) : 0u;
-        if (p0 + 32 > scan_end) valid &= (uint32_t)((1ull << (scan_end - p0)) - 1);
-        uint32_t m2 = ~b1 & b2 & valid & kraft_complete_mask(w0, w1, w2, w3);
-        // LEN == ~NLEN at byte positions p0 + 8j, j = 1..5; position i pads to j = (i + 10) / 8
-        const uint64_t W12 = (uint64_t)w1 | ((uint64_t)w2 << 32);
-        const uint32_t x1 = (uint32_t)(W >> 8), x2 = (uint32_t)(W >> 16), x3 = (uint32_t)(W >> 24), x4 = w1,
-                       x5 = (uint32_t)(W12 >> 8);
-#define NDFL_LENOK(x) ((((x) ^ ((x) >> 16)) & 0xFFFFu) == 0xFFFFu)
-        const uint32_t okm = (NDFL_LENOK(x1) ? 0x0000003Fu : 0u) | (NDFL_LENOK(x2) ? 0x00003FC0u : 0u) |
-                             (NDFL_LENOK(x3) ? 0x003FC000u : 0u) | (NDFL_LENOK(x4) ? 0x3FC00000u : 0u) |
-                             (NDFL_LENOK(x5) ? 0xC0000000u : 0u);
-#undef NDFL_LENOK
-        uint32_t m0 = ~b1 & ~b2 & valid & okm;
-        while (m2) {
-            const uint32_t o = __builtin_ctz(m2);
-            m2 &= m2 - 1;
-            const uint32_t nf3 = 3 * (((uint32_t)(W >> (o + 13)) & 15u) + 4);
-            if (p0 + o + 17 + nf3 <= nbits) {
-                uint32_t k = atomicAdd(&ncand, 1u);
-                if (k < 2048) cand[k] = (p0 + o) | (1ull << 63);
-            }
-        }
-        while (m0) {
-            const uint32_t o = __builtin_ctz(m0);
-            m0 &= m0 - 1;
-            const uint32_t q = o + 3, al = (q + 7) & ~7u;            // al <= 40
-            const uint32_t pad = al > q ? (uint32_t)(W >> q) & ((1u << (al - q)) - 1u) : 0u;
-            if (pad) continue;
-            const uint32_t ln = (al < 32 ? (uint32_t)(W >> al) : (uint32_t)(W12 >> (al - 32))) & 0xFFFFu;
-            if (p0 + al + 32 + 8ull * ln <= nbits) {
-                uint32_t k = atomicAdd(&ncand, 1u);
-                if (k < 2048) cand[k] = p0 + o;
-            }
-        }
+        const uint64_t tt = ((uint64_t)blockIdx.x * FIND_WPT + kk) * blockDim.x + threadIdx.x;
+        // input word index; the scan covers bit positions [w_lo * 32, scan_end) of the stream
+        const uint64_t t = win_words == period_words ? w_lo + tt    // every position (the default): no division
+                                                     : w_lo + (tt / win_words) * period_words + tt % win_words;
+        find_word(in, t, scan_end, cand, &ncand);
     }
+    find_flush(cand, &ncand, &gbase, qlist, qcount, qcap);
+}
+
+// Partitioned finder (long streams): the scanned range is cut into partitions of part_words input
+// words, and launch `iter` scans window `iter` (FIND_WPT * 256 words) of every partition that has
+// no accepted header yet (done[], set by the strict stage).  So each partition is scanned only up to
+// its first block header -- about half a block on average -- instead of every bit position, and the
+// decode chains start at those headers (a chain decodes on through the block boundaries that are not
+// candidates, to the next partition's header).  One workgroup per partition and window.
+extern "C" __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(NDFL_FIND_WPE)))
+ndfl_inflate_find_sparse_kernel(const uint32_t* w, uint64_t nwords, uint64_t nbits, uint64_t* qlist, uint32_t* qcount,
+                                uint32_t qcap, uint64_t w_lo, uint64_t scan_end, uint32_t part_words, uint32_t iter,
+                                const uint32_t* done, uint32_t* last_win) {
+    using namespace inf;
+    __shared__ uint64_t cand[2048];
+    __shared__ uint32_t ncand, gbase;
+    const uint32_t part = blockIdx.x;
+    if (done[part]) return;                                    // workgroup-uniform
+    if (threadIdx.x == 0) last_win[part] = iter;
+    const uint64_t pw0 = w_lo + (uint64_t)part * part_words;
+    const uint64_t wb = pw0 + (uint64_t)iter * FIND_WPT * 256;
+    const uint64_t we = min(pw0 + part_words, (scan_end + 31) / 32);
+    if (wb >= we) return;
+    if (threadIdx.x == 0) ncand = 0;
+    __syncthreads();
+    In in{w, nwords, nbits};
+    for (uint32_t kk = 0; kk < FIND_WPT; kk++) {
+        const uint64_t t = wb + (uint64_t)kk * blockDim.x + threadIdx.x;
+        if (t < we) find_word(in, t, scan_end, cand, &ncand);
     }
+    find_flush(cand, &ncand, &gbase, qlist, qcount, qcap);
+}
+
+// Completion of the partitioned scan: a partition is scanned in full after all when the window in
+// which its first header was found holds two or more (short blocks: a chain through the partition
+// would decode many blocks one after another), or when that header's block is expensive --
+// phase-locked literal codes (the count pass decodes such blocks from all 8 bit phases) or a high
+// expansion.  Its blocks then become chains of their own, so the chains' costs stay balanced; such
+// regions are cheap to scan (few bits per block, or a small share of the stream).  Workgroup
+// (partition, window).
+extern "C" __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(NDFL_FIND_WPE)))
+ndfl_inflate_find_fill_kernel(const uint32_t* w, uint64_t nwords, uint64_t nbits, uint64_t* qlist, uint32_t* qcount,
+                              uint32_t qcap, uint64_t w_lo, uint64_t scan_end, uint32_t part_words, uint32_t wpp,
+                              const uint32_t* done, const uint32_t* last_win) {
+    using namespace inf;
+    __shared__ uint64_t cand[2048];
+    __shared__ uint32_t ncand, gbase;
+    const uint32_t part = blockIdx.x / wpp, win = blockIdx.x % wpp;
+    const uint32_t st = done[part];
+    if (!((st & PART_EXPENSIVE) || (st & 0xFFFFu) >= 2u) || win <= last_win[part]) return;   // workgroup-uniform
+    const uint64_t pw0 = w_lo + (uint64_t)part * part_words;
+    const uint64_t wb = pw0 + (uint64_t)win * FIND_WPT * 256;
+    const uint64_t we = min(pw0 + part_words, (scan_end + 31) / 32);
+    if (wb >= we) return;
+    if (threadIdx.x == 0) ncand = 0;
     __syncthreads();
-    const uint32_t nc = min(ncand, 2048u);
-    if (threadIdx.x == 0) gbase = nc ? atomicAdd(qcount, nc) : 0u;
-    __syncthreads();
-    for (uint32_t k = threadIdx.x; k < nc; k += blockDim.x)
-        if (gbase + k < qcap) qlist[gbase + k] = cand[k];
+    In in{w, nwords, nbits};
+    for (uint32_t kk = 0; kk < FIND_WPT; kk++) {
+        const uint64_t t = wb + (uint64_t)kk * blockDim.x + threadIdx.x;
+        if (t < we) find_word(in, t, scan_end, cand, &ncand);
+    }
+    find_flush(cand, &ncand, &gbase, qlist, qcount, qcap);
 }
 
 namespace inf {
+// Prefix sums over the length symbols 257 + k (k = 0..28) of their run base (RUN_LENGTH_TABLE,
+// D/decomp/Open.java:841-850) and extra-bit counts: the strict stage's expansion estimate of a
+// header (expected output bytes per stream bit under the code's own symbol probabilities 2^-len).
+struct LenPrefix { uint32_t base[30], extra[30]; };
+constexpr LenPrefix make_len_prefix() {
+    LenPrefix t{};
+    uint32_t b = 0, x = 0;
+    for (uint32_t k = 0; k < 29; k++) {
+        t.base[k] = b; t.extra[k] = x;
+        const uint32_t ne = k < 8 || k == 28 ? 0u : (k >> 2) - 1;
+        const uint32_t base = k < 8 ? k + 3 : k == 28 ? 258u : ((4u + (k & 3)) << ne) + 3;
+        b += base; x += ne;
+    }
+    t.base[29] = b; t.extra[29] = x;
+    return t;
+}
+__device__ constexpr LenPrefix LEN_PREFIX = make_len_prefix();
+
 // strict-stage reader: 64-bit buffer, the next 16-byte group always in flight
 struct SRd {
     uint64_t bb, pos, qw;
@@ -459,7 +554,8 @@ struct SRd {
 extern "C" __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(NDFL_STRICT_WPE)))
 ndfl_inflate_strict_kernel(const uint32_t* w, uint64_t nwords, uint64_t nbits, const uint64_t* qlist,
                            const uint32_t* qcount, uint32_t qcap, uint32_t* seg_cnt, uint64_t* seg_list,
-                           uint32_t* ticket, unsigned long long* sst) {
+                           uint32_t* ticket, unsigned long long* sst, uint32_t* done, uint64_t part_base,
+                           uint64_t part_bits) {
     using namespace inf;
     __shared__ uint4 tabs[256 * 8];                          // 128 bytes per lane
     uint8_t* tab = (uint8_t*)&tabs[threadIdx.x * 8];
@@ -475,6 +571,7 @@ ndfl_inflate_strict_kernel(const uint32_t* w, uint64_t nwords, uint64_t nbits, c
         const uint32_t seg = (uint32_t)(p / ((uint64_t)SEG_BYTES * 8));
         const uint32_t idx = atomicAdd(&seg_cnt[seg], 1u);
         if (idx < SEG_CAP) seg_list[(uint64_t)seg * SEG_CAP + idx] = p;
+        if (done) atomicAdd(&done[(p - part_base) / part_bits], 1u);  // partitioned finder: headers found
     };
     bool active = false;
     uint64_t p = 0;
@@ -482,6 +579,9 @@ ndfl_inflate_strict_kernel(const uint32_t* w, uint64_t nwords, uint64_t nbits, c
     rd.bb = 0; rd.pos = 0; rd.qw = 0; rd.bn = 0; rd.ci = 0;
     uint32_t i = 0, total = 0, numLit = 0, numDist = 0, litK = 0, distK = 0, ones = 0, other = 0, eob = 0, d0 = 0,
              d31 = 0;
+    // partitioned finder: the header's cost class -- phase-locked literal codes (the count pass's
+    // 8-phase rounds) or a high expansion (many blocks / many output bytes per stream bit)
+    uint32_t n8 = 0, e_bytes = 0, e_bits = 0;
     int runVal = -1;
     uint64_t n_iter = 0, n_refill = 0, n_steps = 0;      // NDFL_STATS (sst != nullptr)
     for (;;) {
@@ -553,6 +653,7 @@ ndfl_inflate_strict_kernel(const uint32_t* w, uint64_t nwords, uint64_t nbits, c
                             }
                         }
                         i = 0; runVal = -1; litK = 0; distK = 0; ones = 0; other = 0; eob = 0; d0 = 0; d31 = 0;
+                        n8 = 0; e_bytes = 0; e_bits = 0;
                         active = complete;
                     }
                 }
@@ -585,6 +686,16 @@ ndfl_inflate_strict_kernel(const uint32_t* w, uint64_t nwords, uint64_t nbits, c
             const uint32_t v = (uint32_t)runVal;
             const uint32_t wt = v ? (32768u >> v) : 0u;
             litK += (min(en, numLit) - min(i, numLit)) * wt;
+            if (done) {
+                // symbols [i, min(en, numLit)) of the literal/length code, all of length v
+                const uint32_t a = min(i, numLit), b = min(en, numLit);
+                const uint32_t nl = min(b, 256u) - min(a, 256u);
+                const uint32_t la = min(max(a, 257u), 286u) - 257u, lb = min(max(b, 257u), 286u) - 257u;
+                const uint32_t w8 = wt >> 4;                          // 2^-v in units of 2^-11
+                n8 += v == 8 ? b - a : 0u;
+                e_bytes += w8 * (nl + LEN_PREFIX.base[lb] - LEN_PREFIX.base[la]);
+                e_bits += w8 * (v * (b - a) + LEN_PREFIX.extra[lb] - LEN_PREFIX.extra[la] + 5u * (lb - la));
+            }
             const uint32_t da = max(i, numLit) - numLit, db = max(en, numLit) - numLit, cd = db - da;
             distK += cd * wt;
             ones += v == 1 ? cd : 0u;
@@ -601,7 +712,12 @@ ndfl_inflate_strict_kernel(const uint32_t* w, uint64_t nwords, uint64_t nbits, c
                 else if (numDist == 1 && d0 == 0) ok = true;
                 else if (ones == 1 && other == 0) ok = !(numDist == 32 && d31 == 1);
                 else ok = distK == 32768u;
-                if (ok) record(p);
+                if (ok) {
+                    record(p);
+                    // phase-locked literal codes, or more than 2 output bytes per stream bit
+                    if (done && (n8 >= 192u || e_bytes > 2u * e_bits))
+                        atomicOr(&done[(p - part_base) / part_bits], PART_EXPENSIVE);
+                }
             }
         }
     }
@@ -667,7 +783,14 @@ struct SegPool {
     uint32_t* ctr;        // records handed out
     uint32_t nrec;
     uint64_t nslot;
+    // per Huffman block: the count pass's decode tables and header fields (BT_BYTES each), so the
+    // emit pass loads them instead of parsing the header and building the tables again; a block's
+    // first round record names its table record in SegMeta::pad (NOREC: none)
+    char* bt;
+    uint32_t* bctr;       // table records handed out
+    uint32_t nbt;
 };
+constexpr uint32_t BT_BYTES = 6720;   // wv::Tabs (6656) + hdr bit, data bit (u64 each), bfinal, btype, ed, pad
 
 #include "inflate_wave.hpp"
 
@@ -693,6 +816,8 @@ struct InflateScratch {
     void* d_ph = nullptr;                             // count pass: phase-fallback slot per wave
     void* d_cticket = nullptr;                        // count pass: chain tickets (one per launch)
     void* d_out = nullptr; size_t d_out_cap = 0;
+    void* d_done = nullptr; size_t d_done_cap = 0;    // partitioned finder: header found per partition
+    uint64_t find_parts = 0, find_part_bits = 0;
     double last_ms_find = 0, last_ms_count = 0, last_ms_emit = 0, last_ms_wall = 0;
     hipEvent_t ev[6] = {nullptr, nullptr, nullptr, nullptr, nullptr, nullptr};
     uint64_t repairs = 0, chains = 0, candidates = 0, resolved_groups = 0;
@@ -704,13 +829,13 @@ struct InflateScratch {
     uint64_t p_nbytes = 0;
     void release() {
         void** ps[] = {&d_in, &d_cand, &d_starts, &d_stops, &d_res, &d_cands, &d_stats, &d_q, &d_seg, &d_chains, &d_off,
-                       &d_ref, &d_pend, &d_rl, &d_ticket, &d_ph, &d_cticket, &d_out};
+                       &d_ref, &d_pend, &d_rl, &d_ticket, &d_ph, &d_cticket, &d_out, &d_done};
         for (void** p : ps) { if (*p) hipFree(*p); *p = nullptr; }
         for (auto& e : ev) { if (e) hipEventDestroy(e); e = nullptr; }
         if (h_cnt) hipHostFree(h_cnt);
         h_cnt = nullptr;
         d_in_cap = d_cand_cap = d_starts_cap = d_stops_cap = d_res_cap = d_cands_cap = d_seg_cap = d_q_cap = d_chains_cap = 0;
-        d_off_cap = d_ref_cap = d_pend_cap = d_rl_cap = d_out_cap = 0;
+        d_off_cap = d_ref_cap = d_pend_cap = d_rl_cap = d_out_cap = d_done_cap = 0;
         pending = false;
     }
 };
@@ -819,8 +944,8 @@ static int inflate_run(InflateScratch& S, hipStream_t s, const uint8_t* in, uint
         INF_CHK(hipMemsetAsync((char*)S.d_in + in_len, 0, nwords * 4 + IN_PAD - in_len, s));
         d_w = (const uint32_t*)S.d_in;
     }
-    if (!S.d_stats) INF_CHK(hipMalloc(&S.d_stats, 256));
-    INF_CHK(hipMemsetAsync(S.d_stats, 0, 256, s));
+    if (!S.d_stats) INF_CHK(hipMalloc(&S.d_stats, 512));
+    INF_CHK(hipMemsetAsync(S.d_stats, 0, 512, s));
     if (!S.ev[0]) for (auto& e : S.ev) INF_CHK(hipEventCreate(&e));
     const uint32_t nseg = (uint32_t)std::max<uint64_t>(1, (in_len + SEG_BYTES - 1) / SEG_BYTES);
     INF_CHK(inf_ensure(&S.d_cand, &S.d_cand_cap, (uint64_t)nseg * SEG_CAP * 8ull + (uint64_t)nseg * 4 + 64));
@@ -846,25 +971,70 @@ static int inflate_run(InflateScratch& S, hipStream_t s, const uint8_t* in, uint
         INF_CHK(inf_ensure(&S.d_q, &S.d_q_cap, (uint64_t)qcap * 8 + 64));
         uint32_t* d_qcount = (uint32_t*)S.d_stats + 8;
         uint64_t* d_qlist = (uint64_t*)((char*)S.d_q + 64);
-        if (nthr) {
+        static const uint32_t strict_grid = [] {
+            int dev = 0, ncu = 0, per = 0;
+            if (hipGetDevice(&dev) != hipSuccess ||
+                hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess ||
+                hipOccupancyMaxActiveBlocksPerMultiprocessor(&per, ndfl_inflate_strict_kernel, 256, 0) != hipSuccess ||
+                ncu <= 0 || per <= 0)
+                return 1280u;
+            return (uint32_t)(ncu * per);
+        }();
+        unsigned long long* sst = getenv("NDFL_STATS") ? (unsigned long long*)((uint32_t*)S.d_stats + 16) : nullptr;
+        // partitioned scan (opt-in, NDFL_FIND_PART_BITS = partition bits or "auto"): each partition is
+        // scanned only up to its first header, plus the rest of it where blocks are short or expensive.
+        // Not the default: a decode chain's cost goes with its blocks and output bytes, not its bits,
+        // and chains through partitions ran up to 20 ms against 4.5 ms for one block
+        const uint64_t wg_words = (uint64_t)FIND_WPT * 256;
+        uint64_t part_words = 0;
+        {
+            static const uint32_t count_waves = wave_grid(ndfl_inflate_count_wave_kernel, COUNT_WAVES, "NDFL_COUNT_WPC");
+            const char* pe = getenv("NDFL_FIND_PART_BITS");               // read per call (tests switch it)
+            if (pe && !strcmp(pe, "auto")) part_words = nw32 / (4ull * count_waves);
+            else if (pe) part_words = (uint64_t)strtoull(pe, nullptr, 10) / 32;
+            part_words = part_words / wg_words * wg_words;
+            if (part_words < 2 * wg_words || part_words >= nw32) part_words = 0;    // dense
+        }
+        S.find_parts = 0;
+        if (nthr && part_words) {
+            const uint64_t nparts = (nw32 + part_words - 1) / part_words;
+            if (nparts > 0x7FFFFFFFull) return -2;
+            INF_CHK(inf_ensure(&S.d_done, &S.d_done_cap, nparts * 8 + 64));
+            INF_CHK(hipMemsetAsync(S.d_done, 0, nparts * 4, s));
+            const uint32_t iters = (uint32_t)((part_words + wg_words - 1) / wg_words);
+            uint32_t* d_last = (uint32_t*)S.d_done + nparts;
+            for (uint32_t it = 0; it < iters; it++) {
+                INF_CHK(hipMemsetAsync(d_qcount, 0, 12, s));              // survivor count, (pad), strict ticket
+                hipLaunchKernelGGL(ndfl_inflate_find_sparse_kernel, dim3((uint32_t)nparts), dim3(256), 0, s, d_w, nwords,
+                                   nbits, d_qlist, d_qcount, qcap, w_lo, scan_end, (uint32_t)part_words, it,
+                                   (const uint32_t*)S.d_done, d_last);
+                INF_CHK(hipGetLastError());
+                hipLaunchKernelGGL(ndfl_inflate_strict_kernel, dim3(strict_grid), dim3(256), 0, s, d_w, nwords, nbits,
+                                   (const uint64_t*)d_qlist, (const uint32_t*)d_qcount, qcap, d_cnt, d_list,
+                                   (uint32_t*)S.d_stats + 10, sst, (uint32_t*)S.d_done, w_lo * 32, part_words * 32);
+                INF_CHK(hipGetLastError());
+            }
+            // short-block / expensive partitions: the rest of their windows
+            INF_CHK(hipMemsetAsync(d_qcount, 0, 12, s));
+            hipLaunchKernelGGL(ndfl_inflate_find_fill_kernel, dim3((uint32_t)(nparts * iters)), dim3(256), 0, s, d_w,
+                               nwords, nbits, d_qlist, d_qcount, qcap, w_lo, scan_end, (uint32_t)part_words, iters,
+                               (const uint32_t*)S.d_done, (const uint32_t*)d_last);
+            INF_CHK(hipGetLastError());
+            hipLaunchKernelGGL(ndfl_inflate_strict_kernel, dim3(strict_grid), dim3(256), 0, s, d_w, nwords, nbits,
+                               (const uint64_t*)d_qlist, (const uint32_t*)d_qcount, qcap, d_cnt, d_list,
+                               (uint32_t*)S.d_stats + 10, sst, (uint32_t*)nullptr, (uint64_t)0, (uint64_t)1);
+            INF_CHK(hipGetLastError());
+            S.find_parts = nparts;
+            S.find_part_bits = part_words * 32;
+        } else if (nthr) {
             const bool dense = nw32 <= (uint64_t)period;
             hipLaunchKernelGGL(ndfl_inflate_find_kernel, dim3((uint32_t)((nthr + 256 * FIND_WPT - 1) / (256 * FIND_WPT))), dim3(256), 0, s, d_w,
                                nwords, nbits, d_qlist, d_qcount, qcap, dense ? 1u : win, dense ? 1u : period, w_lo,
                                scan_end);
             INF_CHK(hipGetLastError());
-            static const uint32_t strict_grid = [] {
-                int dev = 0, ncu = 0, per = 0;
-                if (hipGetDevice(&dev) != hipSuccess ||
-                    hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess ||
-                    hipOccupancyMaxActiveBlocksPerMultiprocessor(&per, ndfl_inflate_strict_kernel, 256, 0) != hipSuccess ||
-                    ncu <= 0 || per <= 0)
-                    return 1280u;
-                return (uint32_t)(ncu * per);
-            }();
             hipLaunchKernelGGL(ndfl_inflate_strict_kernel, dim3(strict_grid), dim3(256), 0, s, d_w, nwords, nbits,
                                (const uint64_t*)d_qlist, (const uint32_t*)d_qcount, qcap, d_cnt, d_list,
-                               (uint32_t*)S.d_stats + 10,
-                               getenv("NDFL_STATS") ? (unsigned long long*)((uint32_t*)S.d_stats + 16) : nullptr);
+                               (uint32_t*)S.d_stats + 10, sst, (uint32_t*)nullptr, (uint64_t)0, (uint64_t)1);
             INF_CHK(hipGetLastError());
         }
     }
@@ -904,7 +1074,9 @@ static int inflate_run(InflateScratch& S, hipStream_t s, const uint8_t* in, uint
     // in `starts`), with room for repairs
     const uint64_t nslot = starts.size() + std::max<uint64_t>(4096, starts.size() / 2);
     const uint64_t nrec = std::min<uint64_t>(0xFFFFFFF0ull, 2 * starts.size() + nbits / (wv::MAX_SPAN / 2) + 65536);
-    const uint64_t seg_bytes = nrec * (64 * 8 + 64 * 4 + sizeof(SegMeta)) + nslot * 4;
+    // table records: at most one per block; bounded (a stream of tiny blocks parses the rest again)
+    const uint64_t nbt = std::min<uint64_t>(nrec, getenv("NDFL_NO_BT") ? 0 : (1u << 18));
+    const uint64_t seg_bytes = nrec * (64 * 8 + 64 * 4 + sizeof(SegMeta)) + nslot * 4 + 64 + nbt * BT_BYTES;
     INF_CHK(inf_ensure(&S.d_seg, &S.d_seg_cap, seg_bytes));
     SegPool pool;
     pool.start = (uint64_t*)S.d_seg;
@@ -912,6 +1084,9 @@ static int inflate_run(InflateScratch& S, hipStream_t s, const uint8_t* in, uint
     pool.meta = (SegMeta*)(pool.cnt + nrec * 64);
     pool.head = (uint32_t*)(pool.meta + nrec);
     pool.ctr = (uint32_t*)S.d_stats + 12;
+    pool.bctr = (uint32_t*)S.d_stats + 13;
+    pool.nbt = (uint32_t)nbt;
+    pool.bt = (char*)(((uintptr_t)(pool.head + nslot) + 63) & ~(uintptr_t)63);
     pool.nrec = (uint32_t)nrec;
     pool.nslot = nslot;
     S.pool = pool;
@@ -988,6 +1163,31 @@ static int inflate_run(InflateScratch& S, hipStream_t s, const uint8_t* in, uint
             if (j >= 1 && (linked(j) || res[j].status == ST_FINAL)) { *probe_sync = starts[j]; break; }
         }
         return 0;
+    }
+    if (getenv("NDFL_STATS") && !probe_sync && S.find_parts) {
+        unsigned long long sc[8];
+        INF_CHK(hipMemcpy(sc, (const uint32_t*)S.d_stats + 16, sizeof(sc), hipMemcpyDeviceToHost));
+        const uint64_t range_words = (std::min(end_bit, nbits) + 31) / 32 - (start_bit >> 5);
+        fprintf(stderr, "[ndfl] partitioned finder: %llu partitions of %llu bits, %.1f %% of the range scanned\n",
+                (unsigned long long)S.find_parts, (unsigned long long)S.find_part_bits,
+                range_words ? 100.0 * (double)sc[4] / (double)range_words : 0.0);
+    }
+    if (getenv("NDFL_STATS") && !probe_sync) {
+        // the most expensive chains (wave time, blocks, bits, output bytes)
+        std::vector<size_t> idx(res.size());
+        for (size_t k = 0; k < idx.size(); k++) idx[k] = k;
+        const size_t top = std::min<size_t>(8, idx.size());
+        std::partial_sort(idx.begin(), idx.begin() + top, idx.end(),
+                          [&](size_t a, size_t b) { return (res[a].pad >> 16) > (res[b].pad >> 16); });
+        for (size_t t = 0; t < top; t++) {
+            const ChainRes& r = res[idx[t]];
+            const uint64_t pk = S.find_parts ? (starts[idx[t]] - (start_bit & ~31ull)) / S.find_part_bits : 0;
+            fprintf(stderr, "[ndfl] count chain %zu: %.2f ms, %u blocks, start %llu, %llu bits, %llu bytes, status %u; "
+                    "partition %llu\n",
+                    idx[t], (r.pad >> 16) * 0.01, r.pad & 0xFFFFu, (unsigned long long)starts[idx[t]],
+                    (unsigned long long)(r.end_bit - starts[idx[t]]), (unsigned long long)r.out_count, r.status,
+                    (unsigned long long)pk);
+        }
     }
     {
         float a = 0, b = 0;
@@ -1081,8 +1281,10 @@ static int inflate_run(InflateScratch& S, hipStream_t s, const uint8_t* in, uint
                 "serial %.1f record %.1f build %.1f phase-mapped %.1f\n", t64[0] * 1e-5, t64[1] * 1e-5, t64[2] * 1e-5, t64[3] * 1e-5,
                 t64[4] * 1e-5, t64[5] * 1e-5, t64[6] * 1e-5, t64[7] * 1e-5);
         const double span = (double)(t64[9] - ~t64[10]);
-        fprintf(stderr, "[ndfl] count waves %llu: busy %.1f ms x waves, span %.3f ms, occupancy %.3f\n",
-                (unsigned long long)t64[11], t64[8] * 1e-5, span * 1e-5, t64[11] ? t64[8] / (span * t64[11]) : 0.0);
+        fprintf(stderr, "[ndfl] count waves %llu: busy %.1f ms x waves, span %.3f ms, occupancy %.3f, longest chain %.3f ms; "
+                "finder partitions %llu\n",
+                (unsigned long long)t64[11], t64[8] * 1e-5, span * 1e-5, t64[11] ? t64[8] / (span * t64[11]) : 0.0,
+                t64[12] * 1e-5, (unsigned long long)S.find_parts);
     }
     const uint64_t total = off - dict_len;
     ht[3] = hnow();
@@ -1117,7 +1319,7 @@ static int inflate_run(InflateScratch& S, hipStream_t s, const uint8_t* in, uint
     hipLaunchKernelGGL(ndfl_inflate_emit_wave_kernel, dim3(std::min<uint32_t>(nch, emit_grid)), dim3(64), 0, s, d_w,
                        nwords, nbits, (const EmitChain*)S.d_chains, nch, (uint32_t*)S.d_ticket, d_out,
                        (ChainRes*)S.d_res, (const uint64_t*)S.d_cands, ncand, (uint32_t*)S.d_ref, (uint32_t*)S.d_pend,
-                       pool, (wv::PhArr*)S.d_ph);
+                       pool, (wv::PhArr*)S.d_ph, stats_on ? (uint32_t*)S.d_stats : nullptr);
     INF_CHK(hipGetLastError());
     INF_CHK(hipEventRecord(e3, s));
     std::vector<ChainRes> er(nch);
@@ -1127,6 +1329,14 @@ static int inflate_run(InflateScratch& S, hipStream_t s, const uint8_t* in, uint
     float ms = 0;
     hipEventElapsedTime(&ms, e2, e3);
     S.last_ms_emit = ms;
+    if (stats_on) {
+        uint64_t t64[48];
+        INF_CHK(hipMemcpy(t64, (const char*)S.d_stats + 128, sizeof(t64), hipMemcpyDeviceToHost));
+        const double span = (double)(t64[17] - ~t64[18]);
+        fprintf(stderr, "[ndfl] emit waves %llu: busy %.1f ms x waves, span %.3f ms, occupancy %.3f, longest chain %.3f ms\n",
+                (unsigned long long)t64[19], t64[16] * 1e-5, span * 1e-5, t64[19] ? t64[16] / (span * t64[19]) : 0.0,
+                t64[20] * 1e-5);
+    }
     if (deferred) {
         S.pending = true;
         S.p_out = d_out; S.p_nbytes = nbytes;

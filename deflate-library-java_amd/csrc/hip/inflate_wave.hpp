@@ -1087,7 +1087,7 @@ ndfl_inflate_count_wave_kernel(const uint32_t* w, uint64_t nwords, uint64_t nbit
                                uint64_t limit, ChainRes* res, uint32_t* stats, uint64_t slot_base, SegPool pool,
                                uint32_t* ticket, wv::PhArr* ph_all, const uint32_t* order) {
     using namespace wv;
-    __shared__ Shared S;
+    __shared__ __attribute__((aligned(16))) Shared S;
     __shared__ Stage stg;
     __shared__ uint32_t s_ticket;
     const int lane = threadIdx.x;
@@ -1112,9 +1112,16 @@ ndfl_inflate_count_wave_kernel(const uint32_t* w, uint64_t nwords, uint64_t nbit
     PhaseClock* pc = nullptr;
 #endif
     uint64_t tb = pc ? wall_clock64() : 0;
+    const uint64_t t_chain = stats ? wall_clock64() : 0;
     CandCur cc;
-    cc.init(cands, ncand, start);
+    if (slot_base == 0 && c < ncand) {          // the first pass: chain c starts at candidate c (no search)
+        cc.c = cands; cc.n = ncand; cc.i = c; cc.v = cands[c];
+    } else {
+        cc.init(cands, ncand, start);
+    }
+    uint32_t nblk = 0;
     for (int blk = 0;; blk++) {
+        nblk = (uint32_t)blk;
         // a chain ends at the first later block boundary that is itself a header candidate (its own
         // chain links on from there) or at the range end; false candidates are passed over
         if (blk > 0 && (cur >= stop || cc.at(cur, &next_idx))) { status = ST_BOUNDARY; endpos = cur; break; }
@@ -1137,6 +1144,25 @@ ndfl_inflate_count_wave_kernel(const uint32_t* w, uint64_t nwords, uint64_t nbit
         if (pc) { const uint64_t x = wall_clock64(); pc->hdr += x - tb; tb = x; }
         const int te = build_tables(S, lane, ed);
         if (te) { status = ST_ERROR; reason = (uint32_t)te; endpos = d0; break; }
+        // the block's tables and header fields for the emit pass (a table record)
+        uint32_t brec = NOREC;
+        if (recording && pool.nbt) {
+            if (lane == 0) brec = atomicAdd(pool.bctr, 1u);
+            brec = __shfl(brec, 0, 64);
+            if (brec < pool.nbt) {
+                uint4* dst = (uint4*)(pool.bt + (uint64_t)brec * BT_BYTES);
+                const uint4* src = (const uint4*)&S.t;
+                for (uint32_t q = (uint32_t)lane; q < sizeof(Tabs) / 16; q += 64) dst[q] = src[q];
+                if (lane == 0) {
+                    uint64_t* h = (uint64_t*)(pool.bt + (uint64_t)brec * BT_BYTES + sizeof(Tabs));
+                    h[0] = cur; h[1] = d0;
+                    uint32_t* h32 = (uint32_t*)(h + 2);
+                    h32[0] = S.h_bfinal; h32[1] = S.h_btype; h32[2] = ed ? 1u : 0u; h32[3] = 0;
+                }
+            } else {
+                brec = NOREC;
+            }
+        }
         if (pc) { const uint64_t x = wall_clock64(); pc->build += x - tb; tb = x; }
         uint64_t rs = d0;
         bool block_done = false, chain_done = false;
@@ -1183,12 +1209,13 @@ ndfl_inflate_count_wave_kernel(const uint32_t* w, uint64_t nwords, uint64_t nbit
                     if (lane == 0) {
                         SegMeta m;
                         m.ft = ft; m.kind_ft = fk; m.reason_ft = fr; m.next = NOREC;
-                        m.end_ft = fe; m.exit63 = fe; m.pw = g.pw; m.pad = 0;
+                        m.end_ft = fe; m.exit63 = fe; m.pw = g.pw; m.pad = brec;
                         pool.meta[idx] = m;
                         if (prev_rec == NOREC) pool.head[slot_base + c] = idx;
                         else pool.meta[prev_rec].next = idx;
                     }
                     prev_rec = idx;
+                    brec = NOREC;               // (only the block's first round names its tables)
                 } else {
                     recording = false;          // the emit pass re-derives the remaining rounds
                 }
@@ -1214,7 +1241,9 @@ ndfl_inflate_count_wave_kernel(const uint32_t* w, uint64_t nwords, uint64_t nbit
     if (lane == 0) {
         ChainRes o;
         o.end_bit = endpos; o.out_count = total; o.status = status; o.reason = reason;
-        o.next = next_idx; o.pad = 0;
+        o.next = next_idx;
+        // NDFL_STATS: the chain's wave time (10 us units, 16 bits) and blocks (16 bits)
+        o.pad = stats ? (min((uint32_t)((wall_clock64() - t_chain) / 1000), 0xFFFFu) << 16) | min(nblk + 1, 0xFFFFu) : 0u;
         o.bnd_bit = 0; o.bnd_cnt = 0;
         res[c] = o;
         if (stats) {
@@ -1223,6 +1252,7 @@ ndfl_inflate_count_wave_kernel(const uint32_t* w, uint64_t nwords, uint64_t nbit
             atomicAdd(&st64[0], pcl.hdr); atomicAdd(&st64[1], pcl.spec); atomicAdd(&st64[2], pcl.verify);
             atomicAdd(&st64[3], pcl.phases); atomicAdd(&st64[4], pcl.serial); atomicAdd(&st64[5], pcl.rec);
             atomicAdd(&st64[6], pcl.build); atomicAdd(&st64[7], pcl.phmap);
+            atomicMax(&st64[12], (unsigned long long)(wall_clock64() - t_chain));
         }
     }
     }
@@ -1248,14 +1278,16 @@ ndfl_inflate_count_wave_kernel(const uint32_t* w, uint64_t nwords, uint64_t nbit
 extern "C" __global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(NDFL_EMIT_WAVES_PER_SIMD)))
 ndfl_inflate_emit_wave_kernel(const uint32_t* w, uint64_t nwords, uint64_t nbits, const EmitChain* chains,
                               uint32_t nlist, uint32_t* ticket, uint8_t* out, ChainRes* res, const uint64_t* cands,
-                              uint32_t ncand, uint32_t* ref, uint32_t* pend, SegPool pool, wv::PhArr* ph_all) {
+                              uint32_t ncand, uint32_t* ref, uint32_t* pend, SegPool pool, wv::PhArr* ph_all,
+                              uint32_t* stats) {
     using namespace wv;
-    __shared__ Shared S;
+    __shared__ __attribute__((aligned(16))) Shared S;
     __shared__ Stage stg;
     __shared__ uint32_t s_ticket;
     const int lane = threadIdx.x;
     gu8* gout = (gu8*)out;
     PhArr* S_ph = ph_all + blockIdx.x;
+    const uint64_t t_begin = stats ? wall_clock64() : 0;
     for (;;) {
     __syncthreads();
     if (lane == 0) s_ticket = atomicAdd(ticket, 1u);
@@ -1264,6 +1296,7 @@ ndfl_inflate_emit_wave_kernel(const uint32_t* w, uint64_t nwords, uint64_t nbits
     if (ci >= nlist) break;
     const In in{w, nwords, nbits};
     const EmitChain ch = chains[ci];
+    const uint64_t t_chain = stats ? wall_clock64() : 0;
     uint64_t cur = ch.start_bit, base = ch.out_off;
     uint32_t status = ST_BOUNDARY, reason = 0;
     uint64_t endpos = ch.start_bit;
@@ -1278,10 +1311,26 @@ ndfl_inflate_emit_wave_kernel(const uint32_t* w, uint64_t nwords, uint64_t nbits
     for (int blk = 0;; blk++) {
         if (blk > 0 && cur == ch.end_bit) { status = ST_BOUNDARY; endpos = cur; break; }
         bnd_bit = cur; bnd_out = base;
-        for (uint32_t s = (uint32_t)lane; s < 320; s += 64) S.lens[s] = 0;
-        __syncthreads();
-        if (lane == 0) parse_hdr(in, cur, S);
-        __syncthreads();
+        // the count pass's tables of this block, when its first round record names them
+        const char* btr = (rec != NOREC && pm.pad < pool.nbt) ? pool.bt + (uint64_t)pm.pad * BT_BYTES : nullptr;
+        if (btr && *(const uint64_t*)(btr + sizeof(Tabs)) != cur) btr = nullptr;     // (not this block)
+        if (btr) {
+            __syncthreads();                    // the previous block's table reads are done
+            const uint4* src = (const uint4*)btr;
+            uint4* dst = (uint4*)&S.t;
+            for (uint32_t q = (uint32_t)lane; q < sizeof(Tabs) / 16; q += 64) dst[q] = src[q];
+            if (lane == 0) {
+                const uint64_t* h = (const uint64_t*)(btr + sizeof(Tabs));
+                const uint32_t* h32 = (const uint32_t*)(h + 2);
+                S.h_err = 0; S.h_d0 = h[1]; S.h_bfinal = h32[0]; S.h_btype = h32[1]; S.h_len = h32[2];
+            }
+            __syncthreads();
+        } else {
+            for (uint32_t s = (uint32_t)lane; s < 320; s += 64) S.lens[s] = 0;
+            __syncthreads();
+            if (lane == 0) parse_hdr(in, cur, S);
+            __syncthreads();
+        }
         if (S.h_err) { status = ST_ERROR; reason = S.h_err; endpos = S.h_pos; break; }
         const uint64_t d0 = S.h_d0;
         const bool bfinal = S.h_bfinal != 0;
@@ -1300,8 +1349,12 @@ ndfl_inflate_emit_wave_kernel(const uint32_t* w, uint64_t nwords, uint64_t nbits
             continue;
         }
         bool ed;
-        const int te = build_tables(S, lane, ed);
-        if (te) { status = ST_ERROR; reason = (uint32_t)te; endpos = d0; break; }
+        if (btr) {
+            ed = S.h_len != 0;                  // (the loaded record's empty-distance flag)
+        } else {
+            const int te = build_tables(S, lane, ed);
+            if (te) { status = ST_ERROR; reason = (uint32_t)te; endpos = d0; break; }
+        }
         uint64_t rs = d0;
         bool block_done = false, chain_done = false;
         while (!block_done) {
@@ -1432,7 +1485,16 @@ ndfl_inflate_emit_wave_kernel(const uint32_t* w, uint64_t nwords, uint64_t nbits
         o.next = 0xFFFFFFFFu; o.pad = 0;
         o.bnd_bit = bnd_bit; o.bnd_cnt = bnd_out - ch.out_off;
         res[ci] = o;
+        if (stats) atomicMax((unsigned long long*)(stats + 32) + 20, (unsigned long long)(wall_clock64() - t_chain));
     }
+    }
+    if (stats && lane == 0) {                   // wave occupancy of the pass: busy sum, first start, last end
+        unsigned long long* st64 = (unsigned long long*)(stats + 32);
+        const uint64_t t_end = wall_clock64();
+        atomicAdd(&st64[16], t_end - t_begin);
+        atomicMax(&st64[17], t_end);
+        atomicMax(&st64[18], ~t_begin);
+        atomicAdd(&st64[19], 1ull);
     }
 }
 
