@@ -131,9 +131,13 @@ def main():
             t_c = ctx.timings()["deflate"]
             endbits = part.nbits
             cbytes = (endbits + 7) // 8
-            if gather:
-                state["stream"] = P.gather_stream(codec, dist, torch, part, rank, world, out=state.get("stream"))
+            # the gather runs on RCCL's stream while this rank decodes its own range (the parts it
+            # moves are final once deflate_shard returns); the step ends when both are done
+            pend = P.gather_stream(codec, dist, torch, part, rank, world, out=state.get("stream"),
+                                   async_op=True) if gather else None
             r, olen, dl = P.inflate_shard(codec, dist, torch, part, dec, rank, world)
+            if pend is not None:
+                state["stream"] = pend.wait()
             state["dict_len"] = dl
         if r != 0:
             raise RuntimeError(f"decode error {r}")

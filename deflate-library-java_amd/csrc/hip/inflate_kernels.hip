@@ -766,6 +766,161 @@ struct EmitChain {
     uint64_t slot;        // count-pass segment record of this chain (>= slot capacity: none)
 };
 
+// ---- device-side candidate list and chain linking (one host synchronization per decode) ----------
+// Link summary (DevLink::info, u64): the decode's results the host reads once at the end.
+enum : uint32_t { LI_NCAND = 0, LI_NCH, LI_TOTAL, LI_FLAGS, LI_STOP, LI_CODE, LI_OUTLEN, LI_CONSUMED, LI_NCAND_ALL,
+                  LI_LO, LI_WORDS = 16 };
+enum : uint64_t { LF_REPAIR = 1, LF_RANGE = 2, LF_CAPACITY = 4 };
+constexpr uint32_t NOLINK = 0xFFFFFFFFu;
+
+// Exclusive scan of the finder segments' candidate counts (capped at SEG_CAP) from 1 (slot 0 is
+// the range start): the compact kernel's offsets; info[LI_NCAND_ALL] = the list length.
+extern "C" __global__ void __launch_bounds__(1024)
+ndfl_inflate_segscan_kernel(const uint32_t* cnt, uint32_t nseg, uint64_t* segoff, uint64_t* info) {
+    using namespace inf;
+    __shared__ uint64_t sh[16];
+    const uint32_t per = (nseg + 1023) / 1024;
+    const uint32_t b0 = min(nseg, threadIdx.x * per), b1 = min(nseg, b0 + per);
+    uint64_t sum = 0;
+    for (uint32_t i = b0; i < b1; i++) sum += min(cnt[i], SEG_CAP);
+    uint64_t tot;
+    uint64_t run = 1 + block_excl_scan<uint64_t, 16>(sum, sh, tot);
+    for (uint32_t i = b0; i < b1; i++) { segoff[i] = run; run += min(cnt[i], SEG_CAP); }
+    if (threadIdx.x == 0) info[LI_NCAND_ALL] = 1 + tot;
+}
+
+// The chain starts: the range start, then the sorted candidates strictly inside (start, end) -- a
+// contiguous slice of the sorted list.  info[LI_NCAND] = their number.
+extern "C" __global__ void __launch_bounds__(256)
+ndfl_inflate_cand_slice_kernel(const uint64_t* sorted, uint64_t* info, uint64_t start_bit, uint64_t end_bit,
+                               uint64_t* cands) {
+    __shared__ uint64_t s_lo, s_hi;
+    const uint64_t na = info[LI_NCAND_ALL];
+    if (threadIdx.x == 0) {
+        uint64_t lo = 1, hi = na;                           // first index with value > start_bit
+        while (lo < hi) { const uint64_t m = (lo + hi) >> 1; if (sorted[m] <= start_bit) lo = m + 1; else hi = m; }
+        uint64_t lo2 = lo, hi2 = na;                        // first index with value >= end_bit
+        while (lo2 < hi2) { const uint64_t m = (lo2 + hi2) >> 1; if (sorted[m] < end_bit) lo2 = m + 1; else hi2 = m; }
+        s_lo = lo; s_hi = lo2;
+        if (blockIdx.x == 0) { info[LI_NCAND] = 1 + (lo2 - lo); info[LI_LO] = lo; cands[0] = start_bit; }
+    }
+    __syncthreads();
+    const uint64_t lo = s_lo, n = s_hi - s_lo;
+    for (uint64_t k = (uint64_t)blockIdx.x * 256 + threadIdx.x; k < n; k += (uint64_t)gridDim.x * 256)
+        cands[1 + k] = sorted[lo + k];
+}
+
+// Claim order of the count pass: longest first by the bits to the next start (24 buckets of 32
+// Kibit), so that no long chain is left for the end of the launch.  One workgroup.
+extern "C" __global__ void __launch_bounds__(1024)
+ndfl_inflate_order_kernel(const uint64_t* cands, uint32_t n, uint64_t end_bit, uint32_t* order) {
+    constexpr uint32_t NB = 24;
+    __shared__ uint32_t bc[NB + 1];
+    if (threadIdx.x <= NB) bc[threadIdx.x] = 0;
+    __syncthreads();
+    auto bucket = [&](uint32_t k) -> uint32_t {
+        const uint64_t nx = k + 1 < n ? cands[k + 1] : end_bit;
+        const uint64_t len = nx > cands[k] ? nx - cands[k] : 0;
+        return NB - 1 - (uint32_t)min<uint64_t>(NB - 1, len >> 15);
+    };
+    for (uint32_t k = threadIdx.x; k < n; k += blockDim.x) atomicAdd(&bc[bucket(k) + 1], 1u);
+    __syncthreads();
+    if (threadIdx.x == 0) for (uint32_t b = 0; b < NB; b++) bc[b + 1] += bc[b];
+    __syncthreads();
+    for (uint32_t k = threadIdx.x; k < n; k += blockDim.x) order[atomicAdd(&bc[bucket(k)], 1u)] = k;
+}
+
+// Linking by pointer jumping.  Chain k links to the chain starting where it stopped when it stopped
+// at a block boundary that is the next candidate (res[k].next), before the range end; the links form
+// a forest (a false candidate's chain may end on a real boundary too).  Init: J0 = the link, S = the
+// chain's output bytes, D = 1 if linked.
+extern "C" __global__ void __launch_bounds__(256)
+ndfl_inflate_link_init_kernel(const ChainRes* res, uint32_t n, const uint64_t* cands, uint64_t end_bit, uint32_t* J0,
+                              uint64_t* S, uint32_t* D) {
+    using namespace inf;
+    for (uint32_t k = blockIdx.x * 256 + threadIdx.x; k < n; k += gridDim.x * 256) {
+        const ChainRes r = res[k];
+        const bool lk = r.status == ST_BOUNDARY && r.end_bit < end_bit && r.next < n && cands[r.next] == r.end_bit;
+        J0[k] = lk ? r.next : NOLINK;
+        S[k] = r.out_count;
+        D[k] = lk ? 1u : 0u;
+    }
+}
+// One doubling round: J_{r+1} = J_r o J_r, S and D summed along (double-buffered).
+extern "C" __global__ void __launch_bounds__(256)
+ndfl_inflate_link_jump_kernel(const uint32_t* J, uint32_t* J2, const uint64_t* S, uint64_t* S2, const uint32_t* D,
+                              uint32_t* D2, uint32_t n) {
+    for (uint32_t k = blockIdx.x * 256 + threadIdx.x; k < n; k += gridDim.x * 256) {
+        const uint32_t j = J[k];
+        if (j != NOLINK) { J2[k] = J[j]; S2[k] = S[k] + S[j]; D2[k] = D[k] + D[j]; }
+        else { J2[k] = NOLINK; S2[k] = S[k]; D2[k] = D[k]; }
+    }
+}
+// The chain list from the range start: position t is the chain t links away from chain 0
+// (binary lifting over the J levels), its output offset dict_len + S[0] - S[node].  The terminal
+// chain sets the summary: chains, total bytes, the stop bit, flags (a boundary that is no
+// candidate: repair on the host; the range end inside a block; output beyond out_cap).
+extern "C" __global__ void __launch_bounds__(256)
+ndfl_inflate_link_path_kernel(const uint32_t* Jall, uint32_t nlev, const uint64_t* S, const uint32_t* D,
+                              const ChainRes* res, const uint64_t* cands, uint32_t n, uint64_t dict_len, uint64_t end_bit,
+                              uint64_t out_cap, EmitChain* chains, uint64_t* info) {
+    using namespace inf;
+    const uint32_t len = D[0] + 1;
+    for (uint32_t t = blockIdx.x * 256 + threadIdx.x; t < len; t += gridDim.x * 256) {
+        uint32_t node = 0;
+        for (uint32_t r = 0; r < nlev; r++)
+            if ((t >> r) & 1u) node = Jall[(uint64_t)r * n + node];
+        const ChainRes c = res[node];
+        EmitChain e;
+        e.start_bit = cands[node];
+        e.end_bit = c.end_bit;
+        e.out_off = dict_len + S[0] - S[node];
+        e.out_count = c.out_count;
+        e.slot = node;
+        chains[t] = e;
+        if (t + 1 == len) {
+            uint64_t flags = 0, stop = 0;
+            if (c.status == ST_FINAL) stop = c.end_bit;
+            else if (c.status == ST_BOUNDARY) {
+                if (c.end_bit == end_bit) stop = end_bit;
+                else if (c.end_bit > end_bit) flags |= LF_RANGE;
+                else flags |= LF_REPAIR;
+            }
+            if (S[0] > out_cap) flags |= LF_CAPACITY;
+            info[LI_NCH] = len; info[LI_TOTAL] = S[0]; info[LI_FLAGS] = flags; info[LI_STOP] = stop;
+        }
+    }
+}
+// The decode's result from the emit pass's chain results: the first error in stream order (a
+// partial-input decode that ran out of input inside a block stops at that block's start instead).
+extern "C" __global__ void __launch_bounds__(1024)
+ndfl_inflate_summary_kernel(const ChainRes* er, const EmitChain* chains, uint64_t* info, uint64_t dict_len,
+                            uint32_t partial) {
+    using namespace inf;
+    __shared__ uint32_t first;
+    if (threadIdx.x == 0) first = NOLINK;
+    __syncthreads();
+    const uint32_t nch = (uint32_t)info[LI_NCH];
+    for (uint32_t k = threadIdx.x; k < nch; k += blockDim.x)
+        if (er[k].status == ST_ERROR) atomicMin(&first, k);
+    __syncthreads();
+    if (threadIdx.x != 0) return;
+    if (first == NOLINK) {
+        info[LI_CODE] = 0; info[LI_OUTLEN] = info[LI_TOTAL]; info[LI_CONSUMED] = info[LI_STOP];
+        return;
+    }
+    const ChainRes r = er[first];
+    if (partial && r.reason == R_UEOS) {
+        info[LI_CODE] = NEED_INPUT;
+        info[LI_OUTLEN] = chains[first].out_off - dict_len + r.bnd_cnt;
+        info[LI_CONSUMED] = r.bnd_bit;
+    } else {
+        info[LI_CODE] = r.reason;
+        info[LI_OUTLEN] = chains[first].out_off - dict_len + r.out_count;
+        info[LI_CONSUMED] = r.end_bit;
+    }
+}
+
 // Count-pass records of every round of a chain: each lane's exact segment, so the emit pass
 // decodes each segment once instead of re-running the speculation.  Records come from a pool and
 // are linked per chain in decode order (chain slot -> head record -> next ...).
@@ -822,6 +977,9 @@ struct InflateScratch {
     hipEvent_t ev[6] = {nullptr, nullptr, nullptr, nullptr, nullptr, nullptr};
     uint64_t repairs = 0, chains = 0, candidates = 0, resolved_groups = 0;
     void* h_cnt = nullptr;                            // pinned: resolve list size
+    void* d_info = nullptr;                           // device-side linking: summary (LI_*)
+    void* h_info = nullptr;                           //   and its pinned host copy
+    void* d_link = nullptr; size_t d_link_cap = 0;    //   pointer-jumping levels and sums
     bool count_first = false;
     // state kept for ndfl_inflate_resolve after a deferred-window range decode
     bool pending = false;
@@ -834,6 +992,12 @@ struct InflateScratch {
         for (auto& e : ev) { if (e) hipEventDestroy(e); e = nullptr; }
         if (h_cnt) hipHostFree(h_cnt);
         h_cnt = nullptr;
+        if (h_info) hipHostFree(h_info);
+        h_info = nullptr;
+        if (d_info) hipFree(d_info);
+        d_info = nullptr;
+        if (d_link) hipFree(d_link);
+        d_link = nullptr; d_link_cap = 0;
         d_in_cap = d_cand_cap = d_starts_cap = d_stops_cap = d_res_cap = d_cands_cap = d_seg_cap = d_q_cap = d_chains_cap = 0;
         d_off_cap = d_ref_cap = d_pend_cap = d_rl_cap = d_out_cap = d_done_cap = 0;
         pending = false;
@@ -862,7 +1026,11 @@ static hipError_t inf_ensure(void** p, size_t* cap, size_t n) {
 }
 
 
-#define INF_CHK(x) do { hipError_t _e = (x); if (_e != hipSuccess) return -4; } while (0)
+static bool inf_debug() { static const bool d = getenv("NDFL_DEBUG") != nullptr; return d; }
+#define INF_CHK(x) do { hipError_t _e = (x); if (_e != hipSuccess) {                                             \
+        if (inf_debug()) fprintf(stderr, "[ndfl] HIP error %d (%s) at inflate_kernels.hip:%d\n", (int)_e,     \
+                                 hipGetErrorString(_e), __LINE__);                                              \
+        return -4; } } while (0)
 
 // Resolve the deferred copies of an emit pass: pointer-jumping rounds over the pending 32-byte
 // groups of out[0, nbytes) until none is left.  *groups = pending groups at the start.
@@ -882,6 +1050,7 @@ static int resolve_rounds(InflateScratch& S, hipStream_t s, uint8_t* d_out, uint
     hipLaunchKernelGGL(ndfl_inflate_pending_list_kernel, dim3((uint32_t)((npw + 4095) / 4096)), dim3(256), 0, s,
                        (const uint32_t*)pend, (uint64_t)0, npw, lst[0], cnt);
     INF_CHK(hipGetLastError());
+    if (!S.h_cnt) INF_CHK(hipHostMalloc(&S.h_cnt, 64, 0));
     uint32_t* h = (uint32_t*)S.h_cnt;
     // rounds are queued four at a time on grid-stride kernels; the host reads the list size between
     // batches only (pointer jumping needs ~log2(reference depth) rounds)
@@ -911,6 +1080,232 @@ static int resolve_rounds(InflateScratch& S, hipStream_t s, uint8_t* d_out, uint
         INF_CHK(hipGetLastError());
         cur ^= 1;
     }
+}
+
+// Segment-record pool for `nstarts` chain starts (SegPool): the rounds of all chains, one head per
+// counted chain start, with room for repairs, and the per-block table records.
+static int setup_pool(InflateScratch& S, hipStream_t s, uint64_t nstarts, uint64_t nbits) {
+    using namespace inf;
+    const uint64_t nslot = nstarts + std::max<uint64_t>(4096, nstarts / 2);
+    const uint64_t nrec = std::min<uint64_t>(0xFFFFFFF0ull, 2 * nstarts + nbits / (wv::MAX_SPAN / 2) + 65536);
+    // table records: at most one per block; bounded (a stream of tiny blocks parses the rest again)
+    const uint64_t nbt = std::min<uint64_t>(nrec, getenv("NDFL_NO_BT") ? 0 : (1u << 18));
+    const uint64_t seg_bytes = nrec * (64 * 8 + 64 * 4 + sizeof(SegMeta)) + nslot * 4 + 64 + nbt * BT_BYTES;
+    INF_CHK(inf_ensure(&S.d_seg, &S.d_seg_cap, seg_bytes));
+    SegPool pool;
+    pool.start = (uint64_t*)S.d_seg;
+    pool.cnt = (uint32_t*)(pool.start + nrec * 64);
+    pool.meta = (SegMeta*)(pool.cnt + nrec * 64);
+    pool.head = (uint32_t*)(pool.meta + nrec);
+    pool.ctr = (uint32_t*)S.d_stats + 12;
+    pool.bctr = (uint32_t*)S.d_stats + 13;
+    pool.nbt = (uint32_t)nbt;
+    pool.bt = (char*)(((uintptr_t)(pool.head + nslot) + 63) & ~(uintptr_t)63);
+    pool.nrec = (uint32_t)nrec;
+    pool.nslot = nslot;
+    S.pool = pool;
+    INF_CHK(hipMemsetAsync(pool.head, 0xFF, nslot * 4, s));
+    return 0;
+}
+
+// Queue `rounds` resolve rounds without reading anything back (the kernels read the list sizes on
+// the device; a round with nothing pending costs two empty launches).  *cnt_slot = where the size of
+// the list left after them is (cnt + cur).
+static int resolve_rounds_dev(InflateScratch& S, hipStream_t s, uint8_t* d_out, uint64_t nbytes, int rounds,
+                              uint32_t** left, uint64_t* first_count_dst) {
+    using namespace inf;
+    const uint64_t npw = (nbytes + 31) / 32;
+    *left = nullptr;
+    if (npw == 0) return 0;
+    if (npw > 0xFFFFFFFFull) return -2;
+    INF_CHK(inf_ensure(&S.d_rl, &S.d_rl_cap, npw * 12 + 64));
+    uint32_t* cnt = (uint32_t*)S.d_rl;
+    uint32_t* lst[2] = {(uint32_t*)((char*)S.d_rl + 64), (uint32_t*)((char*)S.d_rl + 64) + npw};
+    uint32_t* nb = lst[1] + npw;
+    uint32_t* pend = (uint32_t*)S.d_pend;
+    uint32_t* ref = (uint32_t*)S.d_ref;
+    INF_CHK(hipMemsetAsync(cnt, 0, 8, s));
+    hipLaunchKernelGGL(ndfl_inflate_pending_list_kernel, dim3((uint32_t)((npw + 4095) / 4096)), dim3(256), 0, s,
+                       (const uint32_t*)pend, (uint64_t)0, npw, lst[0], cnt);
+    INF_CHK(hipGetLastError());
+    if (first_count_dst) INF_CHK(hipMemcpyAsync(first_count_dst, cnt, 4, hipMemcpyDeviceToDevice, s));
+    int cur = 0;
+    for (int round = 0; round < rounds; round++) {
+        INF_CHK(hipMemsetAsync(cnt + (cur ^ 1), 0, 4, s));
+        hipLaunchKernelGGL(ndfl_inflate_resolve_kernel, dim3(4096), dim3(256), 0, s, (const uint32_t*)lst[cur],
+                           (const uint32_t*)(cnt + cur), (const uint32_t*)pend, ref, d_out, nb);
+        INF_CHK(hipGetLastError());
+        hipLaunchKernelGGL(ndfl_inflate_resolve_apply_kernel, dim3(1024), dim3(256), 0, s, (const uint32_t*)lst[cur],
+                           (const uint32_t*)(cnt + cur), pend, (const uint32_t*)nb, lst[cur ^ 1], cnt + (cur ^ 1),
+                           (uint32_t*)nullptr);
+        INF_CHK(hipGetLastError());
+        cur ^= 1;
+    }
+    *left = cnt + cur;
+    return 0;
+}
+
+constexpr int LINK_FALLBACK = 1000;      // the device-side path hands over to the host path
+
+// The decode after the header finder with everything on the device and ONE host synchronization
+// in the middle (the number of chain starts, which sizes the record pool and the grids) and one at
+// the end (the summary): candidate list (segment scan, compaction, the range's slice), the count
+// pass in longest-first order, chain linking by pointer jumping, the emit pass, the first error,
+// the resolve rounds.  Returns LINK_FALLBACK when the host's linking has to step in (a chain that
+// stopped at a boundary that is no candidate) -- the host path then starts over from the finder's
+// candidates -- or when the list of chain starts is too long for the jump tables.
+static int inflate_devlink(InflateScratch& S, hipStream_t s, const uint32_t* d_w, uint64_t nwords, uint64_t nbits,
+                           uint32_t nseg, const uint32_t* d_cnt, const uint64_t* d_list, uint64_t start_bit,
+                           uint64_t end_bit, uint8_t* out, uint64_t dict_len, uint64_t out_cap, uint64_t* out_len,
+                           uint64_t* consumed_bits, uint32_t flags, bool deferred, bool partial, double* last_ms) {
+    using namespace inf;
+    if (!S.d_info) INF_CHK(hipMalloc(&S.d_info, LI_WORDS * 8));
+    if (!S.h_info) INF_CHK(hipHostMalloc(&S.h_info, LI_WORDS * 8, 0));
+    uint64_t* info = (uint64_t*)S.d_info;
+    volatile uint64_t* hinfo = (volatile uint64_t*)S.h_info;
+    INF_CHK(hipMemsetAsync(info, 0, LI_WORDS * 8, s));
+    const uint64_t cap_all = (uint64_t)nseg * SEG_CAP + 1;      // the sorted list's length at most
+    INF_CHK(inf_ensure(&S.d_starts, &S.d_starts_cap, (cap_all + nseg + 2) * 8));
+    uint64_t* d_sorted = (uint64_t*)S.d_starts;
+    uint64_t* d_segoff = d_sorted + cap_all;
+    hipLaunchKernelGGL(ndfl_inflate_segscan_kernel, dim3(1), dim3(1024), 0, s, d_cnt, nseg, d_segoff, info);
+    INF_CHK(hipGetLastError());
+    hipLaunchKernelGGL(ndfl_inflate_compact_kernel, dim3((nseg + 255) / 256), dim3(256), 0, s, d_cnt, d_list,
+                       (const uint64_t*)d_segoff, nseg, d_sorted);
+    INF_CHK(hipGetLastError());
+    INF_CHK(inf_ensure(&S.d_cands, &S.d_cands_cap, (cap_all + 1) * 8ull));
+    hipLaunchKernelGGL(ndfl_inflate_cand_slice_kernel, dim3((uint32_t)std::min<uint64_t>(4096, (cap_all + 255) / 256)),
+                       dim3(256), 0, s, (const uint64_t*)d_sorted, info, start_bit, end_bit, (uint64_t*)S.d_cands);
+    INF_CHK(hipGetLastError());
+    INF_CHK(hipMemcpyAsync((void*)hinfo, info, 8, hipMemcpyDeviceToHost, s));
+    INF_CHK(hipStreamSynchronize(s));                          // (1) the number of chain starts
+    const uint64_t n = hinfo[LI_NCAND];
+    if (n == 0 || n > (1ull << 24)) return LINK_FALLBACK;
+    const uint32_t ncand = (uint32_t)n;
+    int rc = setup_pool(S, s, n, nbits);
+    if (rc) return rc;
+    // count pass, longest chains first
+    INF_CHK(inf_ensure(&S.d_stops, &S.d_stops_cap, n * 12));
+    INF_CHK(inf_ensure(&S.d_res, &S.d_res_cap, n * sizeof(ChainRes)));
+    uint32_t* d_order = (uint32_t*)((char*)S.d_stops + n * 8);
+    hipLaunchKernelGGL(ndfl_inflate_order_kernel, dim3(1), dim3(1024), 0, s, (const uint64_t*)S.d_cands, ncand, end_bit,
+                       d_order);
+    INF_CHK(hipGetLastError());
+    if (!S.d_ph) INF_CHK(hipMalloc(&S.d_ph, (size_t)std::max(COUNT_WAVES, EMIT_WAVES) * sizeof(wv::PhArr)));
+    if (!S.d_cticket) INF_CHK(hipMalloc(&S.d_cticket, 64));
+    INF_CHK(hipMemsetAsync(S.d_cticket, 0, 4, s));
+    static const bool stats_on = getenv("NDFL_STATS") != nullptr;
+    const uint64_t limit = std::min(end_bit, nbits);
+    INF_CHK(hipEventRecord(S.ev[2], s));
+    static const uint32_t count_grid = wave_grid(ndfl_inflate_count_wave_kernel, COUNT_WAVES, "NDFL_COUNT_WPC");
+    hipLaunchKernelGGL(ndfl_inflate_count_wave_kernel, dim3(std::min<uint32_t>(ncand, count_grid)), dim3(64), 0, s,
+                       d_w, nwords, nbits, (const uint64_t*)S.d_cands, (const uint64_t*)nullptr, ncand,
+                       (const uint64_t*)S.d_cands, ncand, limit, (ChainRes*)S.d_res,
+                       stats_on ? (uint32_t*)S.d_stats : nullptr, (uint64_t)0, S.pool, (uint32_t*)S.d_cticket,
+                       (wv::PhArr*)S.d_ph, (const uint32_t*)d_order, end_bit);
+    INF_CHK(hipGetLastError());
+    INF_CHK(hipEventRecord(S.ev[3], s));
+    // linking: J levels (u32), S and D double-buffered
+    uint32_t nlev = 1;
+    while ((1ull << nlev) < n) nlev++;
+    const size_t link_bytes = (size_t)(nlev + 1) * n * 4 + 2 * n * 8 + 2 * n * 4 + 64;
+    INF_CHK(inf_ensure(&S.d_link, &S.d_link_cap, link_bytes));
+    uint32_t* J = (uint32_t*)S.d_link;
+    uint64_t* Ssum[2] = {(uint64_t*)(((uintptr_t)(J + (size_t)(nlev + 1) * n) + 7) & ~(uintptr_t)7), nullptr};
+    Ssum[1] = Ssum[0] + n;
+    uint32_t* Dd[2] = {(uint32_t*)(Ssum[1] + n), nullptr};
+    Dd[1] = Dd[0] + n;
+    const uint32_t lg = (uint32_t)std::min<uint64_t>(4096, (n + 255) / 256);
+    hipLaunchKernelGGL(ndfl_inflate_link_init_kernel, dim3(lg), dim3(256), 0, s, (const ChainRes*)S.d_res, ncand,
+                       (const uint64_t*)S.d_cands, end_bit, J, Ssum[0], Dd[0]);
+    INF_CHK(hipGetLastError());
+    int cur = 0;
+    for (uint32_t r = 0; r < nlev; r++) {
+        hipLaunchKernelGGL(ndfl_inflate_link_jump_kernel, dim3(lg), dim3(256), 0, s, (const uint32_t*)(J + (size_t)r * n),
+                           J + (size_t)(r + 1) * n, (const uint64_t*)Ssum[cur], Ssum[cur ^ 1], (const uint32_t*)Dd[cur],
+                           Dd[cur ^ 1], ncand);
+        INF_CHK(hipGetLastError());
+        cur ^= 1;
+    }
+    INF_CHK(inf_ensure(&S.d_chains, &S.d_chains_cap, n * sizeof(EmitChain)));
+    hipLaunchKernelGGL(ndfl_inflate_link_path_kernel, dim3(lg), dim3(256), 0, s, (const uint32_t*)J, nlev,
+                       (const uint64_t*)Ssum[cur], (const uint32_t*)Dd[cur], (const ChainRes*)S.d_res,
+                       (const uint64_t*)S.d_cands, ncand, dict_len, end_bit, out_cap, (EmitChain*)S.d_chains, info);
+    INF_CHK(hipGetLastError());
+    // emit into the output (or a device staging buffer sized by the bound out_cap)
+    uint8_t* d_out;
+    const bool direct = (flags & 2u) != 0;
+    // the output's size is known on the device only: the scratch (back-references, pending bits,
+    // a staging copy) is sized by out_cap, capped at DEFLATE's largest expansion (258 bytes per 2 bits)
+    const uint64_t obytes = dict_len + std::min<uint64_t>(out_cap, 129 * nbits + 65536);
+    if (obytes > (40ull << 30)) return LINK_FALLBACK;          // (the host path sizes it exactly)
+    if (direct) d_out = out;
+    else {
+        INF_CHK(inf_ensure(&S.d_out, &S.d_out_cap, obytes + 64));
+        d_out = (uint8_t*)S.d_out;
+        if (dict_len) INF_CHK(hipMemcpyAsync(d_out, out, dict_len, hipMemcpyHostToDevice, s));
+    }
+    const uint64_t nbytes = obytes;
+    if ((nbytes + 31) / 32 > 0xFFFFFFFFull) return LINK_FALLBACK;
+    const uint64_t npw = (nbytes + 31) / 32;
+    INF_CHK(inf_ensure(&S.d_ref, &S.d_ref_cap, nbytes * 4 + 64));
+    INF_CHK(inf_ensure(&S.d_pend, &S.d_pend_cap, npw * 4 + 64));
+    INF_CHK(hipMemsetAsync(S.d_pend, 0, npw * 4 + 64, s));
+    if (!S.d_ticket) INF_CHK(hipMalloc(&S.d_ticket, 64));
+    INF_CHK(hipMemsetAsync(S.d_ticket, 0, 64, s));
+    INF_CHK(hipEventRecord(S.ev[4], s));
+    static const uint32_t emit_grid = wave_grid(ndfl_inflate_emit_wave_kernel, EMIT_WAVES, "NDFL_EMIT_WPC");
+    hipLaunchKernelGGL(ndfl_inflate_emit_wave_kernel, dim3(std::min<uint32_t>(ncand, emit_grid)), dim3(64), 0, s, d_w,
+                       nwords, nbits, (const EmitChain*)S.d_chains, ncand, (uint32_t*)S.d_ticket, d_out,
+                       (ChainRes*)S.d_res, (const uint64_t*)S.d_cands, ncand, (uint32_t*)S.d_ref, (uint32_t*)S.d_pend,
+                       S.pool, (wv::PhArr*)S.d_ph, stats_on ? (uint32_t*)S.d_stats : nullptr, (const uint64_t*)info);
+    INF_CHK(hipGetLastError());
+    INF_CHK(hipEventRecord(S.ev[5], s));
+    hipLaunchKernelGGL(ndfl_inflate_summary_kernel, dim3(1), dim3(1024), 0, s, (const ChainRes*)S.d_res,
+                       (const EmitChain*)S.d_chains, info, dict_len, partial ? 1u : 0u);
+    INF_CHK(hipGetLastError());
+    // the resolve rounds, as far as they usually go, without a host read in between
+    uint32_t* left = nullptr;
+    if (!deferred) {
+        rc = resolve_rounds_dev(S, s, d_out, nbytes, 6, &left, (uint64_t*)nullptr);
+        if (rc) return rc;
+        if (left) INF_CHK(hipMemcpyAsync(info + LI_WORDS - 1, left, 4, hipMemcpyDeviceToDevice, s));
+    }
+    INF_CHK(hipMemcpyAsync((void*)hinfo, info, LI_WORDS * 8, hipMemcpyDeviceToHost, s));
+    INF_CHK(hipStreamSynchronize(s));                          // (2) the summary
+    const uint64_t lflags = hinfo[LI_FLAGS];
+    if (lflags & LF_REPAIR) return LINK_FALLBACK;
+    if (lflags & LF_RANGE) return -1;                          // the range end is no block boundary
+    S.chains = hinfo[LI_NCH];
+    S.candidates = ncand;
+    S.repairs = 0;
+    if (lflags & LF_CAPACITY) { *out_len = hinfo[LI_TOTAL]; return -3; }
+    const uint32_t pending_left = (uint32_t)(hinfo[LI_WORDS - 1] & 0xFFFFFFFFu);
+    if (!deferred && pending_left) {
+        uint64_t groups = 0;
+        rc = resolve_rounds(S, s, d_out, nbytes, &groups);     // (the rest, with the host's checks)
+        if (rc) return rc;
+    }
+    {
+        float a = 0, b = 0, c = 0;
+        hipEventElapsedTime(&a, S.ev[0], S.ev[1]);
+        hipEventElapsedTime(&b, S.ev[2], S.ev[3]);
+        hipEventElapsedTime(&c, S.ev[4], S.ev[5]);
+        S.last_ms_find = a; S.last_ms_count = b; S.last_ms_emit = c;
+    }
+    if (deferred) { S.pending = true; S.p_out = d_out; S.p_nbytes = dict_len + hinfo[LI_TOTAL]; }
+    INF_CHK(hipEventRecord(S.ev[5], s));
+    INF_CHK(hipStreamSynchronize(s));
+    float w = 0;
+    hipEventElapsedTime(&w, S.ev[0], S.ev[5]);
+    S.last_ms_wall = w;
+    *last_ms = w;
+    const int code = (int)hinfo[LI_CODE];
+    const uint64_t produced = hinfo[LI_OUTLEN];
+    if (!direct && produced) INF_CHK(hipMemcpy(out + dict_len, d_out + dict_len, produced, hipMemcpyDeviceToHost));
+    *out_len = produced;
+    *consumed_bits = hinfo[LI_CONSUMED];
+    return code;
 }
 
 // Decode one raw DEFLATE stream, or the block-aligned range [start_bit, end_bit) of one.
@@ -1039,6 +1434,15 @@ static int inflate_run(InflateScratch& S, hipStream_t s, const uint8_t* in, uint
         }
     }
     INF_CHK(hipEventRecord(S.ev[1], s));
+    // the device-side path (NDFL_HOST_LINK selects the host's linking); sync probes keep the host's
+    {
+        static const bool host_link = getenv("NDFL_HOST_LINK") != nullptr;
+        if (!probe_sync && !host_link) {
+            const int rc = inflate_devlink(S, s, d_w, nwords, nbits, nseg, d_cnt, d_list, start_bit, end_bit, out,
+                                           dict_len, out_cap, out_len, consumed_bits, flags, deferred, partial, last_ms);
+            if (rc != LINK_FALLBACK) return rc;
+        }
+    }
     std::vector<uint32_t> hcnt(nseg);
     INF_CHK(hipMemcpyAsync(hcnt.data(), d_cnt, nseg * 4ull, hipMemcpyDeviceToHost, s));
     INF_CHK(hipStreamSynchronize(s));
@@ -1135,7 +1539,8 @@ static int inflate_run(InflateScratch& S, hipStream_t s, const uint8_t* in, uint
                            d_w, nwords, nbits,
                            (const uint64_t*)S.d_starts, (const uint64_t*)S.d_stops, (uint32_t)n,
                            (const uint64_t*)S.d_cands, ncand, limit, (ChainRes*)S.d_res, stats_on ? (uint32_t*)S.d_stats : nullptr,
-                           slot_base, pool, (uint32_t*)S.d_cticket, (wv::PhArr*)S.d_ph, (const uint32_t*)d_order);
+                           slot_base, pool, (uint32_t*)S.d_cticket, (wv::PhArr*)S.d_ph, (const uint32_t*)d_order,
+                           end_bit);
         INF_CHK(hipGetLastError());
         if (S.count_first) { INF_CHK(hipEventRecord(S.ev[3], s)); S.count_first = false; }
         r.resize(n);
@@ -1319,7 +1724,7 @@ static int inflate_run(InflateScratch& S, hipStream_t s, const uint8_t* in, uint
     hipLaunchKernelGGL(ndfl_inflate_emit_wave_kernel, dim3(std::min<uint32_t>(nch, emit_grid)), dim3(64), 0, s, d_w,
                        nwords, nbits, (const EmitChain*)S.d_chains, nch, (uint32_t*)S.d_ticket, d_out,
                        (ChainRes*)S.d_res, (const uint64_t*)S.d_cands, ncand, (uint32_t*)S.d_ref, (uint32_t*)S.d_pend,
-                       pool, (wv::PhArr*)S.d_ph, stats_on ? (uint32_t*)S.d_stats : nullptr);
+                       pool, (wv::PhArr*)S.d_ph, stats_on ? (uint32_t*)S.d_stats : nullptr, (const uint64_t*)nullptr);
     INF_CHK(hipGetLastError());
     INF_CHK(hipEventRecord(e3, s));
     std::vector<ChainRes> er(nch);

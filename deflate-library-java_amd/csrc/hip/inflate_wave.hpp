@@ -1085,7 +1085,7 @@ extern "C" __global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per
 ndfl_inflate_count_wave_kernel(const uint32_t* w, uint64_t nwords, uint64_t nbits, const uint64_t* starts,
                                const uint64_t* stops, uint32_t nchains, const uint64_t* cands, uint32_t ncand,
                                uint64_t limit, ChainRes* res, uint32_t* stats, uint64_t slot_base, SegPool pool,
-                               uint32_t* ticket, wv::PhArr* ph_all, const uint32_t* order) {
+                               uint32_t* ticket, wv::PhArr* ph_all, const uint32_t* order, uint64_t stop_all) {
     using namespace wv;
     __shared__ __attribute__((aligned(16))) Shared S;
     __shared__ Stage stg;
@@ -1100,7 +1100,7 @@ ndfl_inflate_count_wave_kernel(const uint32_t* w, uint64_t nwords, uint64_t nbit
     __syncthreads();
     if (s_ticket >= nchains) break;
     const uint32_t c = order[s_ticket];
-    const uint64_t start = starts[c], stop = stops[c];
+    const uint64_t start = starts[c], stop = stops ? stops[c] : stop_all;
     uint64_t cur = start, total = 0, endpos = start;
     uint32_t status = ST_BOUNDARY, reason = 0, nslow = 0, nfix = 0, nround = 0, next_idx = 0xFFFFFFFFu;
     bool recording = slot_base + c < pool.nslot;
@@ -1279,7 +1279,7 @@ extern "C" __global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per
 ndfl_inflate_emit_wave_kernel(const uint32_t* w, uint64_t nwords, uint64_t nbits, const EmitChain* chains,
                               uint32_t nlist, uint32_t* ticket, uint8_t* out, ChainRes* res, const uint64_t* cands,
                               uint32_t ncand, uint32_t* ref, uint32_t* pend, SegPool pool, wv::PhArr* ph_all,
-                              uint32_t* stats) {
+                              uint32_t* stats, const uint64_t* info) {
     using namespace wv;
     __shared__ __attribute__((aligned(16))) Shared S;
     __shared__ Stage stg;
@@ -1288,6 +1288,10 @@ ndfl_inflate_emit_wave_kernel(const uint32_t* w, uint64_t nwords, uint64_t nbits
     gu8* gout = (gu8*)out;
     PhArr* S_ph = ph_all + blockIdx.x;
     const uint64_t t_begin = stats ? wall_clock64() : 0;
+    if (info) {                                 // device-side linking: the list length, and nothing
+        if (info[LI_FLAGS]) return;             // to emit when the host has to step in (uniform)
+        nlist = (uint32_t)info[LI_NCH];
+    }
     for (;;) {
     __syncthreads();
     if (lane == 0) s_ticket = atomicAdd(ticket, 1u);

@@ -264,7 +264,23 @@ def inflate_split(codec, dist, torch, stream, in_len, out, rank, world):
     return first, olen, dict_len, offs[rank]
 
 
-def gather_stream(codec, dist, torch, part, rank, world, root=0, out=None):
+class Pending:
+    """An asynchronous gather_stream: wait() completes the transfers (and, on the root, ORs the shared
+    first bytes in) and returns what gather_stream returns."""
+
+    def __init__(self, reqs, finish):
+        self._reqs, self._finish, self._done, self._value = reqs, finish, False, None
+
+    def wait(self):
+        if not self._done:
+            for r in self._reqs:
+                r.wait()
+            self._value = self._finish()
+            self._done = True
+        return self._value
+
+
+def gather_stream(codec, dist, torch, part, rank, world, root=0, out=None, async_op=False):
     """Reassemble the global stream on `root` (SURVEY §8e compress step 4): every rank sends its
     realigned part -- the first byte (shared with the previous shard when the global bit offset is
     not byte-aligned) and the body -- and the root receives each body straight into its byte offset
@@ -272,7 +288,9 @@ def gather_stream(codec, dist, torch, part, rank, world, root=0, out=None):
     first bytes in: BitOut's byte packing (D/DeflaterOutputStream.java:147-156) across GPUs, on
     device.  Returns the stream tensor (bytes ceil(total bits / 8)) on the root, None elsewhere.
     `out`: an optional preallocated root buffer of at least that many bytes (its old contents do not
-    matter: only the bytes every part's first byte is ORed into are cleared)."""
+    matter: only the bytes every part's first byte is ORed into are cleared).
+    async_op: return a Pending at once (RCCL moves the parts on its own stream while the caller goes
+    on, e.g. decoding its shard); host-staged (gloo) transfers complete before it returns."""
     offs = part.bit_offsets
     B = [o // 8 for o in offs[:-1]]
     nb = [(offs[r] % 8 + offs[r + 1] - offs[r] + 7) // 8 for r in range(world)]
@@ -304,13 +322,16 @@ def gather_stream(codec, dist, torch, part, rank, world, root=0, out=None):
                 if nb[r] > 1:
                     ops.append(dist.P2POp(dist.irecv, out[B[r] + 1:B[r] + nb[r]], r))
                 ops.append(dist.P2POp(dist.irecv, firsts[r:r + 1], r))
-        if ops:
-            for req in dist.batch_isend_irecv(ops):
-                req.wait()
-        for r in range(world):
-            if nb[r]:
-                out[B[r]:B[r] + 1].bitwise_or_(firsts[r:r + 1])
-        return out[:total]
+        reqs = dist.batch_isend_irecv(ops) if ops else []
+
+        def finish():
+            for r in range(world):
+                if nb[r]:
+                    out[B[r]:B[r] + 1].bitwise_or_(firsts[r:r + 1])
+            return out[:total]
+        pend = Pending(reqs, finish)
+        return pend if async_op else pend.wait()
+    reqs = []
     if nb[rank]:
         if staged:
             if nb[rank] > 1:
@@ -320,9 +341,9 @@ def gather_stream(codec, dist, torch, part, rank, world, root=0, out=None):
             ops = [dist.P2POp(dist.isend, part.buf[0:1].contiguous(), root)]
             if nb[rank] > 1:
                 ops.insert(0, dist.P2POp(dist.isend, part.buf[1:nb[rank]], root))
-            for req in dist.batch_isend_irecv(ops):
-                req.wait()
-    return None
+            reqs = dist.batch_isend_irecv(ops)
+    pend = Pending(reqs, lambda: None)
+    return pend if async_op else pend.wait()
 
 
 def assemble(parts):
