@@ -551,12 +551,15 @@ struct SRd {
 // through a per-lane 128-entry table of the code-length code (LDS, indexed by the next 7 bits
 // MSB first: canonical codes fill it in (length, symbol) order).  Accepted headers go to their
 // 64 KiB segment's list.
-extern "C" __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(NDFL_STRICT_WPE)))
-ndfl_inflate_strict_kernel(const uint32_t* w, uint64_t nwords, uint64_t nbits, const uint64_t* qlist,
-                           const uint32_t* qcount, uint32_t qcap, uint32_t* seg_cnt, uint64_t* seg_list,
-                           uint32_t* ticket, unsigned long long* sst, uint32_t* done, uint64_t part_base,
-                           uint64_t part_bits) {
+// PART: the partitioned finder's variant (done != nullptr: per-partition header counts and cost
+// classes); the dense scan's variant keeps no class state (its registers would spill).
+template <bool PART>
+__device__ __forceinline__ void strict_stage(const uint32_t* w, uint64_t nwords, uint64_t nbits, const uint64_t* qlist,
+                                             const uint32_t* qcount, uint32_t qcap, uint32_t* seg_cnt,
+                                             uint64_t* seg_list, uint32_t* ticket, unsigned long long* sst,
+                                             uint32_t* done, uint64_t part_base, uint64_t part_bits) {
     using namespace inf;
+    if (!PART) done = nullptr;
     __shared__ uint4 tabs[256 * 8];                          // 128 bytes per lane
     uint8_t* tab = (uint8_t*)&tabs[threadIdx.x * 8];
     const uint32_t n = min(*qcount, qcap);
@@ -686,7 +689,7 @@ ndfl_inflate_strict_kernel(const uint32_t* w, uint64_t nwords, uint64_t nbits, c
             const uint32_t v = (uint32_t)runVal;
             const uint32_t wt = v ? (32768u >> v) : 0u;
             litK += (min(en, numLit) - min(i, numLit)) * wt;
-            if (done) {
+            if (PART) {
                 // symbols [i, min(en, numLit)) of the literal/length code, all of length v
                 const uint32_t a = min(i, numLit), b = min(en, numLit);
                 const uint32_t nl = min(b, 256u) - min(a, 256u);
@@ -715,7 +718,7 @@ ndfl_inflate_strict_kernel(const uint32_t* w, uint64_t nwords, uint64_t nbits, c
                 if (ok) {
                     record(p);
                     // phase-locked literal codes, or more than 2 output bytes per stream bit
-                    if (done && (n8 >= 192u || e_bytes > 2u * e_bits))
+                    if (PART && (n8 >= 192u || e_bytes > 2u * e_bits))
                         atomicOr(&done[(p - part_base) / part_bits], PART_EXPENSIVE);
                 }
             }
@@ -727,6 +730,20 @@ ndfl_inflate_strict_kernel(const uint32_t* w, uint64_t nwords, uint64_t nbits, c
         atomicAdd(&sst[2], (unsigned long long)n_steps);
         atomicAdd(&sst[3], 1ull);
     }
+}
+extern "C" __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(NDFL_STRICT_WPE)))
+ndfl_inflate_strict_kernel(const uint32_t* w, uint64_t nwords, uint64_t nbits, const uint64_t* qlist,
+                           const uint32_t* qcount, uint32_t qcap, uint32_t* seg_cnt, uint64_t* seg_list,
+                           uint32_t* ticket, unsigned long long* sst) {
+    strict_stage<false>(w, nwords, nbits, qlist, qcount, qcap, seg_cnt, seg_list, ticket, sst, nullptr, 0, 1);
+}
+extern "C" __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(NDFL_STRICT_WPE)))
+ndfl_inflate_strict_part_kernel(const uint32_t* w, uint64_t nwords, uint64_t nbits, const uint64_t* qlist,
+                                const uint32_t* qcount, uint32_t qcap, uint32_t* seg_cnt, uint64_t* seg_list,
+                                uint32_t* ticket, unsigned long long* sst, uint32_t* done, uint64_t part_base,
+                                uint64_t part_bits) {
+    strict_stage<true>(w, nwords, nbits, qlist, qcount, qcap, seg_cnt, seg_list, ticket, sst, done, part_base,
+                       part_bits);
 }
 
 // Sort each segment's candidates (arrival order is arbitrary) and compact them into one sorted
@@ -1404,7 +1421,7 @@ static int inflate_run(InflateScratch& S, hipStream_t s, const uint8_t* in, uint
                                    nbits, d_qlist, d_qcount, qcap, w_lo, scan_end, (uint32_t)part_words, it,
                                    (const uint32_t*)S.d_done, d_last);
                 INF_CHK(hipGetLastError());
-                hipLaunchKernelGGL(ndfl_inflate_strict_kernel, dim3(strict_grid), dim3(256), 0, s, d_w, nwords, nbits,
+                hipLaunchKernelGGL(ndfl_inflate_strict_part_kernel, dim3(strict_grid), dim3(256), 0, s, d_w, nwords, nbits,
                                    (const uint64_t*)d_qlist, (const uint32_t*)d_qcount, qcap, d_cnt, d_list,
                                    (uint32_t*)S.d_stats + 10, sst, (uint32_t*)S.d_done, w_lo * 32, part_words * 32);
                 INF_CHK(hipGetLastError());
@@ -1417,19 +1434,17 @@ static int inflate_run(InflateScratch& S, hipStream_t s, const uint8_t* in, uint
             INF_CHK(hipGetLastError());
             hipLaunchKernelGGL(ndfl_inflate_strict_kernel, dim3(strict_grid), dim3(256), 0, s, d_w, nwords, nbits,
                                (const uint64_t*)d_qlist, (const uint32_t*)d_qcount, qcap, d_cnt, d_list,
-                               (uint32_t*)S.d_stats + 10, sst, (uint32_t*)nullptr, (uint64_t)0, (uint64_t)1);
+                               (uint32_t*)S.d_stats + 10, sst);
             INF_CHK(hipGetLastError());
             S.find_parts = nparts;
             S.find_part_bits = part_words * 32;
         } else if (nthr) {
-            const bool dense = nw32 <= (uint64_t)period;
             hipLaunchKernelGGL(ndfl_inflate_find_kernel, dim3((uint32_t)((nthr + 256 * FIND_WPT - 1) / (256 * FIND_WPT))), dim3(256), 0, s, d_w,
-                               nwords, nbits, d_qlist, d_qcount, qcap, dense ? 1u : win, dense ? 1u : period, w_lo,
-                               scan_end);
+                               nwords, nbits, d_qlist, d_qcount, qcap, win, period, w_lo, scan_end);
             INF_CHK(hipGetLastError());
             hipLaunchKernelGGL(ndfl_inflate_strict_kernel, dim3(strict_grid), dim3(256), 0, s, d_w, nwords, nbits,
                                (const uint64_t*)d_qlist, (const uint32_t*)d_qcount, qcap, d_cnt, d_list,
-                               (uint32_t*)S.d_stats + 10, sst, (uint32_t*)nullptr, (uint64_t)0, (uint64_t)1);
+                               (uint32_t*)S.d_stats + 10, sst);
             INF_CHK(hipGetLastError());
         }
     }
