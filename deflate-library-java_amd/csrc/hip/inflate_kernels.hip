@@ -986,6 +986,8 @@ struct InflateScratch {
     void* d_rl = nullptr; size_t d_rl_cap = 0;        // resolve: two group lists + round bits
     void* d_ticket = nullptr;
     void* d_ph = nullptr;                             // count pass: phase-fallback slot per wave
+    void* d_hrec = nullptr;                           // count pass: header records, one per candidate
+    size_t d_hrec_cap = 0;
     void* d_cticket = nullptr;                        // count pass: chain tickets (one per launch)
     void* d_out = nullptr; size_t d_out_cap = 0;
     void* d_done = nullptr; size_t d_done_cap = 0;    // partitioned finder: header found per partition
@@ -1004,7 +1006,7 @@ struct InflateScratch {
     uint64_t p_nbytes = 0;
     void release() {
         void** ps[] = {&d_in, &d_cand, &d_starts, &d_stops, &d_res, &d_cands, &d_stats, &d_q, &d_seg, &d_chains, &d_off,
-                       &d_ref, &d_pend, &d_rl, &d_ticket, &d_ph, &d_cticket, &d_out, &d_done};
+                       &d_ref, &d_pend, &d_rl, &d_ticket, &d_ph, &d_cticket, &d_out, &d_done, &d_hrec};
         for (void** p : ps) { if (*p) hipFree(*p); *p = nullptr; }
         for (auto& e : ev) { if (e) hipEventDestroy(e); e = nullptr; }
         if (h_cnt) hipHostFree(h_cnt);
@@ -1016,7 +1018,7 @@ struct InflateScratch {
         if (d_link) hipFree(d_link);
         d_link = nullptr; d_link_cap = 0;
         d_in_cap = d_cand_cap = d_starts_cap = d_stops_cap = d_res_cap = d_cands_cap = d_seg_cap = d_q_cap = d_chains_cap = 0;
-        d_off_cap = d_ref_cap = d_pend_cap = d_rl_cap = d_out_cap = d_done_cap = 0;
+        d_off_cap = d_ref_cap = d_pend_cap = d_rl_cap = d_out_cap = d_done_cap = d_hrec_cap = 0;
         pending = false;
     }
 };
@@ -1214,12 +1216,20 @@ static int inflate_devlink(InflateScratch& S, hipStream_t s, const uint32_t* d_w
     static const bool stats_on = getenv("NDFL_STATS") != nullptr;
     const uint64_t limit = std::min(end_bit, nbits);
     INF_CHK(hipEventRecord(S.ev[2], s));
+    static const bool hrec_on = !getenv("NDFL_NO_HDRREC");
+    if (hrec_on) {
+        INF_CHK(inf_ensure(&S.d_hrec, &S.d_hrec_cap, (size_t)ncand * sizeof(wv::HdrRec)));
+        hipLaunchKernelGGL(ndfl_inflate_hdr_kernel, dim3((ncand + 63) / 64), dim3(64), 0, s, d_w, nwords, nbits,
+                           (const uint64_t*)S.d_cands, ncand, (wv::HdrRec*)S.d_hrec);
+        INF_CHK(hipGetLastError());
+    }
     static const uint32_t count_grid = wave_grid(ndfl_inflate_count_wave_kernel, COUNT_WAVES, "NDFL_COUNT_WPC");
     hipLaunchKernelGGL(ndfl_inflate_count_wave_kernel, dim3(std::min<uint32_t>(ncand, count_grid)), dim3(64), 0, s,
                        d_w, nwords, nbits, (const uint64_t*)S.d_cands, (const uint64_t*)nullptr, ncand,
                        (const uint64_t*)S.d_cands, ncand, limit, (ChainRes*)S.d_res,
                        stats_on ? (uint32_t*)S.d_stats : nullptr, (uint64_t)0, S.pool, (uint32_t*)S.d_cticket,
-                       (wv::PhArr*)S.d_ph, (const uint32_t*)d_order, end_bit);
+                       (wv::PhArr*)S.d_ph, (const uint32_t*)d_order, end_bit,
+                       hrec_on ? (const wv::HdrRec*)S.d_hrec : nullptr);
     INF_CHK(hipGetLastError());
     INF_CHK(hipEventRecord(S.ev[3], s));
     // linking: J levels (u32), S and D double-buffered
@@ -1555,7 +1565,7 @@ static int inflate_run(InflateScratch& S, hipStream_t s, const uint8_t* in, uint
                            (const uint64_t*)S.d_starts, (const uint64_t*)S.d_stops, (uint32_t)n,
                            (const uint64_t*)S.d_cands, ncand, limit, (ChainRes*)S.d_res, stats_on ? (uint32_t*)S.d_stats : nullptr,
                            slot_base, pool, (uint32_t*)S.d_cticket, (wv::PhArr*)S.d_ph, (const uint32_t*)d_order,
-                           end_bit);
+                           end_bit, (const wv::HdrRec*)nullptr);
         INF_CHK(hipGetLastError());
         if (S.count_first) { INF_CHK(hipEventRecord(S.ev[3], s)); S.count_first = false; }
         r.resize(n);

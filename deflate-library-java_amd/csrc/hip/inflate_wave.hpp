@@ -280,15 +280,20 @@ __device__ __forceinline__ bool run_to(const Lv& v, uint32_t& pos, const Tabs& t
 }
 
 // ---- block header (lane 0) ----------------------------------------------------------------------
-// Parses the header at p into S.h_* and (dynamic) S.lens; validation in the reference's order up to
-// END_OF_BLOCK_CODE_ZERO_LENGTH; the tree checks of the two codes follow in build_code.
-__device__ void parse_hdr(const In& in, uint64_t p, Shared& S) {
+// Parses the header at p into h and (dynamic) lens[0, numLit) and lens[288, 288 + numDist) (the
+// caller zeroes lens); validation in the reference's order up to END_OF_BLOCK_CODE_ZERO_LENGTH; the
+// tree checks of the two codes follow in build_code.  cl_tab: 128 u16 of scratch (LDS).
+struct Hdr {
+    uint64_t pos, d0;
+    uint32_t err, bfinal, btype, len, numlit, numdist;
+};
+__device__ __forceinline__ void parse_hdr_core(const In& in, uint64_t p, uint8_t* lens, uint16_t* cl_tab, Hdr& h) {
     Rd rd;
     rd.init(in, p);
-    S.h_err = 0; S.h_len = 0; S.h_numlit = 0; S.h_numdist = 0;
+    h.err = 0; h.len = 0; h.numlit = 0; h.numdist = 0; h.pos = 0; h.d0 = 0;
     const uint32_t bf = rd.get(in, 1), bt = rd.get(in, 2);
-    S.h_bfinal = bf; S.h_btype = bt;
-#define HFAIL(r) do { S.h_err = (r); S.h_pos = rd.pos; return; } while (0)
+    h.bfinal = bf; h.btype = bt;
+#define HFAIL(r) do { h.err = (r); h.pos = rd.pos; return; } while (0)
     if (rd.pos > in.nbits) HFAIL(R_UEOS);
     if (bt == 3) HFAIL(R_RESERVED_BLOCK_TYPE);
     if (bt == 0) {
@@ -296,10 +301,10 @@ __device__ void parse_hdr(const In& in, uint64_t p, Shared& S) {
         const uint32_t ln = rd.get(in, 16), nln = rd.get(in, 16);
         if (rd.pos > in.nbits) HFAIL(R_UEOS);
         if (ln != (nln ^ 0xFFFFu)) HFAIL(R_LEN_MISMATCH);
-        S.h_len = ln; S.h_d0 = rd.pos; S.h_pos = rd.pos;
+        h.len = ln; h.d0 = rd.pos; h.pos = rd.pos;
         return;
     }
-    if (bt == 1) { S.h_d0 = rd.pos; S.h_pos = rd.pos; return; }
+    if (bt == 1) { h.d0 = rd.pos; h.pos = rd.pos; return; }
     const uint32_t hlit = rd.get(in, 5), hdist = rd.get(in, 5), hclen = rd.get(in, 4);
     if (rd.pos > in.nbits) HFAIL(R_UEOS);
     const uint32_t numLit = hlit + 257, numDist = hdist + 1, numCl = hclen + 4;
@@ -327,7 +332,7 @@ __device__ void parse_hdr(const In& in, uint64_t p, Shared& S) {
             const uint32_t l = cl[s];
             if (!l) continue;
             const uint32_t r = rev_bits(first[l] + nx[l]++, l);
-            for (uint32_t k = r; k < 128; k += (1u << l)) S.cl_tab[k] = (uint16_t)(s | (l << 9));
+            for (uint32_t k = r; k < 128; k += (1u << l)) cl_tab[k] = (uint16_t)(s | (l << 9));
         }
     }
     const uint32_t total = numLit + numDist;
@@ -335,7 +340,7 @@ __device__ void parse_hdr(const In& in, uint64_t p, Shared& S) {
     int runVal = -1;
     while (i < total) {
         rd.fill(in);
-        const uint32_t ent = S.cl_tab[rd.peek(7)];
+        const uint32_t ent = cl_tab[rd.peek(7)];
         rd.skip(ent >> 9);
         const uint32_t sym = ent & 0x1FF;
         if (rd.pos > in.nbits) HFAIL(R_UEOS);
@@ -348,13 +353,31 @@ __device__ void parse_hdr(const In& in, uint64_t p, Shared& S) {
         else { runVal = 0; run = rd.get(in, 7) + 11; v = 0; }
         if (rd.pos > in.nbits) HFAIL(R_UEOS);
         if (i + run > total) HFAIL(R_CL_OVER_FULL);
-        for (uint32_t k = 0; k < run; k++, i++) S.lens[i < numLit ? i : 288 + (i - numLit)] = (uint8_t)v;
+        if (v) for (uint32_t k = 0; k < run; k++, i++) lens[i < numLit ? i : 288 + (i - numLit)] = (uint8_t)v;
+        else i += run;                          // (lens are zeroed by the caller)
     }
-    if (S.lens[256] == 0) HFAIL(R_EOB_ZERO);
-    S.h_numlit = numLit; S.h_numdist = numDist;
-    S.h_d0 = rd.pos; S.h_pos = rd.pos;
+    if (lens[256] == 0) HFAIL(R_EOB_ZERO);
+    h.numlit = numLit; h.numdist = numDist;
+    h.d0 = rd.pos; h.pos = rd.pos;
 #undef HFAIL
 }
+__device__ __forceinline__ void hdr_to_shared(const Hdr& h, Shared& S) {
+    S.h_pos = h.pos; S.h_d0 = h.d0; S.h_err = h.err; S.h_bfinal = h.bfinal; S.h_btype = h.btype;
+    S.h_len = h.len; S.h_numlit = h.numlit; S.h_numdist = h.numdist;
+}
+__device__ void parse_hdr(const In& in, uint64_t p, Shared& S) {
+    Hdr h;
+    parse_hdr_core(in, p, S.lens, S.cl_tab, h);
+    hdr_to_shared(h, S);
+}
+
+// Header records (ndfl_inflate_hdr_kernel): every header candidate's parse, one lane each, so the
+// count pass's first block of a chain loads it instead of parsing on one lane of its wave.
+struct HdrRec {
+    uint32_t lens[80];                       // S.lens as words
+    Hdr h;
+    uint64_t at;                             // the candidate's bit position
+};
 
 // Canonical code from S.lens[base .. base+n) into the primary table `prim` (pbits) and the
 // extension area `x` (cap words): second-level tables for the codes longer than the primary when
@@ -726,12 +749,6 @@ __device__ void round_decode(const In& in, const Tabs& t, bool ed, uint64_t rs, 
 #ifndef NDFL_PHASE_GROUP
 #define NDFL_PHASE_GROUP 8     // phase runs decoded together (1, 2, 4 or 8; measured 1: 14.6, 2: 13.9,
 #endif                         // 4: 12.9, 8: 12.8 ms count pass)
-struct PhMap {
-    uint32_t cnt[8][64];                     // bytes of the phase run
-    uint32_t fbc[8][64];                     // bytes of its first token
-    uint8_t kr[8][64];                       // kind << 5 | reason
-};
-static_assert(sizeof(PhMap) <= sizeof(PhArr), "phase map shares the fallback slot");
 
 // count run from st to the first token boundary at or past e (or the block end); the first step is
 // a single token whose end and bytes are returned in fb / fbc (fb = NOCP: none)
@@ -838,15 +855,15 @@ __device__ __forceinline__ uint32_t map_compose(uint32_t A, uint32_t B) {
 
 __device__ __noinline__ void round_decode_phased(const In& in, const Tabs& t, bool ed, uint64_t rs, uint64_t E,
                                                  Shared& S, Stage& stg, int lane, Seg& out, uint32_t& first_term,
-                                                 uint32_t& nfix, PhArr* ph, Geo& g) {
+                                                 uint32_t& nfix, Geo& g) {
     g = make_geo(in, rs, E);
     stage_round(in, g, stg, lane);
     const Lv v = make_lv(stg, g, lane);
     const uint32_t nb = g.nb;
     uint32_t s, e;
     lane_seg(g, lane, s, e);
-    PhMap* pm = (PhMap*)ph;
-    uint32_t endv[8];
+    // the 8 runs' results stay in registers (a lane reads back only its own, through sel8)
+    uint32_t endv[8], cntv[8], fbcv[8], krv[8];
     uint32_t fbl = 0, fbh = 0;
 #if NDFL_PHASE_GROUP > 1
     constexpr uint32_t G = NDFL_PHASE_GROUP >= 8 ? 8 : NDFL_PHASE_GROUP >= 4 ? 4 : 2;
@@ -858,9 +875,9 @@ __device__ __noinline__ void round_decode_phased(const In& in, const Tabs& t, bo
         for (uint32_t h = 0; h < G; h++) {
             const uint32_t g = f + h;
             endv[g] = P[h].end;
-            pm->cnt[g][lane] = P[h].cnt;
-            pm->fbc[g][lane] = P[h].fbc;
-            pm->kr[g][lane] = (uint8_t)P[h].kr;
+            cntv[g] = P[h].cnt;
+            fbcv[g] = P[h].fbc;
+            krv[g] = P[h].kr;
             const uint32_t fo = (P[h].fb != NOCP && P[h].fb - s < 255u) ? P[h].fb - s : 255u;
             if (g < 4) fbl |= fo << (8 * g); else fbh |= fo << (8 * (g - 4));
         }
@@ -870,10 +887,12 @@ __device__ __noinline__ void round_decode_phased(const In& in, const Tabs& t, bo
         uint32_t en, cn, kr, fb, fbc;
         phase_run(v, t, ed, nb, s + f, e, en, cn, kr, fb, fbc);      // (past e: empty, ends at s + f)
 #pragma unroll
-        for (uint32_t k = 0; k < 8; k++) endv[k] = k == f ? en : endv[k];
-        pm->cnt[f][lane] = cn;
-        pm->fbc[f][lane] = fbc;
-        pm->kr[f][lane] = (uint8_t)kr;
+        for (uint32_t k = 0; k < 8; k++) {
+            endv[k] = k == f ? en : endv[k];
+            cntv[k] = k == f ? cn : cntv[k];
+            fbcv[k] = k == f ? fbc : fbcv[k];
+            krv[k] = k == f ? kr : krv[k];
+        }
         const uint32_t fo = (fb != NOCP && fb - s < 255u) ? fb - s : 255u;
         if (f < 4) fbl |= fo << (8 * f); else fbh |= fo << (8 * (f - 4));
     }
@@ -903,9 +922,9 @@ __device__ __noinline__ void round_decode_phased(const In& in, const Tabs& t, bo
         const uint32_t f = pc & 15u;
         if (f == myph) {
             known = true;
-            const uint32_t kr = pm->kr[f][lane];
+            const uint32_t kr = sel8(krv, f);
             r.end = sel8(endv, f);
-            r.cnt = pm->cnt[f][lane] - ((pc & 16u) ? pm->fbc[f][lane] : 0u);
+            r.cnt = sel8(cntv, f) - ((pc & 16u) ? sel8(fbcv, f) : 0u);
             r.kind = kr >> 5; r.reason = kr & 31u;
         }
     }
@@ -1010,16 +1029,59 @@ typedef __attribute__((address_space(1))) uint64_t gu64;
 #else
 #define NDFL_OA(x) (x)
 #endif
+// NDFL_EMIT_W16: completed literal words are held (up to 3) and leave as one 16-byte store, so a lane
+// issues a quarter of the scattered stores (each store instruction of a wave touches 64 lines)
+#ifndef NDFL_EMIT_W16
+#define NDFL_EMIT_W16 1
+#endif
+typedef uint32_t u32x4v __attribute__((ext_vector_type(4)));
+typedef __attribute__((address_space(1))) u32x4v gu128;
 struct Wr {
     uint64_t acc;               // pending literal bytes (low byte first)
     uint32_t an;                // pending byte count (0..3 between tokens)
     uint64_t dst;               // output address of acc's first byte
+#if NDFL_EMIT_W16
+    uint32_t q0, q1, q2, hn;    // completed words held back (hn of them), at dst - 4 hn
+#endif
 };
+__device__ __forceinline__ void wr_init(Wr& w, uint64_t dst) {
+    w.acc = 0; w.an = 0; w.dst = dst;
+#if NDFL_EMIT_W16
+    w.q0 = 0; w.q1 = 0; w.q2 = 0; w.hn = 0;
+#endif
+}
+// held words out (before a copy or at the end)
+__device__ __forceinline__ void wr_drain(Wr& w, gu8* out) {
+#if NDFL_EMIT_W16
+    if (w.hn) {
+        gu8* d = out + NDFL_OA(w.dst - 4 * w.hn);
+        if (w.hn >= 2) *(gu64*)d = (uint64_t)w.q0 | ((uint64_t)w.q1 << 32);
+        if (w.hn == 1) *(gu32*)d = w.q0;
+        if (w.hn == 3) *(gu32*)(d + 8) = w.q2;
+        w.hn = 0;
+    }
+#else
+    (void)w; (void)out;
+#endif
+}
 __device__ __forceinline__ void wr_lit(Wr& w, gu8* out, uint32_t val, uint32_t n) {
     w.acc |= (uint64_t)val << (8 * w.an);
     w.an += n;
     if (w.an >= 4) {
-        *(gu32*)(out + NDFL_OA(w.dst)) = (uint32_t)w.acc;
+        const uint32_t word = (uint32_t)w.acc;
+#if NDFL_EMIT_W16
+        if (w.hn == 3) {
+            *(gu128*)(out + NDFL_OA(w.dst - 12)) = u32x4v{w.q0, w.q1, w.q2, word};
+            w.hn = 0;
+        } else {
+            w.q0 = w.hn == 0 ? word : w.q0;
+            w.q1 = w.hn == 1 ? word : w.q1;
+            w.q2 = w.hn == 2 ? word : w.q2;
+            w.hn++;
+        }
+#else
+        *(gu32*)(out + NDFL_OA(w.dst)) = word;
+#endif
         w.acc >>= 32;
         w.an -= 4;
         w.dst += 4;
@@ -1027,6 +1089,7 @@ __device__ __forceinline__ void wr_lit(Wr& w, gu8* out, uint32_t val, uint32_t n
 }
 // pending bytes out before a copy at w.dst + w.an (which covers the store's spare bytes)
 __device__ __forceinline__ void wr_flush_word(Wr& w, gu8* out) {
+    wr_drain(w, out);
     if (w.an) {
         *(gu32*)(out + NDFL_OA(w.dst)) = (uint32_t)w.acc;
         w.dst += w.an;
@@ -1036,6 +1099,7 @@ __device__ __forceinline__ void wr_flush_word(Wr& w, gu8* out) {
 }
 // pending bytes out exactly (end of the lane's output)
 __device__ __forceinline__ void wr_flush_exact(Wr& w, gu8* out) {
+    wr_drain(w, out);
     for (uint32_t k = 0; k < w.an; k++) out[NDFL_OA(w.dst + k)] = (uint8_t)(w.acc >> (8 * k));
     w.dst += w.an;
     w.acc = 0;
@@ -1060,6 +1124,16 @@ __device__ __forceinline__ void wr_copy(gu8* out, uint64_t dst, uint32_t len, ui
         }
         return;
     }
+#if NDFL_EMIT_W16
+    if (dist >= 16 && len >= 16) {
+        uint32_t k = 0;
+        u32x4v x = {0, 0, 0, 0};
+        for (; k + 16 <= len; k += 16) { x = *(const gu128*)(sp + k); *(gu128*)(d + k) = x; }
+        if (k < len) { x = *(const gu128*)(sp + len - 16); *(gu128*)(d + len - 16) = x; }
+        lastb = x.w >> 24;
+        return;
+    }
+#endif
     if (dist >= 8 && len >= 8) {
         uint32_t k = 0;
         uint64_t x = 0;
@@ -1082,6 +1156,29 @@ __device__ __forceinline__ void wr_copy(gu8* out, uint64_t dst, uint32_t len, ui
 
 }  // namespace wv
 
+// Header records: one lane per header candidate parses it (the count pass's lane-0 parse, which
+// leaves 63 lanes idle through a chain of dependent loads, becomes a load of 336 bytes).
+extern "C" __global__ void __launch_bounds__(64)
+ndfl_inflate_hdr_kernel(const uint32_t* w, uint64_t nwords, uint64_t nbits, const uint64_t* cands, uint32_t ncand,
+                        wv::HdrRec* rec) {
+    using namespace wv;
+    __shared__ __attribute__((aligned(16))) uint32_t lens[64][80];
+    __shared__ uint16_t clt[64][128];
+    const uint32_t lane = threadIdx.x;
+    const uint32_t k = blockIdx.x * 64 + lane;
+    if (k >= ncand) return;                     // (no barrier below)
+    const In in{w, nwords, nbits};
+    for (uint32_t q = 0; q < 80; q++) lens[lane][q] = 0;
+    const uint64_t p = cands[k];
+    Hdr h;
+    parse_hdr_core(in, p, (uint8_t*)lens[lane], clt[lane], h);
+    HdrRec* r = rec + k;
+    for (uint32_t q = 0; q < 80; q += 4)
+        *(uint4*)&r->lens[q] = make_uint4(lens[lane][q], lens[lane][q + 1], lens[lane][q + 2], lens[lane][q + 3]);
+    r->h = h;
+    r->at = p;
+}
+
 // Count pass: persistent waves, each claiming candidate chains through `ticket`; the phase-fallback
 // arrays live in the wave's own global slot (ph_all[blockIdx.x]); LDS holds the tables and the
 // round's staged input.
@@ -1092,7 +1189,8 @@ extern "C" __global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per
 ndfl_inflate_count_wave_kernel(const uint32_t* w, uint64_t nwords, uint64_t nbits, const uint64_t* starts,
                                const uint64_t* stops, uint32_t nchains, const uint64_t* cands, uint32_t ncand,
                                uint64_t limit, ChainRes* res, uint32_t* stats, uint64_t slot_base, SegPool pool,
-                               uint32_t* ticket, wv::PhArr* ph_all, const uint32_t* order, uint64_t stop_all) {
+                               uint32_t* ticket, wv::PhArr* ph_all, const uint32_t* order, uint64_t stop_all,
+                               const wv::HdrRec* hrec) {
     using namespace wv;
     __shared__ __attribute__((aligned(16))) Shared S;
     __shared__ Stage stg;
@@ -1132,10 +1230,20 @@ ndfl_inflate_count_wave_kernel(const uint32_t* w, uint64_t nwords, uint64_t nbit
         // a chain ends at the first later block boundary that is itself a header candidate (its own
         // chain links on from there) or at the range end; false candidates are passed over
         if (blk > 0 && (cur >= stop || cc.at(cur, &next_idx))) { status = ST_BOUNDARY; endpos = cur; break; }
-        for (uint32_t s = (uint32_t)lane; s < 320; s += 64) S.lens[s] = 0;
-        __syncthreads();
-        if (lane == 0) parse_hdr(in, cur, S);
-        __syncthreads();
+        if (hrec && blk == 0 && cc.i < cc.n && cc.v == cur) {
+            // the chain starts at a header candidate: its parse is in the header records
+            const HdrRec* hr = hrec + cc.i;
+            uint32_t* lw = (uint32_t*)S.lens;
+            lw[lane] = hr->lens[lane];
+            if (lane < 16) lw[64 + lane] = hr->lens[64 + lane];
+            if (lane == 0) hdr_to_shared(hr->h, S);
+            __syncthreads();
+        } else {
+            for (uint32_t s = (uint32_t)lane; s < 320; s += 64) S.lens[s] = 0;
+            __syncthreads();
+            if (lane == 0) parse_hdr(in, cur, S);
+            __syncthreads();
+        }
         if (S.h_err) { status = ST_ERROR; reason = S.h_err; endpos = S.h_pos; break; }
         const uint64_t d0 = S.h_d0;
         const bool bfinal = S.h_bfinal != 0;
@@ -1191,7 +1299,7 @@ ndfl_inflate_count_wave_kernel(const uint32_t* w, uint64_t nwords, uint64_t nbit
             Geo g;
             if (phased) {
                 const uint64_t t0p = pc ? wall_clock64() : 0;
-                round_decode_phased(in, S.t, ed, rs, E, S, stg, lane, r, ft, nfix, ph, g);
+                round_decode_phased(in, S.t, ed, rs, E, S, stg, lane, r, ft, nfix, g);
                 if (pc) pc->phmap += wall_clock64() - t0p;
             } else {
                 const uint32_t ns0 = nslow;
@@ -1404,7 +1512,7 @@ ndfl_inflate_emit_wave_kernel(const uint32_t* w, uint64_t nwords, uint64_t nbits
             const uint64_t dst0 = base + pre;
             uint64_t n = 0;                 // bytes produced
             Wr wr;
-            wr.acc = 0; wr.an = 0; wr.dst = dst0;
+            wr_init(wr, dst0);
             uint64_t dfr = ~0ull;           // first deferred byte of this lane (absolute)
             uint64_t lastsrc = 0;           // a byte holding the value of the last output byte
             uint32_t lastb = 0;             // the last output byte, when it is final (lastok)
