@@ -668,7 +668,11 @@ __device__ __forceinline__ void strict_stage(const uint32_t* w, uint64_t nwords,
             if (next >= end && drained) break;
             continue;
         }
-        n_steps += 64 - nidle;
+        // steps until enough lanes are idle for a refill (or none is active): a loop of its own, so
+        // the step's state stays in place across iterations (the refill above is cold code)
+        const bool more = next < end || !drained;
+        for (uint32_t ni = nidle;;) {
+        n_steps += 64 - ni;
         if (active) {
             // one code-length symbol (D/decomp/Open.java's dynamic header loop, same checks)
             // one refill covers the code (<= 7 bits) and its extra bits (<= 7): no branch per symbol kind
@@ -722,6 +726,11 @@ __device__ __forceinline__ void strict_stage(const uint32_t* w, uint64_t nwords,
                         atomicOr(&done[(p - part_base) / part_bits], PART_EXPENSIVE);
                 }
             }
+        }
+        const uint64_t am = __ballot(active);
+        ni = 64u - (uint32_t)__popcll(am);
+        if (!am || (more && ni >= NDFL_STRICT_REFILL)) break;
+        n_iter++;
         }
     }
     if (sst && lane == 0) {

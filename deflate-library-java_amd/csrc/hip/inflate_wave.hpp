@@ -1034,6 +1034,9 @@ typedef __attribute__((address_space(1))) uint64_t gu64;
 #ifndef NDFL_EMIT_W16
 #define NDFL_EMIT_W16 1
 #endif
+#ifndef NDFL_EMIT_NT
+#define NDFL_EMIT_NT 0          // (A/B: non-temporal 16-byte literal stores)
+#endif
 typedef uint32_t u32x4v __attribute__((ext_vector_type(4)));
 typedef __attribute__((address_space(1))) u32x4v gu128;
 struct Wr {
@@ -1071,7 +1074,11 @@ __device__ __forceinline__ void wr_lit(Wr& w, gu8* out, uint32_t val, uint32_t n
         const uint32_t word = (uint32_t)w.acc;
 #if NDFL_EMIT_W16
         if (w.hn == 3) {
+#if NDFL_EMIT_NT
+            __builtin_nontemporal_store(u32x4v{w.q0, w.q1, w.q2, word}, (gu128*)(out + NDFL_OA(w.dst - 12)));
+#else
             *(gu128*)(out + NDFL_OA(w.dst - 12)) = u32x4v{w.q0, w.q1, w.q2, word};
+#endif
             w.hn = 0;
         } else {
             w.q0 = w.hn == 0 ? word : w.q0;
