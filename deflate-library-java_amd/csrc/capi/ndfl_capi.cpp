@@ -979,6 +979,13 @@ int ndfl_inflate_resolve(ndfl_ctx* c, uint64_t* n_reemitted) {
     return inflate_resolve(c->inf, ordered_stream(c), n_reemitted);
 }
 
+int ndfl_inflate_tail(ndfl_ctx* c, uint64_t tail_len, uint8_t* dst) {
+    if (!c || (!dst && tail_len)) return NDFL_E_ARG;
+    HIPCHK(hipSetDevice(c->device));
+    const int r = inflate_tail(c->inf, ordered_stream(c), tail_len, dst);
+    return r == -5 ? NDFL_E_STATE : r == -6 ? NDFL_E_UNSUPPORTED : r == -1 ? NDFL_E_ARG : r;
+}
+
 int ndfl_bits_shift(ndfl_ctx* c, const uint8_t* in, uint64_t nbits, uint32_t shift, uint8_t* out, uint64_t out_cap,
                     uint32_t flags) {
     if (!c || (!in && nbits) || !out || shift > 7) return NDFL_E_ARG;

@@ -1830,6 +1830,41 @@ static int inflate_sync(InflateScratch& S, hipStream_t s, const uint8_t* in, uin
                        sync_bit);
 }
 
+// The last n bytes of a deferred-window range decode's output once the caller has written the
+// window, without resolving the rest: each byte follows its back-references (pending bytes only;
+// window bytes are never pending) to a final byte.  A chain longer than TAIL_STEPS sets *fail.
+constexpr uint32_t TAIL_STEPS = 4096;
+extern "C" __global__ void __launch_bounds__(256)
+ndfl_inflate_tail_kernel(const uint32_t* pend, const uint32_t* ref, const uint8_t* out, uint64_t t0, uint64_t n,
+                         uint8_t* dst, uint32_t* fail) {
+    const uint64_t k = (uint64_t)blockIdx.x * 256 + threadIdx.x;
+    if (k >= n) return;
+    uint64_t p = t0 + k;
+    uint32_t steps = 0;
+    while ((pend[p >> 5] >> (p & 31)) & 1) {
+        p -= ref[p];
+        if (++steps > TAIL_STEPS) { atomicOr(fail, 1u); return; }
+    }
+    dst[k] = out[p];
+}
+
+static int inflate_tail(InflateScratch& S, hipStream_t s, uint64_t n, uint8_t* dst) {
+    if (!S.pending) return -5;
+    if (n > S.p_nbytes) return -1;
+    if (n == 0) return 0;
+    if (!S.h_cnt) INF_CHK(hipHostMalloc(&S.h_cnt, 64, 0));
+    uint32_t* d_fail = (uint32_t*)S.d_stats + 14;
+    INF_CHK(hipMemsetAsync(d_fail, 0, 4, s));
+    hipLaunchKernelGGL(ndfl_inflate_tail_kernel, dim3((uint32_t)((n + 255) / 256)), dim3(256), 0, s,
+                       (const uint32_t*)S.d_pend, (const uint32_t*)S.d_ref, (const uint8_t*)S.p_out, S.p_nbytes - n, n,
+                       dst, d_fail);
+    INF_CHK(hipGetLastError());
+    uint32_t* h = (uint32_t*)S.h_cnt;
+    INF_CHK(hipMemcpyAsync(h + 8, d_fail, 4, hipMemcpyDeviceToHost, s));
+    INF_CHK(hipStreamSynchronize(s));
+    return h[8] ? -6 : 0;
+}
+
 // Second half of a deferred-window range decode: the caller has written the window
 // (out[0, dict_len)); resolve every deferred copy (those that read the window directly or through
 // other copies included).  *n_resolved = pending 32-byte groups at the start.

@@ -355,6 +355,17 @@ class Context:
         check(load().ndfl_inflate_resolve(self._h, ctypes.byref(n)), "ndfl_inflate_resolve")
         return n.value
 
+    def inflate_tail_raw(self, tail_len, dst_addr):
+        """ndfl_inflate_tail: the last tail_len output bytes of the pending DICT_DEFERRED decode (its
+        window written) into device memory at dst_addr; False if a reference chain is too long
+        (NDFL_E_UNSUPPORTED: resolve first)."""
+        self._order()
+        r = load().ndfl_inflate_tail(self._h, tail_len, ctypes.c_void_p(dst_addr))
+        if r == _lib.E_UNSUPPORTED:
+            return False
+        check(r, "ndfl_inflate_tail")
+        return True
+
     def bits_shift_raw(self, in_addr, nbits, shift, out_addr, out_cap):
         """ndfl_bits_shift on device buffers: in's first nbits bits placed at bit `shift` of out."""
         self._order()

@@ -37,7 +37,8 @@ EXPORTS = ["ndfl_abi_version", "ndfl_error_string", "ndfl_ctx_create", "ndfl_ctx
            "ndfl_deflate_chunks_lz77", "ndfl_deflate_chunks_multi", "ndfl_deflate_chunks_binsplit",
            "ndfl_deflate_bound",
            "ndfl_inflate", "ndfl_inflate_range", "ndfl_inflate_resolve", "ndfl_bits_shift", "ndfl_crc32", "ndfl_adler32",
-           "ndfl_crc32_combine", "ndfl_decide", "ndfl_compress_to", "ndfl_decision_free", "ndfl_inflate_sync"]
+           "ndfl_crc32_combine", "ndfl_decide", "ndfl_compress_to", "ndfl_decision_free", "ndfl_inflate_sync",
+           "ndfl_inflate_tail"]
 
 KIND_LZ77, KIND_UNCOMPRESSED = 0, 1
 
@@ -92,6 +93,7 @@ def load():
     L.ndfl_inflate_range.argtypes = [vp, vp, u64, u64, u64, vp, u64, u64, ctypes.POINTER(u64), ctypes.POINTER(u64),
                                      u32]
     L.ndfl_inflate_resolve.argtypes = [vp, ctypes.POINTER(u64)]
+    L.ndfl_inflate_tail.argtypes = [vp, u64, vp]
     L.ndfl_inflate_sync.argtypes = [vp, vp, u64, u64, u64, ctypes.POINTER(u64), u32]
     L.ndfl_bits_shift.argtypes = [vp, vp, u64, u32, vp, u64, u32]
     L.ndfl_crc32.argtypes = [vp, ctypes.POINTER(u32), vp, u64, u32]

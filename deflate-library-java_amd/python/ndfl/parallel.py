@@ -80,6 +80,12 @@ class DeviceCodec:
     def resolve(self):
         return self.ctx.inflate_resolve()
 
+    def tail(self, n):
+        """The last n output bytes of the pending deferred decode (its window written), before the
+        resolve; None if a reference chain is too long to follow (resolve first)."""
+        t = self.empty(n)
+        return t[:n] if self.ctx.inflate_tail_raw(n, t.data_ptr()) else None
+
     def sync(self, src, in_len, from_bit, window_bits):
         from . import IN_DEVICE
         return self.ctx.inflate_sync_raw(src.data_ptr(), in_len, from_bit, window_bits, IN_DEVICE)
@@ -179,14 +185,23 @@ def inflate_shard(codec, dist, torch, part, out, rank, world):
                                         deferred)
     if code < 0:
         raise RuntimeError(f"inflate_range failed: {code}")
-    # window chain: rank r-1's last 32 KiB of output -> rank r
+    # window chain: rank r-1's last 32 KiB of output -> rank r.  Rank r passes its own last 32 KiB
+    # on as soon as its window is in (ndfl_inflate_tail follows those bytes' references), and
+    # resolves the rest of its range after that, so the chain's step per rank is one small kernel
+    # and one message, not a whole resolve.
+    nxt = min(WINDOW, part.byte_offsets[rank + 1]) if rank + 1 < world else 0
+    end = dict_len + olen
+    sent = False
     if rank > 0 and dict_len:
         _recv(dist, out[:dict_len], rank - 1)
+        if code == 0 and nxt and end >= nxt:
+            tail = codec.tail(nxt)
+            if tail is not None:
+                _send(dist, tail, rank + 1)
+                sent = True
         if code == 0:
             codec.resolve()
-    if rank + 1 < world:
-        nxt = min(WINDOW, part.byte_offsets[rank + 1])
-        end = dict_len + olen
+    if rank + 1 < world and not sent:
         if code == 0 and end >= nxt:
             _send(dist, out[end - nxt:end].contiguous(), rank + 1)
         else:                                    # an error ends the stream here: keep the chain moving

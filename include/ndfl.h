@@ -247,6 +247,16 @@ int ndfl_inflate_sync(ndfl_ctx* ctx, const uint8_t* in, uint64_t in_len, uint64_
                       uint64_t* sync_bit, uint32_t flags);
 /* Finish the last NDFL_DICT_DEFERRED range decode on this context (NDFL_E_STATE if none). */
 int ndfl_inflate_resolve(ndfl_ctx* ctx, uint64_t* n_reemitted);
+/*
+ * Multi-GPU window chain: once the caller has written the window of the last
+ * NDFL_DICT_DEFERRED range decode, dst[0, tail_len) (device memory) = the final values of the last
+ * tail_len bytes of out[0, dict_len + out_len), without resolving the rest -- the next GPU's window,
+ * passed on before this GPU's own resolve (ndfl_inflate_resolve still finishes the decode).  In the
+ * reference this is the 32 KiB dictionary that Open carries from one block to the next
+ * (D/decomp/Open.java:592-603).  NDFL_E_STATE if no deferred decode is pending, NDFL_E_UNSUPPORTED if
+ * a byte's back-reference chain is too long to follow (resolve first, then take the bytes from out).
+ */
+int ndfl_inflate_tail(ndfl_ctx* ctx, uint64_t tail_len, uint8_t* dst);
 
 /*
  * Multi-GPU seam step for compression: place the first `nbits` bits of `in` at bit

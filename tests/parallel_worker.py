@@ -60,6 +60,17 @@ class OracleCodec:
         self.pending = (data, start, end, out, dict_len) if deferred else None
         return self._decode(data, start, end, out, dict_len, window)
 
+    tails = 0
+
+    def tail(self, n):
+        """As ndfl_inflate_tail: the last n bytes of the pending decode, the window written, without
+        finishing it (the checker decodes the range with the window and keeps the decode pending)."""
+        data, start, end, out, dict_len = self.pending
+        tmp = out.clone()
+        code, olen, _ = self._decode(data, start, end, tmp, dict_len, bytes(out[:dict_len].numpy()))
+        self.tails += 1
+        return tmp[dict_len + olen - n:dict_len + olen].clone()
+
     def resolve(self):
         data, start, end, out, dict_len = self.pending
         self.pending = None
@@ -171,6 +182,7 @@ def main():
     ok["decoded_equal"] = olen == sizes[rank] and \
         bytes(out[dict_len:dict_len + olen].cpu().numpy()) == bytes(shard.cpu().numpy())
     ok["resolved"] = getattr(codec, "resolved", None)
+    ok["tails"] = getattr(codec, "tails", None)
     res = [None] * world
     dist.all_gather_object(res, ok)
     if rank == 0:

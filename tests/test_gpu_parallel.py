@@ -136,6 +136,11 @@ def test_deferred_window_then_resolve(env, seed):
                                               len(ref) + 64, ndfl.IN_DEVICE | ndfl.OUT_DEVICE | ndfl.DICT_DEFERRED)
         assert (r, olen) == (0, len(ref))
         out[:32768] = torch.frombuffer(bytearray(window), dtype=torch.uint8).cuda()
+        # the next rank's window first (ndfl_inflate_tail), then the resolve
+        for n in (32768, 40000, 5):
+            tail = torch.zeros(n, dtype=torch.uint8, device="cuda")
+            assert ctx.inflate_tail_raw(n, tail.data_ptr())
+            assert bytes(tail.cpu().numpy()) == (window + ref)[-n:]
         n_re = ctx.inflate_resolve()
         assert n_re >= 1
         assert bytes(out[32768:32768 + olen].cpu().numpy()) == ref
@@ -143,10 +148,13 @@ def test_deferred_window_then_resolve(env, seed):
             ctx.inflate_resolve()                       # nothing pending any more
 
 
-def test_sharded_protocol_two_ranks_one_gpu():
+@pytest.mark.parametrize("world", [2, 3])
+def test_sharded_protocol_ranks_one_gpu(world):
+    """The whole sharded protocol with 2 and 3 ranks sharing cuda:0 over gloo; with 3, the middle
+    rank passes its window on through ndfl_inflate_tail before its own resolve."""
     from test_parallel_cpu import run_workers
-    res = run_workers(2, dict(chunk_len=65536, chunks_per_rank=6, last_bytes=300001, seed=9,
-                              strategy="RLE_DYNAMIC", seam_run=True, codec="device"))
+    res = run_workers(world, dict(chunk_len=65536, chunks_per_rank=6, last_bytes=300001, seed=9,
+                                  strategy="RLE_DYNAMIC", seam_run=True, codec="device"))
     assert res[0]["stream_equal"]
     assert all(r["gathered_equal"] for r in res)      # the device gather onto rank 0
     assert all(r["code"] == 0 and r["decoded_equal"] for r in res)

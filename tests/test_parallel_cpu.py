@@ -44,6 +44,8 @@ def test_sharded_stream_roundtrip(world, cfg):
         assert r["code"] == 0
         assert r["decoded_equal"]
     assert all(r["resolved"] == 1 for r in res[1:])
+    # the ranks between the first and the last pass their window on before resolving (inflate_tail)
+    assert all(r["tails"] == 1 for r in res[1:-1])
 
 
 @pytest.mark.parametrize("world,lie", [(2, False), (3, False), (2, True)])
