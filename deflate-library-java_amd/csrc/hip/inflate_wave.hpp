@@ -134,6 +134,13 @@ struct Tok {
 constexpr uint32_t LPW = NDFL_LPW;             // words per lane segment at most (448 bits by default)
 constexpr uint32_t SW = LPW + 4;               // staged words per lane region (+ the tail window)
 constexpr uint64_t RSPAN = 64ull * LPW * 32;   // round span cap (bits)
+// Words per lane segment at least: a short round (a small block, a block's last round) is split
+// over fewer lanes rather than into segments too short for a speculative decode to meet its true
+// token boundaries before the segment ends (every such lane otherwise costs a fix-up decode).
+#ifndef NDFL_PW_MIN
+#define NDFL_PW_MIN 4
+#endif
+static_assert(NDFL_PW_MIN >= 1 && NDFL_PW_MIN <= NDFL_LPW, "NDFL_PW_MIN");
 
 struct Stage {
     uint32_t w[SW * 64];
@@ -151,7 +158,7 @@ __device__ __forceinline__ Geo make_geo(const In& in, uint64_t rs, uint64_t E, u
     g.r0 = (uint32_t)(rs - g.base);
     g.re = (uint32_t)(E - g.base);
     const uint32_t span = g.re - g.r0;
-    g.pw = pw ? pw : max(1u, ((span + 63) / 64 + 31) / 32);
+    g.pw = pw ? pw : max((uint32_t)NDFL_PW_MIN, ((span + 63) / 64 + 31) / 32);
     g.nb = (uint32_t)min(in.nbits - min(in.nbits, g.base), (uint64_t)0xFFFFFFFFu);
     return g;
 }
@@ -564,6 +571,15 @@ __device__ int build_tables(Shared& S, int lane, bool& empty_dist) {
 #ifndef NDFL_XCP1
 #define NDFL_XCP1 128
 #endif
+// The fallback phases 1..7 are decoded only when more than this many lanes of a round failed to
+// synchronise (a sign of phase-locked codes); fewer, isolated failures are resolved by the fix-up
+// sweeps alone.  NDFL_FIX_SERIAL=1 restores the in-order fix-up loop (A/B).
+#ifndef NDFL_PH_FALLBACK
+#define NDFL_PH_FALLBACK 8
+#endif
+#ifndef NDFL_FIX_SERIAL
+#define NDFL_FIX_SERIAL 0
+#endif
 constexpr uint32_t XCP1 = NDFL_XCP1, XCP2 = 1024;
 constexpr uint32_t NPH = 8;
 constexpr uint32_t NOCP = 0xFFFFFFFFu;
@@ -699,7 +715,7 @@ __device__ void round_decode(const In& in, const Tabs& t, bool ed, uint64_t rs, 
         // lane j0 started right (its predecessor is exact) but did not meet its own speculation:
         // its verify run already decoded the segment.  Lanes after it resolve in order.
         nslow += (uint32_t)__popcll(um);
-        const uint32_t nph = __popcll(um) > 2 ? NPH : 1u;
+        const uint32_t nph = __popcll(um) > NDFL_PH_FALLBACK ? NPH : 1u;
         if (nph > 1 && (uint32_t)lane > j0) {
             for (uint32_t f = 1; f < NPH; f++) {
                 Spec q;
@@ -712,9 +728,10 @@ __device__ void round_decode(const In& in, const Tabs& t, bool ed, uint64_t rs, 
             }
         }
         S.exit_[lane] = r.end;
+        if (pc) { const uint64_t x = wall_clock64(); pc->phases += x - tk0; tk0 = x; }
+#if NDFL_FIX_SERIAL
         S.kind_[lane] = r.kind;
         __syncthreads();
-        if (pc) { const uint64_t x = wall_clock64(); pc->phases += x - tk0; tk0 = x; }
         first_term = (r.kind != T_EXIT && (uint32_t)lane == j0) ? j0 : 64u;
         first_term = __shfl(first_term, (int)j0, 64);
         for (uint32_t j = j0 + 1; j < 64 && first_term == 64; j++) {
@@ -730,6 +747,31 @@ __device__ void round_decode(const In& in, const Tabs& t, bool ed, uint64_t rs, 
             __syncthreads();
             if (S.kind_[j] != T_EXIT) first_term = j;
         }
+#else
+        // Fix-up sweeps: every lane after j0 whose start is not its predecessor's current exit
+        // re-runs its verify from that exit, all such lanes at once.  A lane whose start equals its
+        // predecessor's exit holds the exact result for that start (a synchronised run ends in its
+        // speculation's end state, an unsynchronised one decoded the whole segment), so the lanes
+        // before the first one that re-runs are exact, and each sweep makes at least one more lane
+        // exact (the first re-run starts from an exact exit).  Failures are usually isolated --
+        // the lane after a failing one meets its own speculation from the corrected start -- so a
+        // round needs two or three sweeps where the in-order loop took one step per lane.
+        first_term = 64u;
+        for (;;) {
+            __syncthreads();
+            const uint32_t st = lane ? (uint32_t)S.exit_[lane - 1] : r.start;
+            const bool redo = (uint32_t)lane > j0 && st != r.start;
+            const uint64_t cm = __ballot(redo);
+            const uint32_t fc = cm ? (uint32_t)__builtin_ctzll(cm) : 64u;
+            const uint64_t tx = __ballot((uint32_t)lane < fc && r.kind != T_EXIT);
+            if (tx) { first_term = (uint32_t)__builtin_ctzll(tx); break; }
+            if (!cm) break;
+            nfix++;
+            if (redo) verify_run(v, t, ed, nb, st, s, C1, C2, e, p0, ph, lane, nph, r);
+            __syncthreads();                    // every lane has read its predecessor's exit
+            if (redo) S.exit_[lane] = r.end;
+        }
+#endif
         if (pc) { const uint64_t x = wall_clock64(); pc->serial += x - tk0; tk0 = x; }
     }
     out.start = g.base + r.start; out.end = g.base + r.end; out.cnt = r.cnt;
@@ -1192,6 +1234,12 @@ ndfl_inflate_hdr_kernel(const uint32_t* w, uint64_t nwords, uint64_t nbits, cons
 #ifndef NDFL_COUNT_WPE
 #define NDFL_COUNT_WPE 3
 #endif
+#ifndef NDFL_REC_BATCH
+#define NDFL_REC_BATCH 16       // round records claimed per atomic (the pool keeps 65,536 spare)
+#endif
+#ifndef NDFL_TREC_BATCH
+#define NDFL_TREC_BATCH 4       // table records claimed per atomic
+#endif
 extern "C" __global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(NDFL_COUNT_WPE)))
 ndfl_inflate_count_wave_kernel(const uint32_t* w, uint64_t nwords, uint64_t nbits, const uint64_t* starts,
                                const uint64_t* stops, uint32_t nchains, const uint64_t* cands, uint32_t ncand,
@@ -1206,6 +1254,9 @@ ndfl_inflate_count_wave_kernel(const uint32_t* w, uint64_t nwords, uint64_t nbit
     PhArr* ph = ph_all + blockIdx.x;
     const In in{w, nwords, nbits};
     const uint64_t t_begin = stats ? wall_clock64() : 0;
+    // round and table records are claimed in batches per wave (one contended atomic per batch
+    // instead of one per round; unused slots of a batch stay unused)
+    uint32_t rb_next = 0, rb_end = 0, tb_next = 0, tb_end = 0;
     for (;;) {
     __syncthreads();
     if (lane == 0) s_ticket = atomicAdd(ticket, 1u);
@@ -1269,8 +1320,13 @@ ndfl_inflate_count_wave_kernel(const uint32_t* w, uint64_t nwords, uint64_t nbit
         // the block's tables and header fields for the emit pass (a table record)
         uint32_t brec = NOREC;
         if (recording && pool.nbt) {
-            if (lane == 0) brec = atomicAdd(pool.bctr, 1u);
-            brec = __shfl(brec, 0, 64);
+            if (tb_next >= tb_end) {
+                uint32_t b = 0;
+                if (lane == 0) b = atomicAdd(pool.bctr, (uint32_t)NDFL_TREC_BATCH);
+                b = __builtin_amdgcn_readfirstlane(b);
+                tb_next = b; tb_end = b + NDFL_TREC_BATCH;
+            }
+            brec = tb_next++;
             if (brec < pool.nbt) {
                 uint4* dst = (uint4*)(pool.bt + (uint64_t)brec * BT_BYTES);
                 const uint4* src = (const uint4*)&S.t;
@@ -1319,8 +1375,13 @@ ndfl_inflate_count_wave_kernel(const uint32_t* w, uint64_t nwords, uint64_t nbit
                 const bool live = (uint32_t)lane <= ft;
                 uint32_t idx = NOREC;
                 if (__all(!live || r.cnt < 0xFFFFFFFFull)) {
-                    if (lane == 0) idx = atomicAdd(pool.ctr, 1u);
-                    idx = __shfl(idx, 0, 64);
+                    if (rb_next >= rb_end) {
+                        uint32_t b = 0;
+                        if (lane == 0) b = atomicAdd(pool.ctr, (uint32_t)NDFL_REC_BATCH);
+                        b = __builtin_amdgcn_readfirstlane(b);
+                        rb_next = b; rb_end = b + NDFL_REC_BATCH;
+                    }
+                    idx = rb_next++;
                 }
                 if (idx < pool.nrec) {
                     pool.start[(uint64_t)idx * 64 + lane] = r.start;
