@@ -337,6 +337,9 @@ __device__ __noinline__ bool strict_stored(const In& in, uint64_t p) {
 #ifndef NDFL_FIND_WPE
 #define NDFL_FIND_WPE 3
 #endif
+#ifndef NDFL_FIND_LASTBLK
+#define NDFL_FIND_LASTBLK 0
+#endif
 #ifndef NDFL_STRICT_WPE
 #define NDFL_STRICT_WPE 4
 #endif
@@ -354,7 +357,22 @@ __device__ __forceinline__ void find_word(const In& in, uint64_t t, uint64_t sca
     uint32_t valid = 0xFFFFFFFFu;
     if (p0 + 35 > nbits) valid = (nbits >= p0 + 3) ? (uint32_t)((1ull << (nbits - p0 - 2)) - 1) : 0u;
     if (p0 + 32 > scan_end) valid &= (uint32_t)((1ull << (scan_end - p0)) - 1);
-    uint32_t m2 = ~b1 & b2 & valid & kraft_complete_mask(w0, w1, w2, w3);
+    // Candidates are chain starts, not a decoding decision: a block header that is no candidate is
+    // decoded by the chain before it, so the filter may pass over headers no encoder writes before a
+    // stream's last block -- BFINAL = 1 (the final block is the one block after which nothing needs a
+    // chain of its own) and HLIT or HDIST of 30 or 31 (287/288 literal/length or 31/32 distance
+    // codes: never written, the symbols past 285 / 29 are invalid) -- about a dozen operations per
+    // 32 positions, for half the strict stage's work.  NDFL_FIND_LASTBLK=1 keeps final headers (A/B).
+#if NDFL_FIND_LASTBLK
+    const uint32_t notfinal = ~0u;
+#else
+    const uint32_t notfinal = ~w0;
+#endif
+    const uint32_t h4 = (uint32_t)(W >> 4), h5 = (uint32_t)(W >> 5), h6 = (uint32_t)(W >> 6),
+                   h7 = (uint32_t)(W >> 7), d9 = (uint32_t)(W >> 9), d10 = (uint32_t)(W >> 10),
+                   d11 = (uint32_t)(W >> 11), d12 = (uint32_t)(W >> 12);
+    const uint32_t big = (NDFL_BOP3(h4, h5, h6, 0x80) & h7) | (NDFL_BOP3(d9, d10, d11, 0x80) & d12);
+    uint32_t m2 = ~b1 & b2 & valid & notfinal & ~big & kraft_complete_mask(w0, w1, w2, w3);
     // LEN == ~NLEN at byte positions p0 + 8j, j = 1..5; position i pads to j = (i + 10) / 8
     const uint64_t W12 = (uint64_t)w1 | ((uint64_t)w2 << 32);
     const uint32_t x1 = (uint32_t)(W >> 8), x2 = (uint32_t)(W >> 16), x3 = (uint32_t)(W >> 24), x4 = w1,
@@ -364,7 +382,7 @@ __device__ __forceinline__ void find_word(const In& in, uint64_t t, uint64_t sca
                          (NDFL_LENOK(x3) ? 0x003FC000u : 0u) | (NDFL_LENOK(x4) ? 0x3FC00000u : 0u) |
                          (NDFL_LENOK(x5) ? 0xC0000000u : 0u);
 #undef NDFL_LENOK
-    uint32_t m0 = ~b1 & ~b2 & valid & okm;
+    uint32_t m0 = ~b1 & ~b2 & valid & notfinal & okm;
     while (m2) {
         const uint32_t o = __builtin_ctz(m2);
         m2 &= m2 - 1;
@@ -856,6 +874,29 @@ ndfl_inflate_order_kernel(const uint64_t* cands, uint32_t n, uint64_t end_bit, u
     for (uint32_t k = threadIdx.x; k < n; k += blockDim.x) order[atomicAdd(&bc[bucket(k)], 1u)] = k;
 }
 
+// The emit pass's claim order over the linked chain list (info[LI_NCH] chains): costliest first, by
+// a cost key of input bits and output bytes (32 Kbit or 16 KiB per unit), so that no long chain --
+// a stream's last blocks, which share one chain -- starts at the end of the pass.  One workgroup.
+extern "C" __global__ void __launch_bounds__(1024)
+ndfl_inflate_emit_order_kernel(const EmitChain* chains, const uint64_t* info, uint32_t* order) {
+    constexpr uint32_t NB = 24;
+    __shared__ uint32_t bc[NB + 1];
+    if (info[LI_FLAGS]) return;                 // (the emit pass does not run)
+    const uint32_t n = (uint32_t)info[LI_NCH];
+    if (threadIdx.x <= NB) bc[threadIdx.x] = 0;
+    __syncthreads();
+    auto bucket = [&](uint32_t k) -> uint32_t {
+        const EmitChain& e = chains[k];
+        const uint64_t key = ((e.end_bit - e.start_bit) >> 15) + (e.out_count >> 14);
+        return NB - 1 - (uint32_t)min<uint64_t>(NB - 1, key);
+    };
+    for (uint32_t k = threadIdx.x; k < n; k += blockDim.x) atomicAdd(&bc[bucket(k) + 1], 1u);
+    __syncthreads();
+    if (threadIdx.x == 0) for (uint32_t b = 0; b < NB; b++) bc[b + 1] += bc[b];
+    __syncthreads();
+    for (uint32_t k = threadIdx.x; k < n; k += blockDim.x) order[atomicAdd(&bc[bucket(k)], 1u)] = k;
+}
+
 // Linking by pointer jumping.  Chain k links to the chain starting where it stopped when it stopped
 // at a block boundary that is the next candidate (res[k].next), before the range end; the links form
 // a forest (a false candidate's chain may end on a real boundary too).  Init: J0 = the link, S = the
@@ -1268,6 +1309,10 @@ static int inflate_devlink(InflateScratch& S, hipStream_t s, const uint32_t* d_w
                        (const uint64_t*)Ssum[cur], (const uint32_t*)Dd[cur], (const ChainRes*)S.d_res,
                        (const uint64_t*)S.d_cands, ncand, dict_len, end_bit, out_cap, (EmitChain*)S.d_chains, info);
     INF_CHK(hipGetLastError());
+    // the emit pass claims the linked chains costliest first (the count pass's order buffer is free)
+    hipLaunchKernelGGL(ndfl_inflate_emit_order_kernel, dim3(1), dim3(1024), 0, s, (const EmitChain*)S.d_chains,
+                       (const uint64_t*)info, d_order);
+    INF_CHK(hipGetLastError());
     // emit into the output (or a device staging buffer sized by the bound out_cap)
     uint8_t* d_out;
     const bool direct = (flags & 2u) != 0;
@@ -1294,7 +1339,8 @@ static int inflate_devlink(InflateScratch& S, hipStream_t s, const uint32_t* d_w
     hipLaunchKernelGGL(ndfl_inflate_emit_wave_kernel, dim3(std::min<uint32_t>(ncand, emit_grid)), dim3(64), 0, s, d_w,
                        nwords, nbits, (const EmitChain*)S.d_chains, ncand, (uint32_t*)S.d_ticket, d_out,
                        (ChainRes*)S.d_res, (const uint64_t*)S.d_cands, ncand, (uint32_t*)S.d_ref, (uint32_t*)S.d_pend,
-                       S.pool, (wv::PhArr*)S.d_ph, stats_on ? (uint32_t*)S.d_stats : nullptr, (const uint64_t*)info);
+                       S.pool, (wv::PhArr*)S.d_ph, stats_on ? (uint32_t*)S.d_stats : nullptr, (const uint64_t*)info,
+                       (const uint32_t*)d_order);
     INF_CHK(hipGetLastError());
     INF_CHK(hipEventRecord(S.ev[5], s));
     hipLaunchKernelGGL(ndfl_inflate_summary_kernel, dim3(1), dim3(1024), 0, s, (const ChainRes*)S.d_res,
@@ -1758,7 +1804,8 @@ static int inflate_run(InflateScratch& S, hipStream_t s, const uint8_t* in, uint
     hipLaunchKernelGGL(ndfl_inflate_emit_wave_kernel, dim3(std::min<uint32_t>(nch, emit_grid)), dim3(64), 0, s, d_w,
                        nwords, nbits, (const EmitChain*)S.d_chains, nch, (uint32_t*)S.d_ticket, d_out,
                        (ChainRes*)S.d_res, (const uint64_t*)S.d_cands, ncand, (uint32_t*)S.d_ref, (uint32_t*)S.d_pend,
-                       pool, (wv::PhArr*)S.d_ph, stats_on ? (uint32_t*)S.d_stats : nullptr, (const uint64_t*)nullptr);
+                       pool, (wv::PhArr*)S.d_ph, stats_on ? (uint32_t*)S.d_stats : nullptr, (const uint64_t*)nullptr,
+                       (const uint32_t*)nullptr);
     INF_CHK(hipGetLastError());
     INF_CHK(hipEventRecord(e3, s));
     std::vector<ChainRes> er(nch);

@@ -1462,7 +1462,7 @@ extern "C" __global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per
 ndfl_inflate_emit_wave_kernel(const uint32_t* w, uint64_t nwords, uint64_t nbits, const EmitChain* chains,
                               uint32_t nlist, uint32_t* ticket, uint8_t* out, ChainRes* res, const uint64_t* cands,
                               uint32_t ncand, uint32_t* ref, uint32_t* pend, SegPool pool, wv::PhArr* ph_all,
-                              uint32_t* stats, const uint64_t* info) {
+                              uint32_t* stats, const uint64_t* info, const uint32_t* eorder) {
     using namespace wv;
     __shared__ __attribute__((aligned(16))) Shared S;
     __shared__ Stage stg;
@@ -1479,8 +1479,8 @@ ndfl_inflate_emit_wave_kernel(const uint32_t* w, uint64_t nwords, uint64_t nbits
     __syncthreads();
     if (lane == 0) s_ticket = atomicAdd(ticket, 1u);
     __syncthreads();
-    const uint32_t ci = s_ticket;
-    if (ci >= nlist) break;
+    if (s_ticket >= nlist) break;
+    const uint32_t ci = eorder ? eorder[s_ticket] : s_ticket;    // (costliest chains first)
     const In in{w, nwords, nbits};
     const EmitChain ch = chains[ci];
     const uint64_t t_chain = stats ? wall_clock64() : 0;
