@@ -725,6 +725,10 @@ __device__ __forceinline__ void deflate_chunk(const Args& a, uint32_t* obuf, PS&
         __VA_ARGS__                                                                                    \
     }
 #define NDFL_BYTE(j) ((((j) < 4 ? gw0_ : gw1_) >> (8 * ((j) & 3))) & 0xFFu)
+    // literal copies per group byte j: r1 + r2 + r3 (the classes nest), as a popcount of bits j,
+    // j + 8 and j + 16 of the group's packed class word
+#define NDFL_REPS() (r1g_ | (r2g_ << 8) | (r3g_ << 16))
+#define NDFL_REP(j) ((uint32_t)__builtin_popcount(R_ & (0x010101u << (j))))
     // a run starting at group byte j: its value v, start gpos and end pend (next start)
 #define NDFL_RUN(j, ...)                                                                               \
     if (anyL_ && ((lgg_ >> (j)) & 1)) {                                                                \
@@ -748,11 +752,11 @@ __device__ __forceinline__ void deflate_chunk(const Args& a, uint32_t* obuf, PS&
     }
     if (MODE != MODE_EMIT) {
     NDFL_FOR_GROUPS({
+        const uint32_t R_ = NDFL_REPS();
 _Pragma("unroll")
         for (int j = 0; j < 8; j++) {
             const uint32_t v = NDFL_BYTE(j);
-            uint32_t rep = (r1g_ >> j) & 1;
-            if (any2_) rep += ((r2g_ >> j) & 1) + ((r3g_ >> j) & 1);
+            const uint32_t rep = NDFL_REP(j);
             if (rep) atomicAdd(&hl[v], rep);
             NDFL_RUN(j, {
                 const uint32_t lead = lead_of(gpos, v);
@@ -813,11 +817,11 @@ _Pragma("unroll")
         uint32_t pf[8];
 _Pragma("unroll")
         for (int j = 0; j < 8; j++) pf[j] = ps.litCode[NDFL_BYTE(j)];
+        const uint32_t R_ = NDFL_REPS();
 _Pragma("unroll")
         for (int j = 0; j < 8; j++) {
             const uint32_t lv = pf[j] >> 16;
-            const uint32_t rep = ((r1g_ >> j) & 1) + ((r2g_ >> j) & 1) + ((r3g_ >> j) & 1);
-            mybits += rep * lv;
+            mybits += NDFL_REP(j) * lv;
             NDFL_RUN(j, {
                 const uint32_t lead = lead_of(gpos, v);
                 const uint32_t R = pend - gpos - lead;
