@@ -841,9 +841,17 @@ __device__ __forceinline__ void phase_multi(const Lv& v, const Tabs& t, bool ed,
 #pragma unroll
         for (int k = 0; k < N; k++) { f[k] = l[k] && p[k] + 48 < e; any = any || f[k]; }
         if (!any) break;
-        uint32_t lo[N], hi[N], en[N];
+        // each run's window is its low word pair only; the third word (for a length/distance token's
+        // distance bits) is read in the rare non-literal branch -- phase-locked codes are literals
+        uint32_t lo[N], wb[N], en[N];
 #pragma unroll
-        for (int k = 0; k < N; k++) v.win(f[k] ? p[k] : p[0], lo[k], hi[k]);
+        for (int k = 0; k < N; k++) {
+            const uint32_t pp = f[k] ? p[k] : p[0];
+            const uint32_t* qk = v.p + ((pp >> 5) - v.rw) * 64;
+            const uint32_t a = qk[0];
+            wb[k] = qk[64];
+            lo[k] = __builtin_amdgcn_alignbit(wb[k], a, pp & 31);
+        }
 #pragma unroll
         for (int k = 0; k < N; k++) en[k] = t.lit[lo[k] & ((1u << LB) - 1u)];
 #pragma unroll
@@ -852,7 +860,9 @@ __device__ __forceinline__ void phase_multi(const Lv& v, const Tabs& t, bool ed,
             if (q) { const bool two = (en[k] >> 8) & 1; p[k] += two ? (en[k] >> 4) & 15 : en[k] & 15; c[k] += two ? 2u : 1u; }
             if (f[k] && !q) {
                 Tok tk;
-                tok_e<false>(lo[k], hi[k], en[k], p[k], t, ed, e, nb, tk);
+                const uint32_t cw = v.p[((p[k] >> 5) - v.rw) * 64 + 128];
+                const uint32_t hi = __builtin_amdgcn_alignbit(cw, wb[k], p[k] & 31);
+                tok_e<false>(lo[k], hi, en[k], p[k], t, ed, e, nb, tk);
                 if (tk.kind > K_LEN) { l[k] = false; O[k].kr = tk.kind == K_EOB ? (T_EOB << 5) : ((T_ERR << 5) | tk.val); }
                 else c[k] += tk.n;
             }
