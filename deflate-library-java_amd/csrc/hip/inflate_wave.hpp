@@ -232,11 +232,17 @@ __device__ __forceinline__ void tok_e(uint32_t lo, uint32_t hi, uint32_t e, uint
     uint32_t kind, val, n = 1, dist = 0;
     do {
         if (e >> 31) {
-            const uint32_t l1 = e & 15, l12 = (e >> 4) & 15;
+            // [3:0] the entry's advance (both codes of a pair), [7:4] the first code's length
+            const uint32_t adv = e & 15;
             bool two = (e >> 8) & 1;
-            if (CAREFUL) two = two && pos + l1 < stop && pos + l12 <= nb;
-            pos += two ? l12 : l1;
-            kind = K_LIT; n = two ? 2u : 1u; val = (e >> 9) & (two ? 0xFFFFu : 0xFFu);
+            if (CAREFUL) {
+                const uint32_t l1 = (e >> 4) & 15;
+                two = two && pos + l1 < stop && pos + adv <= nb;
+                pos += two ? adv : l1;
+            } else {
+                pos += adv;
+            }
+            kind = K_LIT; n = 1u + (uint32_t)two; val = (e >> 9) & (two ? 0xFFFFu : 0xFFu);
             if (CAREFUL && pos > nb) { kind = K_BAD; val = R_UEOS; n = 1; }
             break;
         }
@@ -498,8 +504,9 @@ __device__ int build_code(Shared& S, uint32_t base, uint32_t n, uint32_t* prim, 
 }
 
 // Literal pairs in the primary table: an entry whose code is a literal becomes
-// 1 << 31 | l1 | l12 << 4 | pair << 8 | b1 << 9 | b2 << 17, with l12 = l1 + l2 and pair set when the
-// next LB - l1 bits start with a second literal code (its length l2 <= LB - l1).
+// 1 << 31 | adv | l1 << 4 | pair << 8 | b1 << 9 | b2 << 17, with pair set when the next LB - l1 bits
+// start with a second literal code (its length l2 <= LB - l1) and adv = l1 + l2 for a pair, l1
+// otherwise -- an unchecked step adds adv with no select.
 __device__ void group_lits(Tabs& t, int lane) {
     uint32_t nv[(1u << LB) / 64];
 #pragma unroll
@@ -514,7 +521,7 @@ __device__ void group_lits(Tabs& t, int lane) {
             const uint32_t e2 = t.lit[k >> l1];
             const uint32_t l2 = e2 & 31;
             if (l1 < LB && l2 && l1 + l2 <= LB && ((e2 >> 9) & 3) == K_LIT)
-                v = (1u << 31) | l1 | ((l1 + l2) << 4) | (1u << 8) | (b1 << 9) | (((e2 >> 16) & 0xFFu) << 17);
+                v = (1u << 31) | (l1 + l2) | (l1 << 4) | (1u << 8) | (b1 << 9) | (((e2 >> 16) & 0xFFu) << 17);
         }
         nv[q] = v;
     }
@@ -857,7 +864,7 @@ __device__ __forceinline__ void phase_multi(const Lv& v, const Tabs& t, bool ed,
 #pragma unroll
         for (int k = 0; k < N; k++) {
             const bool q = f[k] && (en[k] >> 31);
-            if (q) { const bool two = (en[k] >> 8) & 1; p[k] += two ? (en[k] >> 4) & 15 : en[k] & 15; c[k] += two ? 2u : 1u; }
+            if (q) { p[k] += en[k] & 15; c[k] += 1u + ((en[k] >> 8) & 1u); }
             if (f[k] && !q) {
                 Tok tk;
                 const uint32_t cw = v.p[((p[k] >> 5) - v.rw) * 64 + 128];
