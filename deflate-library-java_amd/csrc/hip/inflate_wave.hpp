@@ -722,18 +722,22 @@ __device__ void round_decode(const In& in, const Tabs& t, bool ed, uint64_t rs, 
         // lane j0 started right (its predecessor is exact) but did not meet its own speculation:
         // its verify run already decoded the segment.  Lanes after it resolve in order.
         nslow += (uint32_t)__popcll(um);
-        const uint32_t nph = __popcll(um) > NDFL_PH_FALLBACK ? NPH : 1u;
-        if (nph > 1 && (uint32_t)lane > j0) {
-            for (uint32_t f = 1; f < NPH; f++) {
-                Spec q;
-                spec_run(v, t, ed, nb, min(s + f, e), s, C1, C1, e, q);
-                // (offsets and byte counts at the first checkpoint fit 16 bits; otherwise no match)
-                ph->cp[f - 1][lane] = (q.cp1 < 0xFFFFu && q.cpc1 <= 0xFFFFu) ? (q.cp1 | (q.cpc1 << 16)) : 0xFFFFu;
-                ph->end[f - 1][lane] = q.end - s;
-                ph->cnt[f - 1][lane] = q.cnt;
-                ph->kr[f - 1][lane] = (uint8_t)((q.kind << 5) | q.reason);
+        uint32_t nph = __popcll(um) > NDFL_PH_FALLBACK ? NPH : 1u;
+        // the lanes after `from` decode their segments from the phases s+1 .. s+7 as well
+        auto phase_runs = [&](uint32_t from) {
+            if ((uint32_t)lane > from) {
+                for (uint32_t f = 1; f < NPH; f++) {
+                    Spec q;
+                    spec_run(v, t, ed, nb, min(s + f, e), s, C1, C1, e, q);
+                    // (offsets and byte counts at the first checkpoint fit 16 bits; otherwise no match)
+                    ph->cp[f - 1][lane] = (q.cp1 < 0xFFFFu && q.cpc1 <= 0xFFFFu) ? (q.cp1 | (q.cpc1 << 16)) : 0xFFFFu;
+                    ph->end[f - 1][lane] = q.end - s;
+                    ph->cnt[f - 1][lane] = q.cnt;
+                    ph->kr[f - 1][lane] = (uint8_t)((q.kind << 5) | q.reason);
+                }
             }
-        }
+        };
+        if (nph > 1) phase_runs(j0);
         S.exit_[lane] = r.end;
         if (pc) { const uint64_t x = wall_clock64(); pc->phases += x - tk0; tk0 = x; }
 #if NDFL_FIX_SERIAL
@@ -763,18 +767,32 @@ __device__ void round_decode(const In& in, const Tabs& t, bool ed, uint64_t rs, 
         // exact (the first re-run starts from an exact exit).  Failures are usually isolated --
         // the lane after a failing one meets its own speculation from the corrected start -- so a
         // round needs two or three sweeps where the in-order loop took one step per lane.
+        // In a cascade (phase-locked stretches: each corrected lane misses its speculation again) a
+        // sweep only moves the exact prefix by one lane, and lanes re-running from starts that are
+        // about to change again only lengthen the sweep; so after the first sweep a lane re-runs only
+        // when it is the first inconsistent lane or its predecessor's exit held still last sweep.
         first_term = 64u;
+        uint64_t chgm = 0;                      // lanes whose exit moved in the last sweep
         for (;;) {
             __syncthreads();
             const uint32_t st = lane ? (uint32_t)S.exit_[lane - 1] : r.start;
-            const bool redo = (uint32_t)lane > j0 && st != r.start;
-            const uint64_t cm = __ballot(redo);
+            const bool inc = (uint32_t)lane > j0 && st != r.start;
+            const uint64_t cm = __ballot(inc);
             const uint32_t fc = cm ? (uint32_t)__builtin_ctzll(cm) : 64u;
             const uint64_t tx = __ballot((uint32_t)lane < fc && r.kind != T_EXIT);
             if (tx) { first_term = (uint32_t)__builtin_ctzll(tx); break; }
             if (!cm) break;
             nfix++;
-            if (redo) verify_run(v, t, ed, nb, st, s, C1, C2, e, p0, ph, lane, nph, r);
+            const bool pchg = lane > 0 && ((chgm >> (lane - 1)) & 1ull);
+            const bool redo = inc && ((uint32_t)lane == fc || !pchg);
+            const uint32_t old_end = r.end;
+            bool met = true;
+            if (redo) met = verify_run(v, t, ed, nb, st, s, C1, C2, e, p0, ph, lane, nph, r);
+            // the frontier lane re-ran from an exact start and still missed its own speculation: a
+            // phase-locked stretch (e.g. fixed-Huffman text), where every later lane would miss too
+            // -- decode the phase runs now, once, so that the next re-runs meet one of them
+            if (nph == 1 && __any((uint32_t)lane == fc && !met)) { phase_runs(fc); nph = NPH; }
+            chgm = __ballot(redo && r.end != old_end);
             __syncthreads();                    // every lane has read its predecessor's exit
             if (redo) S.exit_[lane] = r.end;
         }
