@@ -753,6 +753,14 @@ __device__ __forceinline__ void deflate_chunk(const Args& a, uint32_t* obuf, PS&
     if (MODE != MODE_EMIT) {
     NDFL_FOR_GROUPS({
         const uint32_t R_ = NDFL_REPS();
+        if (!anyL_) {                           // (wave-uniform: no run starts in the group)
+_Pragma("unroll")
+            for (int j = 0; j < 8; j++) {
+                const uint32_t rep = NDFL_REP(j);
+                if (rep) atomicAdd(&hl[NDFL_BYTE(j)], rep);
+            }
+            continue;
+        }
 _Pragma("unroll")
         for (int j = 0; j < 8; j++) {
             const uint32_t v = NDFL_BYTE(j);
@@ -818,6 +826,11 @@ _Pragma("unroll")
 _Pragma("unroll")
         for (int j = 0; j < 8; j++) pf[j] = ps.litCode[NDFL_BYTE(j)];
         const uint32_t R_ = NDFL_REPS();
+        if (!anyL_) {
+_Pragma("unroll")
+            for (int j = 0; j < 8; j++) mybits += NDFL_REP(j) * (pf[j] >> 16);
+            continue;
+        }
 _Pragma("unroll")
         for (int j = 0; j < 8; j++) {
             const uint32_t lv = pf[j] >> 16;
@@ -884,6 +897,20 @@ _Pragma("unroll")
             uint32_t pf[4];
 _Pragma("unroll")
             for (int j = 0; j < 4; j++) pf[j] = ps.litCode[NDFL_BYTE(j)];
+            if (!anyL_) {                       // (wave-uniform: literal pieces only)
+_Pragma("unroll")
+                for (int j = 0; j < 8; j++) {
+                    const uint32_t lc = pf[j & 3];
+                    if (j < 4) pf[j] = ps.litCode[NDFL_BYTE(j + 4)];
+                    const bool r1 = (r1g_ >> j) & 1;
+                    bp.put(r1 ? (lc & 0xFFFF) : 0u, r1 ? (lc >> 16) : 0u);
+                    if (any2_ && ((r2g_ >> j) & 1)) {
+                        bp.put(lc & 0xFFFF, lc >> 16);
+                        if ((r3g_ >> j) & 1) bp.put(lc & 0xFFFF, lc >> 16);
+                    }
+                }
+                continue;
+            }
 _Pragma("unroll")
             for (int j = 0; j < 8; j++) {
                 const uint32_t lc = pf[j & 3];
