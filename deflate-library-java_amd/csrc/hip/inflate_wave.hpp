@@ -587,7 +587,10 @@ __device__ int build_tables(Shared& S, int lane, bool& empty_dist) {
 #ifndef NDFL_FIX_SERIAL
 #define NDFL_FIX_SERIAL 0
 #endif
-constexpr uint32_t XCP1 = NDFL_XCP1, XCP2 = 1024;
+#ifndef NDFL_XCP2
+#define NDFL_XCP2 1024
+#endif
+constexpr uint32_t XCP1 = NDFL_XCP1, XCP2 = NDFL_XCP2;
 constexpr uint32_t NPH = 8;
 constexpr uint32_t NOCP = 0xFFFFFFFFu;
 constexpr uint64_t MAX_SPAN = RSPAN;         // round span cap
