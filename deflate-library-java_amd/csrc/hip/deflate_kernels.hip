@@ -279,24 +279,30 @@ __device__ void canon_codes(const uint8_t* lens, int n, uint32_t* codes, char* s
     __syncthreads();
 }
 
+// One lane's bits into the LDS bit buffer: a 32-bit accumulator (one shift-or per code); a code that
+// crosses the word boundary leaves its top bits as the next word's start (v >> (32 - nb_before),
+// 1..30 bits since n <= 30), and the word goes out with one LDS atomicOr.
 struct BitPut {
-    uint64_t acc;
+    uint32_t lo;
     uint32_t nb;
-    uint32_t wi;
-    uint32_t* buf;
-    __device__ __forceinline__ void init(uint32_t* b, uint32_t bitpos) { buf = b; wi = bitpos >> 5; nb = bitpos & 31; acc = 0; }
-    __device__ __forceinline__ void put(uint32_t v, uint32_t n) {
-        acc |= (uint64_t)v << nb;
-        nb += n;
+    uint32_t wb;         // byte offset of the word being filled
+    char* buf;
+    __device__ __forceinline__ void init(uint32_t* b, uint32_t bitpos) {
+        buf = (char*)b; wb = (bitpos >> 5) * 4; nb = bitpos & 31; lo = 0;
+    }
+    __device__ __forceinline__ void put(uint32_t v, uint32_t n) {     // v < 2^n, n <= 30
+        const uint32_t nb0 = nb;
+        lo |= v << nb0;
+        nb = nb0 + n;
         if (nb >= 32) {
-            atomicOr(&buf[wi], (uint32_t)acc);
-            wi++;
-            acc >>= 32;
+            atomicOr((uint32_t*)(buf + wb), lo);
+            wb += 4;
             nb -= 32;
+            lo = v >> (32 - nb0);
         }
     }
     __device__ __forceinline__ void flush() {
-        if (nb) atomicOr(&buf[wi], (uint32_t)acc);
+        if (nb) atomicOr((uint32_t*)(buf + wb), lo);
     }
 };
 
