@@ -3,8 +3,8 @@
 metric  "input MiB/s (compress+decompress)" (BASELINE.json): bytes fed to the two operations
         (N uncompressed into the encoder + C compressed into the decoder) per second of the step,
         MiB = 2^20, whole job over all ranks.
-step    one round trip over one batch: the rank's 4 GiB shard of the config-4 corpus
-        (Silesia-style mix, seed 0xC4 + rank) is compressed with the gzip default encoder
+step    one round trip over one batch: the rank's share of the 4 GiB config-4 corpus
+        (Silesia-style mix, seed 0xC4; all of it at N = 1) is compressed with the gzip default encoder
         (RLE_DYNAMIC, 64 KiB blocks, bit-exact with the reference) into one DEFLATE stream, and that
         stream is decompressed again.  Inputs and outputs are resident in HBM (device pointers
         through the C ABI); no host copies inside the timed region.
@@ -12,17 +12,20 @@ N > 1   rank r owns chunks [r*K, (r+1)*K) of ONE global stream.  Ranks exchange 
         their shard (history) and their compressed bit totals (RCCL all_gather over xGMI), shift
         their bits to the global bit offset on device, and decode their own bit range with the
         previous rank's last 32 KiB of output as the dictionary (RCCL point-to-point).
-        --scaling weak (default): 4 GiB per rank (seed 0xC4 + rank); --scaling strong: config 4 as
-        BASELINE.json defines it, 4 GiB in total split over the ranks, and the step also gathers the
-        global stream onto rank 0 (RCCL point-to-point into its byte offsets, shared bytes ORed on
-        device; --gather adds that to weak scaling too).
+        --scaling strong (default): config 4 as BASELINE.json defines it, 4 GiB in total split over
+        the ranks, so every N shares the N = 1 workload; --scaling weak: 4 GiB per rank (seed
+        0xC4 + rank).  The step also gathers the global stream onto rank 0 (RCCL point-to-point into
+        its byte offsets, shared bytes ORed on device).
 Run: python bench.py [--gpus N --steps K --warmup W].  With --gpus N > 1 and no WORLD_SIZE in the
 environment, bench.py starts N ranks itself (torch.distributed.run on 127.0.0.1, before anything
 touches the GPU) and exits with their status; under torch.distributed.run it is one rank.
 N > 1 gathers the global stream onto rank 0 in every step by default (north_star: "RCCL gather over
 xGMI to reassemble the output stream"; --no-gather leaves it out).
 bit_exact: every rank compares its WHOLE shard's stream with the oracle's (chunk-parallel on the
-host, outside the timed region), and the flag is the AND over ranks.
+host, outside the timed region), and the flag is the AND over ranks; with N > 1 and strong scaling
+rank 0 also compares the stream the gather assembled with the oracle's encoding of the whole corpus.
+Every collective has a timeout (--dist-timeout, 120 s): a rank that stalls ends the run with an error
+instead of a hang.
 """
 import argparse
 import ctypes
@@ -46,13 +49,15 @@ def main():
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=5)
     ap.add_argument("--warmup", type=int, default=2)
-    ap.add_argument("--size", type=int, default=4 << 30, help="bytes per rank")
+    ap.add_argument("--size", type=int, default=4 << 30, help="corpus bytes (in total; per rank with --scaling weak)")
     ap.add_argument("--cpu-sample", type=int, default=1 << 30, help="bytes for the CPU baseline leg (about 20 s of oracle work)")
     ap.add_argument("--no-cpu", action="store_true")
     ap.add_argument("--no-verify", action="store_true")
     ap.add_argument("--backend", default="nccl", help="nccl (= RCCL over xGMI); gloo only to rehearse N>1 on one GPU")
-    ap.add_argument("--scaling", choices=["weak", "strong"], default="weak",
-                    help="weak: --size bytes per rank; strong: --size bytes in total (config 4), with the gather")
+    ap.add_argument("--scaling", choices=["weak", "strong"], default="strong",
+                    help="strong (default): --size bytes in total (config 4); weak: --size bytes per rank")
+    ap.add_argument("--dist-timeout", type=float, default=120.0,
+                    help="seconds any collective / point-to-point exchange may wait before the run fails")
     ap.add_argument("--gather", action="store_true", help="(default for N > 1) gather the global stream onto rank 0")
     ap.add_argument("--no-gather", action="store_true", help="N > 1: leave the gather to rank 0 out of the step")
     ap.add_argument("--verify-threads", type=int, default=0, help="host threads of the full-stream oracle check "
@@ -76,10 +81,9 @@ def main():
     dist = None
     if world > 1:
         import torch.distributed as dist
-        if args.backend == "nccl":
-            dist.init_process_group("nccl", device_id=torch.device("cuda", local))
-        else:
-            dist.init_process_group(args.backend)
+        from ndfl import parallel as P
+        P.init_process_group(dist, args.backend, torch.device("cuda", local) if args.backend == "nccl" else None,
+                             args.dist_timeout)
 
     gather = world > 1 and not args.no_gather
     if args.scaling == "strong" and world > 1:
@@ -89,7 +93,8 @@ def main():
         n = per if rank + 1 < world else args.size - off
         full = corpus.c4_mixed(args.size, seed=0xC4, device="cuda")
         data = full[off:off + n].clone()
-        del full
+        if rank != 0 or not gather:
+            del full                  # (rank 0 keeps it to check the gathered stream)
     else:
         n = args.size
         data = corpus.c4_mixed(n, seed=0xC4 + rank, device="cuda")
@@ -139,6 +144,7 @@ def main():
             if pend is not None:
                 state["stream"] = pend.wait()
             state["dict_len"] = dl
+            state["total_bits"] = part.bit_offsets[-1]
         if r != 0:
             raise RuntimeError(f"decode error {r}")
         tm = ctx.timings()
@@ -210,10 +216,19 @@ def main():
                              device="cpu" if args.backend == "gloo" else "cuda")
             dist.all_reduce(f, op=dist.ReduceOp.MIN)
             exact["all_ranks"] = bool(f.item())
+        if rank == 0 and gather and args.scaling == "strong":
+            # the stream rank 0 actually holds after the last step's gather (parts received into a
+            # reused buffer while the shards decoded) against the oracle's single-stream encoding
+            # of the whole corpus: the one-GPU stream of the same bytes, bit for bit
+            g = verify_stream(full, None, True, state["stream"], state["total_bits"],
+                              args.verify_threads or max(1, min(16, os.cpu_count() or 1)))
+            exact["gathered"] = {k: g[k] for k in ("bit_exact", "bits_compared", "sha256", "total_s")}
+            del full
     cpu = None
     if rank == 0 and not args.no_cpu:
         cpu = cpu_baseline(data, args.cpu_sample)
-        cpu["bit_exact"] = exact["all_ranks"] if world > 1 else exact["bit_exact"]
+        cpu["bit_exact"] = (exact["all_ranks"] and exact.get("gathered", {"bit_exact": True})["bit_exact"]) \
+            if world > 1 else exact["bit_exact"]
         cpu["verify"] = exact
 
     if rank == 0:
@@ -226,7 +241,7 @@ def main():
             "warmup": args.warmup,
             "ms_per_step": round(per * 1e3, 3),
             "higher_is_better": True,
-            "scaling": args.scaling if world > 1 else "weak",
+            "scaling": args.scaling,
             "vs_baseline": None,
             "dtype": "u8",
             "data": "synthetic (config-4 Silesia-style mix, generated on device, " +

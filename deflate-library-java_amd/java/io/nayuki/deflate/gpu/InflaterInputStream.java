@@ -6,8 +6,15 @@
  * granularity -- and the decode continues from that bit with the last 32 KiB of output as the
  * window (the reference's dictionary ring, :592-603).  With endExactly the underlying stream is
  * reset to its mark and skipped to the byte after the final block (Open.finish, :113-124).
- * Errors: a Reason code raises DataFormatException after the bytes decoded before the error were
- * served (not sticky); an IOException of the underlying stream is sticky (:152-159).
+ * Errors: a Reason code raises DataFormatException from the read call that reaches it, as Open.read
+ * throws from inside the call (D/decomp/Open.java:83-110): a read asking for more bytes than remain
+ * before the error copies them into b uncounted and throws; a read ending at or before the error
+ * returns normally.  DataFormatException is unchecked (D/DataFormatException.java:15), so it is not
+ * sticky; an IOException of the underlying stream is (:152-159).
+ * Memory: with endExactly the underlying stream's mark is moved along with the consumed input
+ * (reset, skip the consumed bytes, mark again, skip back to the read position), so a
+ * BufferedInputStream holds at most about one batch, whatever the member's length -- the reference
+ * marks again on every fill (D/decomp/Open.java:184).
  */
 package io.nayuki.deflate.gpu;
 
@@ -52,13 +59,14 @@ public final class InflaterInputStream extends InputStream {
 		input = Objects.requireNonNull(in);
 		if (inBufLen <= 0)
 			throw new IllegalArgumentException("Non-positive input buffer size");
+		batch = Math.max(inBufLen, BATCH);
 		if (endExactly) {
 			if (!in.markSupported())
 				throw new IllegalArgumentException("Input stream not markable, cannot support detachment");
-			in.mark(Integer.MAX_VALUE);
+			markLimit = batch + MARK_SLACK;
+			in.mark(markLimit);
 		}
 		this.endExactly = endExactly;
-		batch = Math.max(inBufLen, BATCH);
 		this.in = ByteBuffer.allocateDirect(batch + 256);
 		this.in.limit(0);
 	}
@@ -99,11 +107,10 @@ public final class InflaterInputStream extends InputStream {
 			outPos += n;
 			result += n;
 		}
-		if (result == 0 && len > 0) {
-			if (error != null)
-				throw error;
+		if (result < len && error != null)
+			throw error;                    // the bytes before the error are in b, uncounted
+		if (result == 0 && len > 0)
 			return -1;
-		}
 		return (result > 0 || !last || outPos < outEnd) ? result : -1;
 	}
 	
@@ -125,7 +132,7 @@ public final class InflaterInputStream extends InputStream {
 		while (true) {
 			readMore(want);
 			final long all = in.limit();
-			long inLen = all;
+			long inLen = all, over = all;
 			var res = new long[2];
 			int r;
 			while (true) {
@@ -144,12 +151,38 @@ public final class InflaterInputStream extends InputStream {
 					break;
 				if (inLen <= 1)
 					throw new IOException("A single DEFLATE block decodes to more than " + MAX_OUT + " bytes");
+				over = inLen;                       // the shortest prefix known to overflow
 				inLen /= 2;
 			}
-			if (r == NativeCodec.NEED_INPUT && res[0] == 0 && res[1] == bit) {
-				if (inLen < all)                    // the shorter prefix completes no block
+			if (r == NativeCodec.NEED_INPUT && res[0] == 0 && res[1] == bit && inLen < all) {
+				// the shorter prefix completes no block, a longer one overflowed: search between them
+				// for a prefix that completes a block within MAX_OUT; there is none only when the
+				// first block alone decodes to more than MAX_OUT
+				long lo = inLen, hi = over;
+				boolean found = false;
+				while (hi - lo > 1 && !found) {
+					long mid = lo + (hi - lo) / 2;
+					prepareOut(Math.min(windowLen + 4 * mid + 65536, MAX_OUT));
+					r = NativeCodec.inflateRange0(codec.handle(), in, mid, bit, out, windowLen, true, res);
+					if (r == NativeCodec.E_CAPACITY && windowLen + res[0] + 16 <= MAX_OUT) {
+						prepareOut(windowLen + res[0] + 16);
+						r = NativeCodec.inflateRange0(codec.handle(), in, mid, bit, out, windowLen, true, res);
+					}
+					if (r == NativeCodec.E_CAPACITY)
+						hi = mid;
+					else if (r == NativeCodec.NEED_INPUT && res[0] == 0 && res[1] == bit)
+						lo = mid;
+					else
+						found = true;
+				}
+				if (!found)
 					throw new IOException("A single DEFLATE block decodes to more than " + MAX_OUT + " bytes");
-				want = in.limit() + batch;          // no block completed in this batch: read more
+			}
+			if (r == NativeCodec.NEED_INPUT && res[0] == 0 && res[1] == bit) {
+				// no block completed: read more.  The next attempt re-decodes the incomplete block from
+				// its start, so it waits for at least as much new input again (or for the source to
+				// run dry, see readMore)
+				want = (int)Math.min(Integer.MAX_VALUE - 512L - MARK_SLACK, in.limit() + Math.max((long)batch, in.limit()));
 				continue;
 			}
 			outPos = windowLen;
@@ -164,7 +197,7 @@ public final class InflaterInputStream extends InputStream {
 					// Open.finish: reset to the mark, skip the bytes consumed (a partly used byte counts)
 					int used = (int)((bits + 7) >>> 3);
 					input.reset();
-					input.skipNBytes(consumedBefore + used);
+					input.skipNBytes(consumedBefore + used - markPos);
 				}
 			} else {
 				error = new DataFormatException(DataFormatException.Reason.values()[r - 1], "GPU decode: " + r);
@@ -176,15 +209,31 @@ public final class InflaterInputStream extends InputStream {
 	
 	private long consumedBefore = 0;     // input bytes dropped from the front of `in`
 	
+	private static final int MARK_SLACK = 1 << 16;
+	private long markPos = 0;            // stream position of the underlying stream's mark (endExactly)
+	private int markLimit = 0;
+	
 	private void readMore(int want) throws IOException {
 		if (in.capacity() < want + 256) {
 			var bigger = ByteBuffer.allocateDirect(want + 256);
 			bigger.put(in.duplicate().position(0).limit(in.limit())).flip();
 			in = bigger;
 		}
-		// read until `want` bytes are buffered, the stream ends, or a read returns short (a pipe or
-		// socket with nothing more available yet): what is buffered is decoded first, as Open
-		// decodes from whatever its fill returned (D/decomp/Open.java:181-192)
+		if (endExactly && (consumedBefore != markPos || want + MARK_SLACK > markLimit)) {
+			// move the mark to the first unconsumed byte: the bytes after it are all a reset may
+			// need, and a BufferedInputStream keeps no more than that (served from its buffer)
+			input.reset();
+			input.skipNBytes(consumedBefore - markPos);
+			markLimit = Math.max(want, batch) + MARK_SLACK;
+			input.mark(markLimit);
+			input.skipNBytes(in.limit());
+			markPos = consumedBefore;
+		}
+		// read until `want` bytes are buffered or the stream ends.  A short read ends the read-ahead
+		// early only when nothing more is ready (available() == 0: a pipe or socket whose peer may be
+		// waiting for our output): what is buffered is decoded first, as Open decodes from whatever
+		// its fill returned (D/decomp/Open.java:181-192); with data waiting the read-ahead goes on to
+		// the batch, so a fast producer gets one GPU decode per batch, not one per pipe read
 		var tmp = new byte[65536];
 		while (in.limit() < want && !eof) {
 			int ask = Math.min(tmp.length, want - in.limit());
@@ -195,7 +244,7 @@ public final class InflaterInputStream extends InputStream {
 				int p = in.limit();
 				in.limit(p + n);
 				in.put(p, tmp, 0, n);
-				if (n < ask && in.limit() > 0)
+				if (n < ask && in.limit() > 0 && input.available() == 0)
 					break;
 			}
 		}

@@ -91,6 +91,22 @@ class DeviceCodec:
         return self.ctx.inflate_sync_raw(src.data_ptr(), in_len, from_bit, window_bits, IN_DEVICE)
 
 
+def init_process_group(dist, backend, device=None, timeout_s=120.0):
+    """One process per GPU: the process group every exchange below runs on, with a finite timeout,
+    so a rank that stalls (or an exchange issued out of order) ends the run with an error instead of
+    a hang.  `backend` "nccl" is RCCL over xGMI (`device`: this rank's GPU, bound at init); "gloo"
+    only for the CPU tests and one-GPU rehearsals."""
+    import datetime
+    import os
+    # RCCL: a timed-out operation aborts the communicator and raises on the host (the watchdog's
+    # default handling tears the process down), the gloo backend raises from the call itself
+    os.environ.setdefault("TORCH_NCCL_ASYNC_ERROR_HANDLING", "3")
+    kw = dict(timeout=datetime.timedelta(seconds=timeout_s))
+    if device is not None:
+        kw["device_id"] = device
+    dist.init_process_group(backend, **kw)
+
+
 def _staged(dist, t):
     """gloo moves host tensors only: stage device tensors through the host (tests / rehearsals on a
     single GPU); RCCL moves device tensors directly over xGMI."""

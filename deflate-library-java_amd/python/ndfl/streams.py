@@ -199,6 +199,21 @@ class _Pushback:
             out += b
         return out
 
+    def read1(self, n=-1):
+        """At most one read of the underlying stream (the pushed-back bytes first)."""
+        if self._back:
+            k = len(self._back) if n is None or n < 0 else n
+            out, self._back = self._back[:k], self._back[k:]
+            return out
+        rd = getattr(self._raw, "read1", None) or self._raw.read
+        return rd(n)
+
+    def available(self):
+        if self._back:
+            return len(self._back)
+        r = _input_ready(self._raw)
+        return None if r is None else int(r)       # (None: the raw stream cannot tell)
+
     def close(self):
         self._raw.close()
 
@@ -214,9 +229,12 @@ class InflaterInputStream:
     boundary the batch completes; the decode continues from that bit with more input and the last
     32 KiB of output as the window.  Memory stays bounded by the batch, whatever the stream length,
     and pipes / sockets work.  read(b, off, len) returns -1..len and 0 only when len == 0; -1 at end
-    of stream.  A DataFormatException is raised once the bytes decoded before the error have been
-    served (the reference raises it from the read call that reaches the error); an OSError from the
-    underlying stream is sticky (StickyException, :152-159)."""
+    of stream.  A DataFormatException is raised by the read call that reaches the error, as
+    Open.read throws from inside the call (D/decomp/Open.java:83-110): a read that asks for more
+    bytes than remain before the error copies those bytes into `b` uncounted and raises; a read that
+    ends at or before the error returns normally; every later read that needs data raises it again.
+    An OSError from the underlying stream is sticky (StickyException,
+    D/InflaterInputStream.java:151-159)."""
 
     BATCH = 64 << 20
     WINDOW = 32768
@@ -244,12 +262,19 @@ class InflaterInputStream:
         self._sticky = None
         self._on_batch = None         # container hook: called with every decoded batch (CRC / Adler)
 
+    MIN_UNKNOWN_READY = 1 << 20   # a short read from a source that cannot say whether more input
+    # is ready ends the read-ahead only after this many new bytes
+
     def _read_more(self, want):
-        """Read until `want` bytes are buffered or the stream ends -- or until a read returns fewer
-        bytes than asked for (a pipe or socket with nothing more available yet): then what is
-        buffered is decoded first, as Open decodes from whatever its fill returned
-        (D/decomp/Open.java:181-192), so a peer that waits for our output is not deadlocked."""
+        """Read until `want` bytes are buffered or the stream ends.  A read that returns fewer bytes
+        than asked for ends the read-ahead early only when the source has no more input ready
+        (available() == 0, or nothing to select on its descriptor): then what is buffered is decoded
+        first, as Open decodes from whatever its fill returned (D/decomp/Open.java:181-192), so a
+        peer that waits for our output is not deadlocked -- while a pipe with data waiting is read on
+        up to the batch size, so a fast producer still gets one GPU decode per batch, not one per
+        pipe read."""
         rd = getattr(self._in, "read1", None) or self._in.read
+        start = len(self._ibuf)
         try:
             while len(self._ibuf) < want and not self._eof:
                 ask = want - len(self._ibuf)
@@ -259,7 +284,9 @@ class InflaterInputStream:
                 else:
                     self._ibuf += b
                     if len(b) < ask:
-                        break
+                        ready = _input_ready(self._in)
+                        if ready is False or (ready is None and len(self._ibuf) - start >= self.MIN_UNKNOWN_READY):
+                            break
         except OSError as e:
             self._sticky = e
             raise
@@ -310,7 +337,10 @@ class InflaterInputStream:
             if r == _lib.NEED_INPUT and olen == 0 and bits == self._bit:
                 if self._eof:
                     check(_lib.E_INTERNAL, "ndfl_inflate_range")   # unreachable: no IN_PARTIAL at EOF
-                want = len(self._ibuf) + self._batch        # no block completed: read more
+                # no block completed: read more.  The next attempt re-decodes the incomplete block
+                # from its start (the ABI resumes at block boundaries only), so it waits for at least
+                # as much new input again -- or for the source to run dry, see _read_more
+                want = len(self._ibuf) + max(self._batch, len(self._ibuf))
                 continue
             if r < 0 or (r > len(_lib.REASONS) and r != _lib.NEED_INPUT):
                 check(r, "ndfl_inflate_range")
@@ -342,6 +372,13 @@ class InflaterInputStream:
         while self._pos == len(self._buf) and not self._final and self._error is None:
             self._fill()
 
+    def _raise_error(self):
+        # DataFormatException is unchecked in the reference (a RuntimeException,
+        # D/DataFormatException.java:15): InflaterInputStream does not turn it into its sticky state,
+        # so an empty read still returns 0; a later read that needs data raises it again here (the
+        # reference's decoder would go on from the bits after the bad symbol)
+        raise self._error
+
     def read(self, b=None, off=0, length=None):
         """read() -> int byte or -1;  read(bytearray, off, len) -> count or -1."""
         if self._state == "closed":
@@ -355,7 +392,7 @@ class InflaterInputStream:
                 self._pos += 1
                 return v
             if self._error is not None:
-                raise self._error
+                self._raise_error()
             return -1
         if length is None:
             length = len(b) - off
@@ -371,15 +408,19 @@ class InflaterInputStream:
             b[off + total:off + total + k] = self._buf[self._pos:self._pos + k]
             self._pos += k
             total += k
+        if total < length and self._error is not None:
+            self._raise_error()          # the bytes before the error are in b, uncounted
         if total == 0 and length > 0:
-            if self._error is not None:
-                raise self._error
             return -1
         if total == 0 and self._final and self._pos == len(self._buf):
             return -1          # len == 0 at end of stream (D/decomp/Open.java:109)
         return total
 
     def readall(self):
+        if self._sticky is not None:
+            raise self._sticky
+        if self._error is not None and self._pos == len(self._buf):
+            self._raise_error()
         parts = []
         while True:
             self._ensure()
@@ -389,13 +430,35 @@ class InflaterInputStream:
                 continue
             break
         if self._error is not None:
-            raise self._error
+            self._raise_error()
         return b"".join(parts)
 
     def close(self):
         if self._state != "closed" and self._in is not None:
             self._in.close()
         self._state = "closed"
+
+
+def _input_ready(f):
+    """Whether the source has input ready without blocking: its available() (a Java-style stream),
+    else a zero-timeout select on its descriptor (pipes, sockets; regular files are always ready),
+    else None (unknown)."""
+    av = getattr(f, "available", None)
+    if callable(av):
+        try:
+            n = av()
+        except Exception:
+            return None
+        return None if n is None else n > 0
+    try:
+        fd = f.fileno()
+    except Exception:
+        return None
+    try:
+        import select
+        return bool(select.select([fd], [], [], 0)[0])
+    except Exception:
+        return None
 
 
 def _seekable(f):

@@ -135,15 +135,33 @@ def split_main(rank, world, cfg):
 P_PAD = 256          # NDFL_IN_PAD_BYTES after the stream (device buffers are read in place when padded)
 
 
+def stall_main(rank, world, cfg):
+    """One rank stalls before the protocol's first exchange: the others must fail with the process
+    group's timeout instead of waiting for it (bench.py's --dist-timeout path)."""
+    import time
+    if rank == cfg["stall_rank"]:
+        time.sleep(cfg["stall_s"])
+    shard = torch.frombuffer(bytearray(mixed_bytes(65536, 1)), dtype=torch.uint8)
+    P.deflate_shard(OracleCodec(), dist, torch, shard, rank, world)
+    print("RESULT " + json.dumps([{"stalled_run_finished": True}]), flush=True)
+
+
 def main():
-    dist.init_process_group("gloo")
-    rank, world = dist.get_rank(), dist.get_world_size()
     cfg = json.loads(os.environ["NDFL_PAR_CFG"])
+    P.init_process_group(dist, "gloo", None, cfg.get("timeout_s", 120.0))
+    rank, world = dist.get_rank(), dist.get_world_size()
     if cfg.get("mode") == "split":
         return split_main(rank, world, cfg)
+    if cfg.get("mode") == "stall":
+        return stall_main(rank, world, cfg)
     chunk = cfg["chunk_len"]
     sizes = [cfg["chunks_per_rank"] * chunk] * (world - 1) + [cfg["last_bytes"]]
     data = mixed_bytes(sum(sizes), cfg["seed"])
+    if cfg.get("periodic"):
+        # one 7-byte pattern throughout: every LZ77 copy of a rank > 0 reads the window through a
+        # chain of dist-7 references as long as the rank's output / 7 (ndfl_inflate_tail gives up
+        # on chains longer than its step limit, and inflate_shard resolves before passing it on)
+        data = (b"0123456" * (len(data) // 7 + 1))[:len(data)]
     if cfg.get("seam_run"):
         # a byte run across every seam: the next rank's first block copies from the window
         b = bytearray(data)
@@ -167,7 +185,29 @@ def main():
     allp = [None] * world
     dist.all_gather_object(allp, mine)
     ok = {}
-    gathered = P.gather_stream(codec, dist, torch, part, rank, world)
+    pend = None
+    if cfg.get("async_gather"):
+        # bench.py's form: the root's buffer is preallocated (and full of garbage, as a reused buffer
+        # is), the gather is asynchronous and the shard decode runs while it is in flight
+        total = (part.bit_offsets[-1] + 7) // 8
+        garbage = torch.full((total + 100,), 0xA5, dtype=torch.uint8, device=codec.device) if rank == 0 else None
+        pend = P.gather_stream(codec, dist, torch, part, rank, world, out=garbage, async_op=True)
+        gathered = None
+    else:
+        gathered = P.gather_stream(codec, dist, torch, part, rank, world)
+    out = torch.zeros(P.WINDOW + sizes[rank] + 64, dtype=torch.uint8, device=codec.device)
+    tails = {"none": 0}
+    if cfg.get("count_tail_fallbacks"):
+        tail0 = codec.tail
+
+        def counted_tail(n):
+            t = tail0(n)
+            tails["none"] += t is None
+            return t
+        codec.tail = counted_tail
+    code, olen, dict_len = P.inflate_shard(codec, dist, torch, part, out, rank, world)
+    if pend is not None:
+        gathered = pend.wait()
     if rank == 0:
         stream = P.assemble(allp)
         ref = O.deflate(data, cfg["strategy"], chunk)
@@ -176,8 +216,7 @@ def main():
         ok["total_bits"] = part.bit_offsets[-1]
     else:
         ok["gathered_equal"] = gathered is None
-    out = torch.zeros(P.WINDOW + sizes[rank] + 64, dtype=torch.uint8, device=codec.device)
-    code, olen, dict_len = P.inflate_shard(codec, dist, torch, part, out, rank, world)
+    ok["tail_fallbacks"] = tails["none"]
     ok["code"] = code
     ok["decoded_equal"] = olen == sizes[rank] and \
         bytes(out[dict_len:dict_len + olen].cpu().numpy()) == bytes(shard.cpu().numpy())

@@ -282,6 +282,21 @@ def test_streaming_inflater_matches_oracle(ctx, batch):
         with pytest.raises(ndfl.DataFormatException) as ei:
             while (k := s.read(buf, 0, len(buf))) != -1:
                 got += buf[:k]
-        assert ei.value.getReason().name == o[0] and bytes(got) == o[1]
+        # the read that reaches the error raises (Open.read, D/decomp/Open.java:83-110): the bytes it
+        # had copied before the error are in buf, uncounted
+        rest = len(o[1]) - len(got)
+        assert ei.value.getReason().name == o[0] and 0 <= rest < len(buf)
+        assert bytes(got) + bytes(buf[:rest]) == o[1]
+        # one read asking for more than the whole good prefix raises on the first call
+        s = ndfl.InflaterInputStream(_Pipe(bytes(bad), 1000), context=ctx)
+        big = bytearray(len(o[1]) + 4096)
+        with pytest.raises(ndfl.DataFormatException) as ei:
+            s.read(big, 0, len(big))
+        assert ei.value.getReason().name == o[0] and bytes(big[:len(o[1])]) == o[1]
+        # a read ending exactly at the error returns normally, the next one raises
+        s = ndfl.InflaterInputStream(_Pipe(bytes(bad), 1000), context=ctx)
+        assert s.read(big, 0, len(o[1])) == len(o[1]) and s.read(big, 0, 0) == 0
+        with pytest.raises(ndfl.DataFormatException):
+            s.read()
     finally:
         ndfl.InflaterInputStream.BATCH = old

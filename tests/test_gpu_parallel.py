@@ -160,6 +160,29 @@ def test_sharded_protocol_ranks_one_gpu(world):
     assert all(r["code"] == 0 and r["decoded_equal"] for r in res)
 
 
+def test_sharded_protocol_async_gather_into_reused_buffer():
+    """bench.py's step shape on the GPU codec: the root gathers asynchronously into a preallocated
+    buffer full of garbage while every rank decodes its shard; the gathered stream must equal the
+    oracle's single-stream encoding."""
+    from test_parallel_cpu import run_workers
+    res = run_workers(3, dict(chunk_len=65536, chunks_per_rank=4, last_bytes=70001, seed=12,
+                              strategy="RLE_DYNAMIC", seam_run=True, codec="device", async_gather=True))
+    assert res[0]["stream_equal"] and all(r["gathered_equal"] for r in res)
+    assert all(r["code"] == 0 and r["decoded_equal"] for r in res)
+
+
+def test_sharded_protocol_window_chain_longer_than_tail_limit():
+    """A middle rank whose whole output reads the window through dist-7 LZ77 chains far longer than
+    ndfl_inflate_tail follows: the tail gives up (NDFL_E_UNSUPPORTED) and inflate_shard resolves
+    first, then passes its last 32 KiB on; every rank's output and the gathered stream stay exact."""
+    from test_parallel_cpu import run_workers
+    res = run_workers(3, dict(chunk_len=65536, chunks_per_rank=6, last_bytes=100000, seed=13,
+                              strategy="FULL_DYNAMIC", periodic=True, codec="device", count_tail_fallbacks=True))
+    assert res[0]["stream_equal"] and all(r["gathered_equal"] for r in res)
+    assert all(r["code"] == 0 and r["decoded_equal"] for r in res)
+    assert res[1]["tail_fallbacks"] == 1, res
+
+
 @pytest.mark.parametrize("stream", ["RLE_DYNAMIC", "zlib6", "FULL_DYNAMIC"])
 def test_split_decode_of_foreign_stream_two_ranks_one_gpu(stream):
     """inflate_split on the GPU: a stream without a seam index (ours, Python zlib's, LZ77) decoded by

@@ -1,0 +1,64 @@
+"""CPU guards for the committed JNI glue (deflate-library-java_amd/native/ndfl_jni.c), which this
+image cannot build for real (no JDK):
+
+  * it compiles (gcc -fsyntax-only -Wall -Wextra -Werror) against include/ndfl.h and a minimal JNI
+    header holding only the types and JNIEnv functions it uses (tests/native/jni_min/jni.h), so a
+    C-level break of the glue -- a renamed C-ABI entry point, a wrong argument count or type --
+    fails here;
+  * every `native` method of the Java shim (java/io/nayuki/deflate/gpu/NativeCodec.java) has a
+    `Java_io_nayuki_deflate_gpu_NativeCodec_<name>` definition whose parameters are the JNI mapping
+    of the Java ones, and the glue defines no entry point the shim does not declare.
+
+It does not prove the JVM side (class loading, exceptions at run time)."""
+import os
+import re
+import shutil
+import subprocess
+
+import pytest
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+PKG = os.path.join(ROOT, "deflate-library-java_amd")
+GLUE = os.path.join(PKG, "native", "ndfl_jni.c")
+SHIM = os.path.join(PKG, "java", "io", "nayuki", "deflate", "gpu", "NativeCodec.java")
+
+JNI_TYPE = {"long": "jlong", "int": "jint", "boolean": "jboolean", "void": "void", "byte": "jbyte",
+            "ByteBuffer": "jobject", "int[]": "jintArray", "long[]": "jlongArray", "byte[]": "jbyteArray"}
+
+
+@pytest.mark.skipif(shutil.which("gcc") is None, reason="gcc not installed")
+def test_jni_glue_compiles_against_the_c_abi():
+    p = subprocess.run(["gcc", "-fsyntax-only", "-Wall", "-Wextra", "-Werror", "-std=c11",
+                        "-I", os.path.join(ROOT, "tests", "native", "jni_min"), "-I", os.path.join(ROOT, "include"),
+                        GLUE], capture_output=True, text=True)
+    assert p.returncode == 0, p.stderr
+
+
+def _java_natives():
+    src = open(SHIM).read()
+    out = {}
+    for m in re.finditer(r"static\s+native\s+([\w\[\]]+)\s+(\w+)\s*\(([^)]*)\)", src):
+        ret, name, params = m.group(1), m.group(2), m.group(3)
+        types = [re.sub(r"\s+\w+$", "", p.strip()).replace(" ", "") for p in params.split(",") if p.strip()]
+        out[name] = (JNI_TYPE[ret], [JNI_TYPE[t] for t in types])
+    return out
+
+
+def _c_entry_points():
+    src = open(GLUE).read()
+    out = {}
+    for m in re.finditer(r"JNIEXPORT\s+(\w+)\s+JNICALL\s+Java_io_nayuki_deflate_gpu_NativeCodec_(\w+)\s*\(([^)]*)\)", src):
+        ret, name, params = m.group(1), m.group(2), m.group(3)
+        types = [re.sub(r"\s*\**\s*\w+$", "", p.strip()) + ("*" if "*" in p else "") for p in params.split(",")]
+        types = [t.replace(" ", "") for t in types]
+        assert types[:2] == ["JNIEnv*", "jclass"], (name, types)     # static natives: (env, class, ...)
+        out[name] = (ret, types[2:])
+    return out
+
+
+def test_jni_entry_points_match_the_java_natives():
+    java, c = _java_natives(), _c_entry_points()
+    assert java, "no native methods parsed from NativeCodec.java"
+    assert set(java) == set(c), (sorted(set(java) - set(c)), sorted(set(c) - set(java)))
+    for name, sig in java.items():
+        assert c[name] == sig, (name, sig, c[name])

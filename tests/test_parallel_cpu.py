@@ -35,6 +35,8 @@ def run_workers(world, cfg):
     (3, dict(chunk_len=65536, chunks_per_rank=2, last_bytes=7, seed=2, strategy="RLE_DYNAMIC", seam_run=True)),
     (2, dict(chunk_len=32768, chunks_per_rank=4, last_bytes=32768, seed=3, strategy="RLE_STATIC", seam_run=False)),
     (2, dict(chunk_len=65536, chunks_per_rank=2, last_bytes=65536, seed=4, strategy="FULL_DYNAMIC", seam_run=True)),
+    (3, dict(chunk_len=65536, chunks_per_rank=2, last_bytes=40000, seed=6, strategy="RLE_DYNAMIC", seam_run=True,
+             async_gather=True)),
 ])
 def test_sharded_stream_roundtrip(world, cfg):
     res = run_workers(world, cfg)
@@ -46,6 +48,25 @@ def test_sharded_stream_roundtrip(world, cfg):
     assert all(r["resolved"] == 1 for r in res[1:])
     # the ranks between the first and the last pass their window on before resolving (inflate_tail)
     assert all(r["tails"] == 1 for r in res[1:-1])
+
+
+def test_stalled_rank_times_out():
+    """bench.py's process group has a finite timeout: with one rank stalled before the protocol's
+    first exchange, the other rank fails within the timeout (non-zero exit, a timeout message)
+    instead of hanging until an outside limit."""
+    import time
+    t0 = time.time()
+    env = dict(os.environ, OMP_NUM_THREADS="1",
+               NDFL_PAR_CFG=json.dumps(dict(mode="stall", stall_rank=1, stall_s=60, timeout_s=4)))
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node=2",
+           "--master-addr", "127.0.0.1", "--master-port", str(_free_port()),
+           os.path.join(HERE, "parallel_worker.py")]
+    p = subprocess.run(cmd, env=env, capture_output=True, text=True, timeout=120)
+    took = time.time() - t0
+    assert p.returncode != 0
+    assert "RESULT" not in p.stdout
+    assert took < 50, took                      # well before the stalled rank would have woken
+    assert "timed out" in (p.stdout + p.stderr).lower() or "timeout" in (p.stdout + p.stderr).lower()
 
 
 @pytest.mark.parametrize("world,lie", [(2, False), (3, False), (2, True)])

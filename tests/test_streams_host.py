@@ -81,14 +81,20 @@ class OracleRangeCtx:
 
 
 class ShortReads(io.RawIOBase):
-    """A pipe: every read returns at most `piece` bytes."""
+    """A pipe: every read returns at most `piece` bytes.  `ready`: what available() reports (0: a
+    slow producer, nothing more has arrived after each piece; > 0: a fast producer with data
+    waiting; None: a source that cannot tell)."""
 
-    def __init__(self, data, piece):
+    def __init__(self, data, piece, ready=0):
         self._b = io.BytesIO(data)
         self._piece = piece
+        self._ready = ready
 
     def readable(self):
         return True
+
+    def available(self):
+        return self._ready
 
     def read1(self, n=-1):
         return self._b.read(min(n, self._piece) if n >= 0 else self._piece)
@@ -139,10 +145,85 @@ def test_batch_output_is_bounded(monkeypatch):
 
 
 def test_short_reads_decode_as_they_arrive(monkeypatch):
-    """A pipe returning 700-byte pieces: decoding starts before the whole batch has arrived."""
+    """A slow pipe (700-byte pieces, nothing more ready after each): decoding starts before the
+    whole batch has arrived."""
     rng = np.random.default_rng(2)
     data = rng.integers(0, 3, 300_000, dtype=np.uint8).tobytes()
     comp, bounds = _stream(data, 16384)
     got, ctx = _run(monkeypatch, comp, bounds, ShortReads(comp, 700), 1 << 20)
     assert got == data
     assert max(c[1] for c in ctx.calls) < len(comp)   # never waited for the whole stream
+
+
+def test_fast_pipe_is_read_ahead_to_the_batch(monkeypatch):
+    """A pipe with data waiting (available() > 0) returning 700-byte pieces is read on up to the
+    batch: one decode for the whole stream, not one per pipe read."""
+    rng = np.random.default_rng(2)
+    data = rng.integers(0, 3, 300_000, dtype=np.uint8).tobytes()
+    comp, bounds = _stream(data, 16384)
+    got, ctx = _run(monkeypatch, comp, bounds, ShortReads(comp, 700, ready=1 << 16), 1 << 20)
+    assert got == data
+    assert len(ctx.calls) == 1
+
+
+def test_unknown_readiness_reads_a_minimum_before_decoding(monkeypatch):
+    """A source that cannot say whether more input is ready: short reads end the read-ahead only
+    after MIN_UNKNOWN_READY new bytes, so decodes come in bounded numbers."""
+    rng = np.random.default_rng(3)
+    data = rng.integers(0, 3, 300_000, dtype=np.uint8).tobytes()
+    comp, bounds = _stream(data, 16384)
+    monkeypatch.setattr(streams.InflaterInputStream, "MIN_UNKNOWN_READY", 20_000)
+    got, ctx = _run(monkeypatch, comp, bounds, ShortReads(comp, 700, ready=None), 1 << 20)
+    assert got == data
+    assert 2 <= len(ctx.calls) <= len(comp) // 20_000 + 2
+
+
+class ErrorCtx:
+    """The decode of a corrupted stream as the ABI reports it: the bytes before the error, then
+    the Reason (+1), all from the oracle."""
+
+    def __init__(self, stream):
+        self.reason, self.out, self.bits = O.inflate(stream)
+
+    def inflate_range_raw(self, in_addr, n, start_bit, end_bit, out_addr, dict_len, out_cap, flags):
+        if len(self.out) > out_cap:
+            return _lib.E_CAPACITY, len(self.out), 0
+        ctypes.memmove(out_addr + dict_len, self.out, len(self.out))
+        return O.REASONS.index(self.reason) + 1, len(self.out), self.bits
+
+
+def _corrupt_stream():
+    rng = np.random.default_rng(4)
+    data = rng.integers(0, 3, 200_000, dtype=np.uint8).tobytes()
+    comp = bytearray(O.deflate(data, "RLE_DYNAMIC", chunk_len=16384))
+    for k in range(len(comp) * 3 // 4, len(comp)):
+        bad = bytearray(comp)
+        bad[k] ^= 0xFF
+        reason, out, _ = O.inflate(bytes(bad))
+        if reason is not None and len(out) > 50_000:
+            return bytes(bad), out, reason
+    raise AssertionError("no corruption found")
+
+
+def test_error_raised_by_the_read_that_reaches_it():
+    """Open.read throws from the call that reaches the error (D/decomp/Open.java:83-110): a read
+    asking past the last good byte raises at once (its bytes land in b uncounted); a read ending
+    exactly at the error returns normally and the next one raises; every later read that needs
+    data raises again, an empty read returns 0 (DataFormatException is unchecked, so the stream does
+    not enter its sticky state, D/InflaterInputStream.java:151-159)."""
+    bad, good, reason = _corrupt_stream()
+    s = streams.InflaterInputStream(io.BytesIO(bad), context=ErrorCtx(bad))
+    b = bytearray(len(good) + 1000)
+    with pytest.raises(ndfl.DataFormatException) as ei:
+        s.read(b, 0, len(b))
+    assert ei.value.reason.name == reason
+    assert bytes(b[:len(good)]) == good
+    assert s.read(b, 0, 0) == 0
+    with pytest.raises(ndfl.DataFormatException):
+        s.read(b, 0, 1)
+    s = streams.InflaterInputStream(io.BytesIO(bad), context=ErrorCtx(bad))
+    assert s.read(b, 0, len(good)) == len(good)      # up to the error: no exception yet
+    with pytest.raises(ndfl.DataFormatException):
+        s.read()
+    with pytest.raises(ndfl.DataFormatException):
+        s.read(b, 0, 10)
