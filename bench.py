@@ -323,7 +323,7 @@ def _append_final_empty_block(comp, nbits):
     return bytes(b[:(nbits + 10 + 7) // 8])
 
 
-def verify_stream(data_dev, hist, final, comp_dev, nbits, threads):
+def verify_stream(data_dev, hist, final, comp_dev, nbits, threads, strategy="RLE_DYNAMIC"):
     """Whole-stream bit-exactness: the oracle (C restatement of the reference encoder) compresses
     the shard chunk-parallel -- `threads` pieces of whole 64 KiB chunks, each with its own 32 KiB of
     raw history, as the reference's blocks depend only on raw input -- and every
@@ -346,7 +346,7 @@ def verify_stream(data_dev, hist, final, comp_dev, nbits, threads):
         h = (hist or b"")[-32768:] if a == 0 else host[max(0, a - 32768):a]
         pieces.append((h, a, b, final and b == n))
     with ThreadPoolExecutor(threads) as ex:
-        outs = list(ex.map(lambda p: O.deflate_chunks(p[0], host[p[1]:p[2]], final=p[3]), pieces))
+        outs = list(ex.map(lambda p: O.deflate_chunks(p[0], host[p[1]:p[2]], final=p[3], strategy=strategy), pieces))
     t1 = time.perf_counter()
     ok = sum(o[1] for o in outs) == nbits
     off = 0
@@ -364,7 +364,7 @@ def verify_stream(data_dev, hist, final, comp_dev, nbits, threads):
         ok = x.tobytes() == pb[:m]
         off += pbits
     sha = hashlib.sha256(g[:nb].tobytes()).hexdigest()
-    return {"bit_exact": bool(ok), "bits_compared": int(nbits), "bytes_in": n, "pieces": len(pieces),
+    return {"bit_exact": bool(ok), "bits_compared": int(nbits), "bytes_in": n, "pieces": len(pieces), "strategy": strategy,
             "threads": threads, "oracle_s": round(t1 - t0, 2), "total_s": round(time.perf_counter() - t0, 2),
             "sha256": sha}
 

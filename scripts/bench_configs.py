@@ -4,7 +4,9 @@
     c2  decompress a 64 MiB .gz of stored + fixed-Huffman (LZ77, dist 1..32768) blocks
         (tests/corpus.py c2_gzip; device-resident input -> output)
     c3  FULL_DYNAMIC (LZ77 + dynamic Huffman) compress of 1 GiB enwik-style text, device-resident;
-        ratio checked against the oracle on a prefix (bit-exact, so the ratio is the reference's)
+        the WHOLE stream checked against the oracle (chunk-parallel on 16 host threads: a
+        FULL_DYNAMIC block depends only on its chunk and 32 KiB of raw history,
+        D/comp/Lz77Huffman.java:71-84), so the ratio is the reference's
     c5  the 16 GiB random+repeat round trip on one GPU (RLE_DYNAMIC; corpus.c5_device), device-resident,
         the whole stream checked against the oracle
 
@@ -102,21 +104,24 @@ def c3(ctx):
         eb, _ = ctx.deflate_chunks_raw(None, 0, 32768, data.data_ptr(), n, 65536, ndfl.Lz77Huffman.FULL_DYNAMIC, True,
                                        0, out.data_ptr(), cap, DEV)
         st["eb"] = eb
+        st["td"] = ctx.timings()["deflate"]
     dt = timed(run, 2)
     comp = (st["eb"] + 7) // 8
+    from bench import verify_stream
+    v = verify_stream(data, None, True, out, st["eb"], 16, strategy="FULL_DYNAMIC")
     pre = 16 * MIB
     host = data[:pre].cpu().numpy().tobytes()
     t = time.perf_counter()
-    exp = O.deflate(host, "FULL_DYNAMIC")
+    O.deflate(host, "FULL_DYNAMIC")
     tc = time.perf_counter() - t
-    got = ctx.deflate(host, "FULL_DYNAMIC")
     dec = torch.empty(n + 64, dtype=torch.uint8, device="cuda")
     r, olen, _ = ctx.inflate_raw(out.data_ptr(), comp, dec.data_ptr(), dec.numel(), DEV)
     rt = r == 0 and olen == n and torch.equal(dec[:n], data)
     return {"config": "c3: FULL_DYNAMIC compress 1 GiB text (LZ77 + dynamic Huffman, device-resident)",
             "input_MiBps": round(n / dt / MIB, 1), "ms": round(dt * 1e3, 1), "ratio": round(comp / n, 4),
-            "prefix_bit_exact_16MiB": got == exp, "oracle_prefix_ratio": round(len(exp) / pre, 4),
-            "round_trip_ok": rt, "cpu_oracle_MiBps": round(pre / tc / MIB, 2)}
+            "bit_exact": v["bit_exact"], "verify": v, "round_trip_ok": rt,
+            "deflate_device_ms": round(st["td"], 2), "cpu_oracle_MiBps": round(pre / tc / MIB, 2),
+            "cpu_oracle_sample": "first 16 MiB, 1 thread"}
 
 
 def c5(ctx, n=16 << 30):
