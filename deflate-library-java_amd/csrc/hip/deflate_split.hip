@@ -18,22 +18,23 @@
 
 namespace {
 
-// LDS of one code-construction wave.
+// LDS of one code-construction wave (8.8 KB: 18 waves per CU; the round-3 layout's 12.4 KB held
+// 13).  Lifetimes share storage: the package-merge input keys live in pf[1] until the leaves are
+// ranked (level 0 writes pf[1] only after that), the header bits in pf[0] after the last
+// package-merge, the code-length symbols' header offsets in lf after the last package-merge; the
+// merged level is never stored (packages are summed as the merge produces them).
 struct WScr {
     uint32_t hlit[288];
     uint32_t hdist[32];
     uint32_t hdist0[32];      // distance histogram before the single-code fix-up (token bits)
     union {
-        uint32_t key[292];        // padded to a multiple of 4 (package-merge input)
-        uint32_t hdr[HDRW];       // header bits: written after the last package-merge
-    };
-    uint32_t lf[288];
-    uint16_t ls[288];
-    uint32_t pf[2][304];
-    union {
-        uint32_t mf[608];         // package-merge levels
+        uint32_t lf[288];         // ranked leaf frequencies (package-merge)
         uint16_t clOff[320];      // header bit offset of each code-length symbol (after the last one)
     };
+    uint16_t ls[288];
+    uint32_t pf[2][304];      // package frequencies of the current / next level
+    __device__ __forceinline__ uint32_t* key() { return pf[1]; }     // (292 used: n padded to 4)
+    __device__ __forceinline__ uint32_t* hdr() { return pf[0]; }     // (HDRW used)
     uint32_t mpk[15 * 20];
     uint32_t lvl[16];
     uint32_t blc[16], nxc[16], mask[16 * 10];
@@ -56,7 +57,7 @@ __device__ void wpm_lengths(const uint32_t* hist, int n, int L, uint8_t* lens, W
         const int i = base + lane;
         uint32_t k = 0xFFFFFFFFu;
         if (i < n) { const uint32_t f = hist[i]; if (f) k = f << 9 | (uint32_t)i; }
-        if (i < npad) S.key[i] = k;
+        if (i < npad) S.key()[i] = k;
         nl += (uint32_t)__popcll(__ballot(k != 0xFFFFFFFFu));
     }
     for (int t = lane; t < L * 20; t += 64) S.mpk[t] = 0;
@@ -67,11 +68,11 @@ __device__ void wpm_lengths(const uint32_t* hist, int n, int L, uint8_t* lens, W
 #pragma unroll
         for (int q = 0; q < 5; q++) {
             const int i = lane + 64 * q;
-            kk[q] = i < n ? S.key[i] : 0xFFFFFFFFu;
+            kk[q] = i < n ? S.key()[i] : 0xFFFFFFFFu;
             r[q] = 0;
         }
         for (int j = 0; j < npad; j += 4) {
-            const uint4 v = *(const uint4*)&S.key[j];
+            const uint4 v = *(const uint4*)&S.key()[j];
 #pragma unroll
             for (int q = 0; q < 5; q++)
                 r[q] += (uint32_t)(v.x < kk[q]) + (uint32_t)(v.y < kk[q]) + (uint32_t)(v.z < kk[q]) + (uint32_t)(v.w < kk[q]);
@@ -93,11 +94,12 @@ __device__ void wpm_lengths(const uint32_t* hist, int n, int L, uint8_t* lens, W
         const uint32_t m = np + nl;
         const uint32_t* pf = S.pf[cur];
         // merged order: package i before leaf j iff pf[i] <= lf[j] (packages first on equal freq).
-        // Lane l writes merged positions [k0, k1): one merge-path search for how many packages
-        // precede k0, then a sequential merge (one dependent LDS read per output instead of one
-        // binary search per item).
+        // Lane l merges positions [k0, k1): one merge-path search for how many packages precede k0,
+        // then a sequential merge (one dependent LDS read per output instead of one binary search
+        // per item).  k0 is even, so the lane sums its own pairs into the next level's packages.
+        uint32_t* pfn = S.pf[cur ^ 1];
         {
-            const uint32_t per = (m + 63) >> 6;
+            const uint32_t per = (((m + 63) >> 6) + 1) & ~1u;
             const uint32_t k0 = min(m, (uint32_t)lane * per), k1 = min(m, k0 + per);
             uint32_t lo = k0 > nl ? k0 - nl : 0u, hi = min(k0, np);
             while (lo < hi) {
@@ -108,9 +110,12 @@ __device__ void wpm_lengths(const uint32_t* hist, int n, int L, uint8_t* lens, W
             uint32_t pv = i < np ? pf[i] : 0u, lv = j < nl ? S.lf[j] : 0u;
             const uint32_t wb = k0 & ~31u;
             uint64_t bits = 0;
+            uint32_t held = 0;
             for (uint32_t pos = k0; pos < k1; pos++) {
                 const bool takeP = i < np && (j >= nl || pv <= lv);
-                S.mf[pos] = takeP ? pv : lv;
+                const uint32_t item = takeP ? pv : lv;
+                if (pos & 1) pfn[pos >> 1] = held + item;
+                held = item;
                 if (takeP) {
                     bits |= 1ull << (pos - wb);
                     i++;
@@ -125,9 +130,6 @@ __device__ void wpm_lengths(const uint32_t* hist, int n, int L, uint8_t* lens, W
         }
         __syncthreads();
         const uint32_t np2 = m >> 1;
-        uint32_t* pfn = S.pf[cur ^ 1];
-        for (uint32_t t = (uint32_t)lane; t < np2; t += 64) pfn[t] = S.mf[2 * t] + S.mf[2 * t + 1];
-        __syncthreads();
         np = np2;
         cur ^= 1;
     }
@@ -221,7 +223,7 @@ ndfl_deflate_codes_kernel(Args a) {
     uint32_t* rec = (uint32_t*)a.codes + (uint64_t)c * CREC;
     for (int i = lane; i < 288; i += 64) S.hlit[i] = h[i];
     if (lane < 32) { const uint32_t v = h[288 + lane]; S.hdist[lane] = v; S.hdist0[lane] = v; }
-    for (int i = lane; i < HDRW; i += 64) S.hdr[i] = 0;
+    for (int i = lane; i < HDRW; i += 64) S.hdr()[i] = 0;
     __syncthreads();
     uint32_t hdrBits;
     uint64_t tok = 0;                  // token bits incl. the end-of-block code
@@ -238,7 +240,7 @@ ndfl_deflate_codes_kernel(Args a) {
             if (lane < 30) tok += (uint64_t)S.hdist0[lane] * (5 + dist_extra((uint32_t)lane));
         }
         hdrBits = 3;
-        if (lane == 0) S.hdr[0] = (is_final ? 1u : 0u) | (1u << 1);
+        if (lane == 0) S.hdr()[0] = (is_final ? 1u : 0u) | (1u << 1);
         __syncthreads();
     } else {
         // trim litlen histogram, keep >= 257 (:148-151); single used distance code gets a dummy
@@ -324,7 +326,7 @@ ndfl_deflate_codes_kernel(Args a) {
         __syncthreads();
         wpm_lengths(S.clh, 19, 7, S.clLen, S);
         wcanon(S.clLen, 19, S.clCode, S);
-        for (int i = lane; i < HDRW; i += 64) S.hdr[i] = 0;          // (hdr shares key's LDS)
+        for (int i = lane; i < HDRW; i += 64) S.hdr()[i] = 0;        // (hdr shares pf[0])
         // per-symbol header bit offsets (exclusive scan, lane owns [5l, 5l+5))
         uint32_t sb[5], lsum = 0;
 #pragma unroll
@@ -353,7 +355,7 @@ ndfl_deflate_codes_kernel(Args a) {
         __syncthreads();
         // header (:134-135,236-258) into the LDS word buffer
         if (lane == 0) {
-            BitPut bp; bp.init(S.hdr, 0);
+            BitPut bp; bp.init(S.hdr(), 0);
             bp.put(is_final ? 1u : 0u, 1);
             bp.put(2u, 2);
             bp.put((uint32_t)(ln - 257), 5);
@@ -364,14 +366,14 @@ ndfl_deflate_codes_kernel(Args a) {
         }
         for (uint32_t t = (uint32_t)lane; t < tot; t += 64) {
             const uint32_t sy = S.clSym[t];
-            BitPut bp; bp.init(S.hdr, 17 + 3 * (uint32_t)ncl + S.clOff[t]);
+            BitPut bp; bp.init(S.hdr(), 17 + 3 * (uint32_t)ncl + S.clOff[t]);
             bp.put(S.clCode[sy] & 0xFFFF, S.clCode[sy] >> 16);
             if (sy >= 16) bp.put(S.clExtra[t], CL_EXTRA_BITS[sy - 16]);
             bp.flush();
         }
         __syncthreads();
     }
-    for (int i = lane; i < HDRW; i += 64) rec[CREC_HDR + i] = S.hdr[i];
+    for (int i = lane; i < HDRW; i += 64) rec[CREC_HDR + i] = S.hdr()[i];
     tok = wave_sum(tok);
     if (lane == 0) {
         rec[CREC_META] = hdrBits;

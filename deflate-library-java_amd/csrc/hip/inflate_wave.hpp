@@ -275,15 +275,101 @@ __device__ __forceinline__ void tok_e(uint32_t lo, uint32_t hi, uint32_t e, uint
     tk.kind = kind; tk.val = val; tk.n = n; tk.dist = dist;
 }
 
+// ---- register bit buffer (the unchecked token steps) ----------------------------------------------
+// A token's dependency chain through tok<false> is two LDS round trips: the window at pos (three
+// staged words), then the table entry.  Bb keeps the lane's next 32..64 bits in a 64-bit register
+// and the word after them loaded ahead, so the table read is the only LDS access on the chain; the
+// refill (one word when fewer than 32 bits are left, after the length part of a copy token too)
+// only consumes a word loaded a step earlier.  Same steps, same results as tok<false>.
+#ifndef NDFL_BITBUF
+#define NDFL_BITBUF 1
+#endif
+struct Bb {
+    uint64_t buf;      // the bits from pos on (nb of them valid)
+    uint32_t nb;       // 32..64 at a token's start
+    uint32_t wi;       // region word index of the next word to append
+    uint32_t nxt;      // that word
+    uint32_t pos;      // round-relative bit position
+};
+__device__ __forceinline__ void bb_init(Bb& b, const Lv& v, uint32_t pos) {
+    const uint32_t i = (pos >> 5) - v.rw, s = pos & 31;
+    const uint32_t* q = v.p + i * 64;
+    b.buf = ((uint64_t)q[0] | ((uint64_t)q[64] << 32)) >> s;
+    b.nb = 64 - s;
+    b.wi = i + 2;
+    b.nxt = q[128];
+    b.pos = pos;
+}
+__device__ __forceinline__ void bb_refill(Bb& b, const Lv& v) {
+    if (b.nb < 32) {
+        b.buf |= (uint64_t)b.nxt << b.nb;
+        b.nb += 32;
+        b.wi++;
+        b.nxt = v.p[b.wi * 64];
+    }
+}
+__device__ __forceinline__ void bb_skip(Bb& b, uint32_t n) {
+    b.buf >>= n; b.nb -= n; b.pos += n;
+}
+// tok<false> on the bit buffer (the caller guarantees pos + 48 < stop <= nb)
+__device__ __forceinline__ void tok_bb(Bb& b, const Lv& v, const Tabs& t, bool empty_dist, Tok& tk) {
+    uint32_t lo = (uint32_t)b.buf;
+    uint32_t e = t.lit[lo & ((1u << LB) - 1u)];
+    uint32_t kind, val, n = 1, dist = 0;
+    do {
+        if (e >> 31) {
+            const uint32_t adv = e & 15;
+            bb_skip(b, adv);
+            kind = K_LIT; n = 1u + ((e >> 8) & 1u); val = (e >> 9) & (n == 2 ? 0xFFFFu : 0xFFu);
+            break;
+        }
+        if (!(e & 31)) e = long_lit(e, lo, t);
+        const uint32_t cl = e & 31, k = (e >> 9) & 3;
+        if (k != K_LEN) {
+            bb_skip(b, cl);
+            kind = k; val = k == K_LIT ? e >> 16 : (uint32_t)R_RESERVED_LEN;
+            break;
+        }
+        const uint32_t xb = (e >> 5) & 15;
+        const uint32_t run = (e >> 16) + ((lo >> cl) & ((1u << xb) - 1u));
+        bb_skip(b, cl + xb);
+        if (empty_dist) { kind = K_BAD; val = R_EMPTY_DIST; break; }
+        bb_refill(b, v);
+        const uint32_t dw = (uint32_t)b.buf;
+        uint32_t d = t.dst[dw & ((1u << DB) - 1u)];
+        if (!(d & 31)) d = long_dist(d, dw, t);
+        const uint32_t dl = d & 31, dxb = (d >> 5) & 15;
+        if (((d >> 9) & 3) == K_BAD) { bb_skip(b, dl); kind = K_BAD; val = R_RESERVED_DIST; break; }
+        dist = (d >> 16) + ((dw >> dl) & ((1u << dxb) - 1u));
+        bb_skip(b, dl + dxb);
+        kind = K_LEN; n = run; val = 0;
+    } while (false);
+    bb_refill(b, v);
+    tk.kind = kind; tk.val = val; tk.n = n; tk.dist = dist;
+}
+
 // Count tokens from pos to the first token boundary at or past `stop` (<= input end) or to a
 // terminal token (true: end of block or an error, in tk).
 __device__ __forceinline__ bool run_to(const Lv& v, uint32_t& pos, const Tabs& t, bool ed, uint32_t stop, uint32_t nb,
                                        uint32_t& cnt, Tok& tk) {
+#if NDFL_BITBUF
+    if (pos + 48 < stop) {
+        Bb b;
+        bb_init(b, v, pos);
+        do {
+            tok_bb(b, v, t, ed, tk);
+            if (tk.kind > K_LEN) { pos = b.pos; return true; }
+            cnt += tk.n;
+        } while (b.pos + 48 < stop);
+        pos = b.pos;
+    }
+#else
     while (pos + 48 < stop) {
         tok<false>(v, pos, t, ed, stop, nb, tk);
         if (tk.kind > K_LEN) return true;
         cnt += tk.n;
     }
+#endif
     while (pos < stop) {
         tok<true>(v, pos, t, ed, stop, nb, tk);
         if (tk.kind > K_LEN) return true;
@@ -1624,10 +1710,25 @@ ndfl_inflate_emit_wave_kernel(const uint32_t* w, uint64_t nwords, uint64_t nbits
             uint32_t lastb = 0;             // the last output byte, when it is final (lastok)
             bool lastok = false;
             bool active = live;
+#if NDFL_BITBUF
+            Bb bb;
+            bool fast = active && pos + 48 < end;     // (pos only grows: once false, it stays false)
+            if (fast) bb_init(bb, v, pos);
+#endif
             while (active && pos < end) {
                 Tok tk;
+#if NDFL_BITBUF
+                if (fast) {
+                    tok_bb(bb, v, S.t, ed, tk);
+                    pos = bb.pos;
+                    fast = pos + 48 < end;
+                } else {
+                    tok<true>(v, pos, S.t, ed, end, nb, tk);
+                }
+#else
                 if (pos + 48 < end) tok<false>(v, pos, S.t, ed, end, nb, tk);
                 else tok<true>(v, pos, S.t, ed, end, nb, tk);
+#endif
                 if (tk.kind == K_LIT) {
                     wr_lit(wr, gout, tk.val, tk.n);
                     n += tk.n;
