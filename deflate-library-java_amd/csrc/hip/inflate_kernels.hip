@@ -85,6 +85,9 @@ constexpr uint32_t FIND_WPT = NDFL_FIND_WPT;     // finder: input words per thre
 #define NDFL_STRICT_REFILL 32     // strict stage: refill a wave once this many lanes are idle
 #endif
 constexpr uint32_t STRICT_SLICE = NDFL_STRICT_SLICE;  // strict stage: survivors per ticket
+#ifndef NDFL_COUNT_W_DEFAULT
+#define NDFL_COUNT_W_DEFAULT 1
+#endif
 constexpr uint32_t COUNT_WAVES = 256 * 16;       // count / emit passes: persistent waves at most (the
 constexpr uint32_t EMIT_WAVES = 256 * 16;        // grids are sized by occupancy, wave_grid below)
 
@@ -996,6 +999,7 @@ struct SegMeta {
     uint32_t ft, kind_ft, reason_ft, next;
     uint64_t end_ft, exit63;
     uint32_t pw, pad;     // the round's words per lane segment (staging geometry)
+    uint64_t rs;          // staging origin: the record's lane 0 segment start (absolute bit)
 };
 struct SegPool {
     uint64_t* start;      // [nrec][64]
@@ -1015,6 +1019,7 @@ struct SegPool {
 constexpr uint32_t BT_BYTES = 6720;   // wv::Tabs (6656) + hdr bit, data bit (u64 each), bfinal, btype, ed, pad
 
 #include "inflate_wave.hpp"
+#include "inflate_wg.hpp"
 
 // ---- host orchestration ---------------------------------------------------------------------
 
@@ -1083,6 +1088,40 @@ static uint32_t wave_grid(K kernel, uint32_t cap, const char* env = nullptr) {
         return cap;
     if (env && getenv(env)) per = std::max(1, atoi(getenv(env)));     // waves per CU override (tuning)
     return std::min<uint32_t>(cap, (uint32_t)(ncu * per));
+}
+
+// The count pass: one wave per chain (W = 1) or W waves per chain (workgroup rounds,
+// inflate_wg.hpp); NDFL_COUNT_W selects W (1, 2, 4, 8).  Persistent grid sized by occupancy; the
+// phase-fallback slots (d_ph) cover COUNT_WAVES waves.
+static uint32_t count_w() {                    // (read per decode: the tests switch it)
+    const char* e = getenv("NDFL_COUNT_W");
+    const uint32_t v = e ? (uint32_t)atoi(e) : (uint32_t)NDFL_COUNT_W_DEFAULT;
+    return (v == 2 || v == 4 || v == 8) ? v : 1u;
+}
+template <typename K>
+static uint32_t wg_grid(K kernel, uint32_t threads, uint32_t cap) {
+    int dev = 0, ncu = 0, per = 0;
+    if (hipGetDevice(&dev) != hipSuccess || hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess ||
+        hipOccupancyMaxActiveBlocksPerMultiprocessor(&per, kernel, (int)threads, 0) != hipSuccess || ncu <= 0 || per <= 0)
+        return cap;
+    return std::min<uint32_t>(cap, (uint32_t)(ncu * per));
+}
+template <typename... A>
+static void launch_count(hipStream_t s, uint32_t nchains, A... args) {
+    const uint32_t W = count_w();
+    if (W == 1) {
+        static const uint32_t g1 = wave_grid(ndfl_inflate_count_wave_kernel, inf::COUNT_WAVES, "NDFL_COUNT_WPC");
+        hipLaunchKernelGGL(ndfl_inflate_count_wave_kernel, dim3(std::min(nchains, g1)), dim3(64), 0, s, args...);
+    } else if (W == 2) {
+        static const uint32_t g = wg_grid(ndfl_inflate_count_wg_kernel<2>, 128, inf::COUNT_WAVES / 2);
+        hipLaunchKernelGGL(ndfl_inflate_count_wg_kernel<2>, dim3(std::min(nchains, g)), dim3(128), 0, s, args...);
+    } else if (W == 4) {
+        static const uint32_t g = wg_grid(ndfl_inflate_count_wg_kernel<4>, 256, inf::COUNT_WAVES / 4);
+        hipLaunchKernelGGL(ndfl_inflate_count_wg_kernel<4>, dim3(std::min(nchains, g)), dim3(256), 0, s, args...);
+    } else {
+        static const uint32_t g = wg_grid(ndfl_inflate_count_wg_kernel<8>, 512, inf::COUNT_WAVES / 8);
+        hipLaunchKernelGGL(ndfl_inflate_count_wg_kernel<8>, dim3(std::min(nchains, g)), dim3(512), 0, s, args...);
+    }
 }
 
 static hipError_t inf_ensure(void** p, size_t* cap, size_t n) {
@@ -1273,8 +1312,7 @@ static int inflate_devlink(InflateScratch& S, hipStream_t s, const uint32_t* d_w
                            (const uint64_t*)S.d_cands, ncand, (wv::HdrRec*)S.d_hrec);
         INF_CHK(hipGetLastError());
     }
-    static const uint32_t count_grid = wave_grid(ndfl_inflate_count_wave_kernel, COUNT_WAVES, "NDFL_COUNT_WPC");
-    hipLaunchKernelGGL(ndfl_inflate_count_wave_kernel, dim3(std::min<uint32_t>(ncand, count_grid)), dim3(64), 0, s,
+    launch_count(s, ncand,
                        d_w, nwords, nbits, (const uint64_t*)S.d_cands, (const uint64_t*)nullptr, ncand,
                        (const uint64_t*)S.d_cands, ncand, limit, (ChainRes*)S.d_res,
                        stats_on ? (uint32_t*)S.d_stats : nullptr, (uint64_t)0, S.pool, (uint32_t*)S.d_cticket,
@@ -1614,8 +1652,7 @@ static int inflate_run(InflateScratch& S, hipStream_t s, const uint8_t* in, uint
         if (!S.d_cticket) INF_CHK(hipMalloc(&S.d_cticket, 64));
         INF_CHK(hipMemsetAsync(S.d_cticket, 0, 4, s));
         if (S.count_first) INF_CHK(hipEventRecord(S.ev[2], s));
-        static const uint32_t count_grid = wave_grid(ndfl_inflate_count_wave_kernel, COUNT_WAVES, "NDFL_COUNT_WPC");
-        hipLaunchKernelGGL(ndfl_inflate_count_wave_kernel, dim3((uint32_t)std::min<size_t>(n, count_grid)), dim3(64), 0, s,
+        launch_count(s, (uint32_t)n,
                            d_w, nwords, nbits,
                            (const uint64_t*)S.d_starts, (const uint64_t*)S.d_stops, (uint32_t)n,
                            (const uint64_t*)S.d_cands, ncand, limit, (ChainRes*)S.d_res, stats_on ? (uint32_t*)S.d_stats : nullptr,

@@ -478,10 +478,23 @@ struct HdrRec {
     uint64_t at;                             // the candidate's bit position
 };
 
+// Synchronisation of the table build: the whole workgroup (WS = false: the one-wave kernels), or
+// one wave of a multi-wave workgroup building the tables alone (WS = true: its own LDS accesses in
+// order, no workgroup barrier, which the other waves do not reach).
+__device__ __forceinline__ void wsync() {
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    __builtin_amdgcn_wave_barrier();
+}
+template <bool WS>
+__device__ __forceinline__ void bsync() {
+    if (WS) wsync(); else __syncthreads();
+}
+
 // Canonical code from S.lens[base .. base+n) into the primary table `prim` (pbits) and the
 // extension area `x` (cap words): second-level tables for the codes longer than the primary when
 // they fit, else the canonical slow-path arrays (wave).  Returns the tree check result of
 // codeLengthsToCodeTree (D/decomp/Open.java:705-756) (uniform).
+template <bool WS = false>
 __device__ int build_code(Shared& S, uint32_t base, uint32_t n, uint32_t* prim, uint32_t pbits, uint32_t* x,
                           uint32_t cap, bool is_lit, int lane) {
     for (uint32_t k = (uint32_t)lane; k < (1u << pbits); k += 64) prim[k] = 0;
@@ -517,7 +530,7 @@ __device__ int build_code(Shared& S, uint32_t base, uint32_t n, uint32_t* prim, 
             fst[l] = code; off[l] = o; o += c[l];
         }
     }
-    __syncthreads();                            // prim zeroed
+    bsync<WS>();                            // prim zeroed
     // the longest code under each primary prefix of the long codes (a canonical code's prefix set
     // is prefix-free with the short codes, so these entries are free)
 #pragma unroll
@@ -529,7 +542,7 @@ __device__ int build_code(Shared& S, uint32_t base, uint32_t n, uint32_t* prim, 
         for (int L = 1; L < 16; L++) if (l == (uint32_t)L) f = fst[L];
         atomicMax(&prim[rev_bits((f + rank[q]) >> (l - pbits), pbits)], l);
     }
-    __syncthreads();
+    bsync<WS>();
     // second-level table offsets: exclusive scan of 2^(longest - pbits) over the primary entries
     const uint32_t per = (1u << pbits) / 64;
     uint32_t loc = 0;
@@ -565,7 +578,7 @@ __device__ int build_code(Shared& S, uint32_t base, uint32_t n, uint32_t* prim, 
         for (int L = 1; L < 16; L++) if (lane == L) ll = fst[L] + c[L];
         x[n + lane] = lane ? (ll << (15 - lane)) : 0u;
     }
-    __syncthreads();
+    bsync<WS>();
 #pragma unroll
     for (int q = 0; q < 5; q++) {
         const uint32_t l = mylen[q];
@@ -585,7 +598,7 @@ __device__ int build_code(Shared& S, uint32_t base, uint32_t n, uint32_t* prim, 
         }
         if (!two) x[o + rank[q]] = ent;
     }
-    __syncthreads();
+    bsync<WS>();
     return 0;
 }
 
@@ -593,6 +606,7 @@ __device__ int build_code(Shared& S, uint32_t base, uint32_t n, uint32_t* prim, 
 // 1 << 31 | adv | l1 << 4 | pair << 8 | b1 << 9 | b2 << 17, with pair set when the next LB - l1 bits
 // start with a second literal code (its length l2 <= LB - l1) and adv = l1 + l2 for a pair, l1
 // otherwise -- an unchecked step adds adv with no select.
+template <bool WS = false>
 __device__ void group_lits(Tabs& t, int lane) {
     uint32_t nv[(1u << LB) / 64];
 #pragma unroll
@@ -611,10 +625,10 @@ __device__ void group_lits(Tabs& t, int lane) {
         }
         nv[q] = v;
     }
-    __syncthreads();
+    bsync<WS>();
 #pragma unroll
     for (uint32_t q = 0; q < (1u << LB) / 64; q++) t.lit[q * 64 + (uint32_t)lane] = nv[q];
-    __syncthreads();
+    bsync<WS>();
 }
 
 // Fixed code lengths (D/decomp/Open.java:812-830) into S.lens.
@@ -628,28 +642,29 @@ __device__ void fixed_lens(Shared& S, int lane) {
 }
 
 // Tables for the block whose header S.h_* describes.  Returns a Reason (uniform) or 0.
+template <bool WS = false>
 __device__ int build_tables(Shared& S, int lane, bool& empty_dist) {
     empty_dist = false;
     if (S.h_btype == 1) {
         fixed_lens(S, lane);
-        __syncthreads();
-        build_code(S, 0, 288, S.t.lit, LB, S.t.lx, LX, true, lane);
-        build_code(S, 288, 32, S.t.dst, DB, S.t.dx, DX, false, lane);
+        bsync<WS>();
+        build_code<WS>(S, 0, 288, S.t.lit, LB, S.t.lx, LX, true, lane);
+        build_code<WS>(S, 288, 32, S.t.dst, DB, S.t.dx, DX, false, lane);
         return 0;
     }
     const uint32_t numDist = S.h_numdist;
-    int e = build_code(S, 0, 288, S.t.lit, LB, S.t.lx, LX, true, lane);
+    int e = build_code<WS>(S, 0, 288, S.t.lit, LB, S.t.lx, LX, true, lane);
     if (e) return e;
-    group_lits(S.t, lane);
+    group_lits<WS>(S.t, lane);
     // distance code: empty (one zero length) or one used code padded at index 31 (:398-425)
     const uint32_t dl = (lane < 32) ? S.lens[288 + lane] : 0u;
     empty_dist = numDist == 1 && S.lens[288] == 0;
     if (empty_dist) return 0;
     const uint32_t ones = (uint32_t)__popcll(__ballot(dl == 1)), other = (uint32_t)__popcll(__ballot(dl > 1));
-    __syncthreads();
+    bsync<WS>();
     if (ones == 1 && other == 0 && lane == 0) S.lens[288 + 31] = 1;
-    __syncthreads();
-    return build_code(S, 288, 32, S.t.dst, DB, S.t.dx, DX, false, lane);
+    bsync<WS>();
+    return build_code<WS>(S, 288, 32, S.t.dst, DB, S.t.dx, DX, false, lane);
 }
 
 // ---- segmented speculative decode of one round ------------------------------------------------
@@ -1516,7 +1531,7 @@ ndfl_inflate_count_wave_kernel(const uint32_t* w, uint64_t nwords, uint64_t nbit
                     if (lane == 0) {
                         SegMeta m;
                         m.ft = ft; m.kind_ft = fk; m.reason_ft = fr; m.next = NOREC;
-                        m.end_ft = fe; m.exit63 = fe; m.pw = g.pw; m.pad = brec;
+                        m.end_ft = fe; m.exit63 = fe; m.pw = g.pw; m.pad = brec; m.rs = g.base + g.r0;
                         pool.meta[idx] = m;
                         if (prev_rec == NOREC) pool.head[slot_base + c] = idx;
                         else pool.meta[prev_rec].next = idx;
@@ -1684,7 +1699,7 @@ ndfl_inflate_emit_wave_kernel(const uint32_t* w, uint64_t nwords, uint64_t nbits
                 r.end = lane < 63 ? nx : m.exit63;
                 r.kind = T_EXIT; r.reason = 0;
                 if ((uint32_t)lane == ft) { r.end = m.end_ft; r.kind = m.kind_ft; r.reason = m.reason_ft; }
-                g = make_geo(in, rs, rs + 1, m.pw);
+                g = make_geo(in, m.rs, m.rs + 1, m.pw);      // the count pass's staging geometry
                 stage_round(in, g, stg, lane);
             } else {
                 uint64_t E = min(next_cand(cands, ncand, rs, ch.end_bit), rs + MAX_SPAN);
