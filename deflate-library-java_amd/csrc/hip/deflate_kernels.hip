@@ -112,6 +112,7 @@ struct Args {
     uint32_t* hist_out;       // [nchunks][HREC] histograms: literal/length [0,288), distance [288,320)
     const uint32_t* codes;    // [nchunks][CREC] code records
     const uint64_t* chunk_off;// [nchunks] global bit offset of each chunk
+    uint32_t c0;              // split passes: first chunk of this launch (slab pipeline), grid = chunks
     uint32_t pf_dist;         // split passes: touch chunk c + pf_dist (the next wave of resident
                               // workgroups on this XCD) into L2 while chunk c is processed; 0: off
 };
@@ -551,7 +552,7 @@ __device__ __forceinline__ void deflate_chunk(const Args& a, uint32_t* obuf, PS&
     if (MODE == MODE_FUSED) {
         if (tid == 0) ps.chunk = atomicAdd(a.ticket, 1u);
     } else {
-        if (tid == 0) ps.chunk = blockIdx.x;
+        if (tid == 0) ps.chunk = a.c0 + blockIdx.x;
     }
     if (MODE == MODE_FUSED) {
         if (tid < 288) hlit[tid] = 0;

@@ -214,7 +214,7 @@ __device__ __forceinline__ uint32_t dist_extra(uint32_t d) { return d >= 4 ? (d 
 extern "C" __global__ void __launch_bounds__(64)
 ndfl_deflate_codes_kernel(Args a) {
     __shared__ __attribute__((aligned(16))) WScr S;
-    const uint32_t c = blockIdx.x;
+    const uint32_t c = a.c0 + blockIdx.x;
     const int lane = threadIdx.x;
     const uint64_t cs = (uint64_t)c * a.chunk_len;
     const uint32_t len_c = (uint32_t)min((uint64_t)a.chunk_len, a.n - cs);
@@ -383,11 +383,16 @@ ndfl_deflate_codes_kernel(Args a) {
     }
 }
 
-// Pass 3: chunk c's global bit offset = base_bit + sum of the sizes before it; total[0] = end bit.
-// One workgroup; thread t scans a contiguous range of chunks.
+// Pass 3: chunk c's global bit offset = base + sum of the sizes before it; total[0] = end bit.
+// One workgroup; thread t scans a contiguous range of chunks.  base = *base_ptr when base_ptr is set
+// (the slab pipeline: a slab's chunks start at the end bit of the slab before it, which that slab's
+// offsets launch wrote on the device; base_ptr may equal total).
 extern "C" __global__ void __launch_bounds__(1024)
-ndfl_deflate_offsets_kernel(const uint64_t* sizes, uint32_t n, uint64_t base, uint64_t* off, uint64_t* total) {
+ndfl_deflate_offsets_kernel(const uint64_t* sizes, uint32_t n, uint64_t base, uint64_t* off, uint64_t* total,
+                            const uint64_t* base_ptr) {
     __shared__ uint64_t sh[16];
+    if (base_ptr) base = *base_ptr;
+    __syncthreads();                        // (every thread has read *base_ptr before thread 0 writes total)
     const uint32_t per = (n + 1023) / 1024;
     const uint32_t b0 = min(n, threadIdx.x * per), b1 = min(n, b0 + per);
     uint64_t sum = 0;
