@@ -497,13 +497,29 @@ int ndfl_deflate_chunks_lz77(ndfl_ctx* c, const uint8_t* hist, uint32_t hist_len
     ea.out = d_out; ea.status = c->d_status.as<uint64_t>(); ea.ticket = c->d_ticket.as<uint32_t>();
     ea.edge_w = c->d_edge_w.as<uint64_t>(); ea.edge_v = c->d_edge_v.as<uint32_t>();
     ea.chunk_bits = c->cb_out;
+    ea.match_rw = c->d_match.as<uint32_t>();
+    ea.g.buf = buf; ea.g.total = total; ea.g.vstart = la.vstart; ea.g.chunk_len = chunk_len;
+    ea.g.parent_len = la.parent_len; ea.g.hist_limit = hist_limit; ea.g.min_run = la.min_run;
+    ea.g.max_run = la.max_run; ea.g.min_dist = la.min_dist; ea.g.max_dist = la.max_dist;
+    // match search: at the positions the greedy parse visits (default), or at every position by hash
+    // chains (NDFL_LZ_SEARCH=chain, the round-3 search); NDFL_LZ_LEAD=0 drops the tiles' lead-in (so
+    // the encode kernel's fallback search runs at most tile starts: a test of that path)
+    const char* se = getenv("NDFL_LZ_SEARCH");                 // read per call (tests switch them)
+    const bool chain_search = se && !strcmp(se, "chain");
+    const char* le = getenv("NDFL_LZ_LEAD");
+    const uint32_t lead_on = (le && atoi(le) == 0) ? 0u : 1u;
 
     HIPCHK(hipEventRecord(c->ev0, s));
     for (uint32_t cb = 0; cb < nch; cb += batch_ch) {
         const uint32_t ce = std::min(nch, cb + batch_ch);
         const uint64_t x0 = (uint64_t)cb * chunk_len, x1 = std::min<uint64_t>((uint64_t)ce * chunk_len, len);
         const uint64_t P0 = LZ_DS + x0, P1 = LZ_DS + x1;
-        if (P1 > P0) {
+        if (P1 > P0 && !chain_search) {
+            la.L0 = P0; la.p_begin = P0; la.p_end = P1;
+            hipLaunchKernelGGL(ndfl_lz_parse_match_kernel, dim3((uint32_t)((P1 - P0 + LZP_TILE - 1) / LZP_TILE)), dim3(1024),
+                               0, s, la, lead_on);
+            HIPCHK(hipGetLastError());
+        } else if (P1 > P0) {
             const uint64_t L0 = std::max<uint64_t>(la.vstart, P0 - LZ_SEG);
             hipLaunchKernelGGL(ndfl_lz_links_kernel, dim3((uint32_t)((P1 - L0 + LZ_SEG - 1) / LZ_SEG)), dim3(1024), 0, s,
                                (const uint8_t*)buf, total, la.vstart, L0, P1, c->d_link.as<uint16_t>());
@@ -523,9 +539,14 @@ int ndfl_deflate_chunks_lz77(ndfl_ctx* c, const uint8_t* hist, uint32_t hist_len
         HIPCHK(hipMemcpyAsync(st, la.stats, 32, hipMemcpyDeviceToHost, s));
         HIPCHK(hipStreamSynchronize(s));
         hipFree(la.stats);
-        fprintf(stderr, "[ndfl] lz match: %llu searched positions, %.2f hops/pos, %.2f trigram hits/pos, %.2f compare words/pos\n",
-                st[0], (double)st[1] / std::max(1ull, st[0]), (double)st[2] / std::max(1ull, st[0]),
-                (double)st[3] / std::max(1ull, st[0]));
+        if (chain_search)
+            fprintf(stderr, "[ndfl] lz match: %llu searched positions, %.2f hops/pos, %.2f trigram hits/pos, %.2f compare words/pos\n",
+                    st[0], (double)st[1] / std::max(1ull, st[0]), (double)st[2] / std::max(1ull, st[0]),
+                    (double)st[3] / std::max(1ull, st[0]));
+        else
+            fprintf(stderr, "[ndfl] lz parse-driven match: %llu searches for %llu positions (%.2f %%), %.2f bucket entries per search\n",
+                    st[0], (unsigned long long)len, 100.0 * (double)st[0] / std::max<double>(1.0, (double)len),
+                    (double)st[1] / std::max(1ull, st[0]));
     }
     const uint32_t ne = 2 * nch;
     hipLaunchKernelGGL(ndfl_edge_fixup_kernel, dim3((ne + 255) / 256), dim3(256), 0, s,

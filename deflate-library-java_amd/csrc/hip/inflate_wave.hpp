@@ -804,6 +804,11 @@ __device__ void round_decode(const In& in, const Tabs& t, bool ed, uint64_t rs, 
     Spec p0;
     spec_run(v, t, ed, nb, s, s, C1, C2, e, p0);
     S.exit_[lane] = p0.end;
+    // lanes up to the first whose speculative run ended the block: the lanes past the end of a block
+    // decode the next block's bits with this block's tables (a round spans past the block end when
+    // no header candidate marks it) and never synchronise, which must not count as a phase-locked code
+    const uint64_t tsp = __ballot(p0.kind != T_EXIT);
+    const uint64_t inblk = tsp ? (2ull << __builtin_ctzll(tsp)) - 1ull : ~0ull;
     __syncthreads();
     if (pc) { const uint64_t x = wall_clock64(); pc->spec += x - tk0; tk0 = x; }
     SegR r;
@@ -825,8 +830,9 @@ __device__ void round_decode(const In& in, const Tabs& t, bool ed, uint64_t rs, 
     } else {
         // lane j0 started right (its predecessor is exact) but did not meet its own speculation:
         // its verify run already decoded the segment.  Lanes after it resolve in order.
-        nslow += (uint32_t)__popcll(um);
-        uint32_t nph = __popcll(um) > NDFL_PH_FALLBACK ? NPH : 1u;
+        const uint32_t nun = (uint32_t)__popcll(um & inblk);
+        nslow += nun;
+        uint32_t nph = nun > NDFL_PH_FALLBACK ? NPH : 1u;
         // the lanes after `from` decode their segments from the phases s+1 .. s+7 as well
         auto phase_runs = [&](uint32_t from) {
             if ((uint32_t)lane > from) {

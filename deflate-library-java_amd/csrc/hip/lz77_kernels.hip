@@ -225,6 +225,249 @@ ndfl_lz_match_kernel(LzArgs a) {
     }
 }
 
+// ---- 2'. best match at the positions the greedy parse visits ---------------------------------
+// The greedy parse (D/comp/Lz77Huffman.java:68-130) reads the best match only at the positions it
+// visits -- about a fifth of the positions on text, and mostly word starts, whose candidate lists are
+// short: on the config-3 text the visited positions hold 7 % of the candidates that a search at every
+// position walks (tests/lz_parse_stats.c).  So each wave follows the parse through its own 512
+// positions of a tile and searches only where the parse lands; a parse started anywhere merges with
+// the true one within a few tokens (a literal lands on every position, a match on its end), so
+// wave w's path from its segment start is the true path from the first position both visit on.
+// After all waves have run, wave w checks the true entry into its segment (wave w-1's exit, in
+// order): a position its own path visited means the rest of its path is exact; otherwise it follows
+// the true path from the entry until that meets its own (or leaves the segment).  The tile's first
+// wave starts LZP_LEAD positions before the tile (unless the tile starts a chunk, where the parse
+// starts exactly), so its path has merged with the true one by the tile start -- or, rarely, not: a
+// true-path position never searched keeps the sentinel LZP_NONE and the encode kernel searches it
+// (lz_match_global).
+//
+// The search at one position is wave-cooperative: the window's positions are counting-sorted by a
+// 13-bit hash of their first three bytes once per tile, and the 64 lanes test the position's whole
+// bucket, 64 candidates per step -- a candidate whose run reaches minRun (>= 3) shares the three
+// bytes -- keeping the longest run and, among equal runs, the nearest candidate (the reference
+// scans distances upwards and keeps strictly longer runs, :71-84).  A long bucket first tests the
+// 64 nearest distances: a run reaching the cap there ends the search (nothing farther can win).
+namespace {
+constexpr int LZP_TILE = 8192;                     // positions written per tile
+constexpr int LZP_SEG = 512;                       // positions per wave (16 waves)
+constexpr int LZP_LEAD = 64;                       // lead-in of the first wave (tiles inside a chunk)
+constexpr int LZP_HBITS = 13;
+constexpr int LZP_NPOS = LZP_LEAD + LZ_WIN + LZP_TILE;          // window positions (sorted)
+constexpr int LZP_WWORDS = (LZP_NPOS + 272) / 4;                // window bytes as words (+ lookahead)
+constexpr uint32_t LZP_NONE = 0xFFFFFFFFu;         // sentinel: position not searched
+constexpr int LZP_NEAR = 128;                      // buckets longer than this test the nearest distances first
+
+__device__ __forceinline__ uint32_t lzp_hash(uint32_t k) { return (k * 2654435761u) >> (32 - LZP_HBITS); }
+
+struct LzpS {
+    uint32_t wb[LZP_WWORDS + 4];                   // window bytes [wb0, wb0 + 4 * LZP_WWORDS)
+    uint16_t sorted[LZP_NPOS];                     // window offsets, grouped by hash bucket
+    uint32_t bend[1 << LZP_HBITS];                 // counts -> starts -> bucket ends (after the scatter)
+    uint32_t vis[LZP_TILE / 32];                   // positions the waves' paths searched (tile-relative)
+    uint32_t xit[16];                              // each wave's exit (tile-relative, may pass the tile)
+    uint32_t scan[16];
+};
+
+// Wave-cooperative exact search at buffer position q (window-relative rq).  All lanes call with the
+// same q; returns the match word (run << 16 | dist - 1, or the literal byte).
+__device__ __forceinline__ uint32_t lzp_search(const LzArgs& a, const LzpS& S, int64_t wb0, uint64_t q, uint64_t cs0,
+                                               uint64_t pps0, uint32_t* st) {
+    const int lane = threadIdx.x & 63;
+    const uint32_t rq = (uint32_t)((int64_t)q - wb0);
+    const uint64_t cs = cs0 + (uint64_t)(((uint32_t)(q - cs0) / a.chunk_len) * a.chunk_len);
+    const uint64_t e = min(cs + a.chunk_len, a.total);
+    const uint32_t maxlen = (uint32_t)min((uint64_t)a.max_run, e - q);
+    const uint64_t ps = pps0 + (uint64_t)(((uint32_t)(q - pps0) / a.parent_len) * a.parent_len);
+    const uint64_t off = ps - min((uint64_t)a.hist_limit, ps - a.vstart);
+    const int64_t lo = max((int64_t)q - (int64_t)a.max_dist, (int64_t)off);
+    const int64_t hi = (int64_t)q - (int64_t)a.min_dist;
+    const uint32_t lit = lz_byte(S.wb, rq);
+    if (maxlen < a.min_run || hi < lo) return lit;
+    const uint32_t wq = lz_word(S.wb, rq);
+    const uint32_t rlo = (uint32_t)(lo - wb0), rhi = (uint32_t)(hi - wb0);
+    // run of candidate r (window-relative, in [rlo, rhi]) against q, capped at maxlen; 0 when the
+    // first three bytes differ
+    auto run_of = [&](uint32_t r) -> uint32_t {
+        const uint32_t x0 = lz_word(S.wb, r) ^ wq;
+        if (x0 & 0xFFFFFFu) return 0u;
+        if (x0) return min(3u, maxlen);
+        uint32_t k = 4;
+        for (;;) {
+            if (k >= maxlen) return maxlen;
+            const uint32_t y = lz_word(S.wb, r + k) ^ lz_word(S.wb, rq + k);
+            if (y) return min(k + (__builtin_ctz(y) >> 3), maxlen);
+            k += 4;
+        }
+    };
+    const uint32_t h = lzp_hash(wq & 0xFFFFFFu);
+    const uint32_t B0 = h ? S.bend[h - 1] : 0u, B1 = S.bend[h];
+    uint32_t best = 0;                                  // run << 16 | r (larger r: nearer)
+    if (B1 - B0 > (uint32_t)LZP_NEAR) {
+        // the 64 nearest distances: a run reaching the cap among them is the answer
+        const uint32_t r = rhi - (uint32_t)lane;
+        uint32_t k = 0;
+        if ((int64_t)rhi - lane >= (int64_t)rlo) { const uint32_t run = run_of(r); if (run) k = run << 16 | r; }
+#pragma unroll
+        for (int o = 32; o > 0; o >>= 1) k = max(k, (uint32_t)__shfl_xor((int)k, o, 64));
+        if ((k >> 16) >= maxlen) best = k;
+        st[1] += 64u;
+    }
+    if ((best >> 16) < maxlen) {
+        for (uint32_t i = B0; i < B1; i += 64) {
+            uint32_t k = 0;
+            if (i + lane < B1) {
+                const uint32_t r = S.sorted[i + lane];
+                if (r >= rlo && r <= rhi) { const uint32_t run = run_of(r); if (run) k = run << 16 | r; }
+            }
+            best = max(best, k);
+        }
+#pragma unroll
+        for (int o = 32; o > 0; o >>= 1) best = max(best, (uint32_t)__shfl_xor((int)best, o, 64));
+        st[1] += B1 - B0;
+    }
+    st[0]++;
+    const uint32_t run = best >> 16;
+    return run >= a.min_run ? (run << 16 | (rq - (best & 0xFFFFu) - 1)) : lit;
+}
+}  // namespace
+
+extern "C" __global__ void __launch_bounds__(1024)
+ndfl_lz_parse_match_kernel(LzArgs a, uint32_t lead_on) {
+    __shared__ __attribute__((aligned(16))) LzpS S;
+    const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
+    const uint64_t p0 = a.p_begin + (uint64_t)blockIdx.x * LZP_TILE;
+    const uint64_t p1 = min(p0 + LZP_TILE, a.p_end);
+    const uint32_t ntile = (uint32_t)(p1 - p0);
+    const int64_t wb0 = (int64_t)p0 - LZP_LEAD - LZ_WIN;
+    uint32_t st[2] = {0u, 0u};                         // (NDFL_LZ_STATS: searches, bucket entries scanned)
+    // positions never searched read as the sentinel (the searched ones are stored over it below)
+    for (uint32_t k = (uint32_t)tid; k < ntile; k += 1024) a.match[p0 + k - a.p_begin] = LZP_NONE;
+    for (int k = tid; k < LZP_WWORDS + 4; k += 1024) {
+        const int64_t g = wb0 + 4 * (int64_t)k;
+        uint32_t v = 0;
+        if (g >= 0 && g + 4 <= (int64_t)a.total) v = *(const uint32_t*)(a.buf + g);
+        else for (int b = 0; b < 4; b++) if (g + b >= 0 && g + b < (int64_t)a.total) v |= (uint32_t)a.buf[g + b] << (8 * b);
+        S.wb[k] = v;
+    }
+    for (int k = tid; k < (1 << LZP_HBITS); k += 1024) S.bend[k] = 0;
+    for (int k = tid; k < LZP_TILE / 32; k += 1024) S.vis[k] = 0;
+    __syncthreads();
+    // counting sort of the window's positions by hash (candidates: valid bytes, a full trigram)
+    const uint32_t nsort = (uint32_t)(p1 - (uint64_t)wb0);
+    const int64_t gmin = max((int64_t)a.vstart, wb0);
+    for (uint32_t r = (uint32_t)tid; r < nsort; r += 1024) {
+        const int64_t g = wb0 + r;
+        if (g >= gmin && g + 2 < (int64_t)a.total) atomicAdd(&S.bend[lzp_hash(lz_word(S.wb, r) & 0xFFFFFFu)], 1u);
+    }
+    __syncthreads();
+    {
+        constexpr int PER = (1 << LZP_HBITS) / 1024;
+        uint32_t v[PER], sum = 0;
+#pragma unroll
+        for (int i = 0; i < PER; i++) { v[i] = S.bend[tid * PER + i]; sum += v[i]; }
+        uint32_t tot;
+        uint32_t run = block_excl_scan<uint32_t, 16>(sum, S.scan, tot);
+        __syncthreads();
+#pragma unroll
+        for (int i = 0; i < PER; i++) { S.bend[tid * PER + i] = run; run += v[i]; }
+    }
+    __syncthreads();
+    for (uint32_t r = (uint32_t)tid; r < nsort; r += 1024) {
+        const int64_t g = wb0 + r;
+        if (g >= gmin && g + 2 < (int64_t)a.total) {
+            const uint32_t at = atomicAdd(&S.bend[lzp_hash(lz_word(S.wb, r) & 0xFFFFFFu)], 1u);
+            S.sorted[at] = (uint16_t)r;
+        }
+    }
+    __syncthreads();
+    // chunk / parent chunk of the tile's lead-in start (positions step from them with 32-bit math)
+    const uint64_t q00 = p0 - LZP_LEAD >= a.p_begin ? p0 - LZP_LEAD : p0;
+    const uint64_t cs0 = LZ_DS + ((q00 - LZ_DS) / a.chunk_len) * a.chunk_len;
+    const uint64_t pps0 = LZ_DS + ((q00 - LZ_DS) / a.parent_len) * a.parent_len;
+    auto step_of = [&](uint32_t m) -> uint32_t { return (m >> 16) ? (m >> 16) : 1u; };
+    // the waves' paths
+    const uint64_t s_w = p0 + (uint64_t)w * LZP_SEG;
+    const uint64_t e_w = min(s_w + LZP_SEG, p1);
+    if (s_w < p1) {
+        const bool chunk_start = ((p0 - LZ_DS) % a.chunk_len) == 0;
+        uint64_t q = (w == 0 && lead_on && !chunk_start) ? q00 : s_w;
+        while (q < e_w) {
+            const uint32_t m = lzp_search(a, S, wb0, q, cs0, pps0, st);
+            if (q >= s_w) {
+                const uint32_t t = (uint32_t)(q - p0);
+                if (lane == 0) { a.match[q - a.p_begin] = m; atomicOr(&S.vis[t >> 5], 1u << (t & 31)); }
+            }
+            q += step_of(m);
+        }
+        if (lane == 0) S.xit[w] = (uint32_t)(q - p0);
+    }
+    __syncthreads();
+    // the true entry of each wave's segment, in order
+    const int nw = (int)((ntile + LZP_SEG - 1) / LZP_SEG);
+    for (int v = 1; v < nw; v++) {
+        if (w == v) {
+            const uint32_t ent = S.xit[v - 1];
+            const uint32_t sv = (uint32_t)v * LZP_SEG, ev = min(sv + (uint32_t)LZP_SEG, ntile);
+            uint32_t x = S.xit[v];
+            if (ent >= ev) x = ent;                     // the true path passes over this segment
+            else if (!((S.vis[ent >> 5] >> (ent & 31)) & 1u)) {
+                uint32_t t = ent;
+                while (t < ev && !((S.vis[t >> 5] >> (t & 31)) & 1u)) {
+                    const uint64_t q = p0 + t;
+                    const uint32_t m = lzp_search(a, S, wb0, q, cs0, pps0, st);
+                    if (lane == 0) { a.match[q - a.p_begin] = m; atomicOr(&S.vis[t >> 5], 1u << (t & 31)); }
+                    t += step_of(m);
+                }
+                if (t >= ev) x = t;                     // (else: met its own path, whose exit stands)
+            }
+            if (lane == 0) S.xit[v] = x;
+        }
+        __syncthreads();
+    }
+    if (a.stats && lane == 0) { atomicAdd(&a.stats[0], (unsigned long long)st[0]); atomicAdd(&a.stats[1], (unsigned long long)st[1]); }
+}
+
+// Exact search at one position from global memory (the encode kernel's rare fallback for a true-path
+// position the parse-driven search did not reach): every distance of the window, 64 per step, the
+// nearest first; a step whose best run reaches the cap ends the search.  Wave-uniform q.
+namespace {
+struct LzGlob {
+    const uint8_t* buf;
+    uint64_t total, vstart;
+    uint32_t chunk_len, parent_len, hist_limit, min_run, max_run, min_dist, max_dist;
+};
+__device__ uint32_t lz_match_global(const LzGlob& g, uint64_t q) {
+    const int lane = threadIdx.x & 63;
+    const uint64_t cs = LZ_DS + ((q - LZ_DS) / g.chunk_len) * g.chunk_len;
+    const uint64_t e = min(cs + g.chunk_len, g.total);
+    const uint32_t maxlen = (uint32_t)min((uint64_t)g.max_run, e - q);
+    const uint64_t ps = LZ_DS + ((q - LZ_DS) / g.parent_len) * g.parent_len;
+    const uint64_t off = ps - min((uint64_t)g.hist_limit, ps - g.vstart);
+    const int64_t lo = max((int64_t)q - (int64_t)g.max_dist, (int64_t)off);
+    const uint32_t lit = g.buf[q];
+    if (maxlen < g.min_run || (int64_t)q - (int64_t)g.min_dist < lo) return lit;
+    const uint32_t dmax = (uint32_t)((int64_t)q - lo);
+    uint32_t best = 0;                                  // run << 16 | (65535 - dist)
+    for (uint32_t d0 = g.min_dist; d0 <= dmax; d0 += 64) {
+        const uint32_t d = d0 + (uint32_t)lane;
+        uint32_t k = 0;
+        if (d <= dmax) {
+            const uint8_t* x = g.buf + (q - d);
+            const uint8_t* y = g.buf + q;
+            uint32_t run = 0;
+            while (run < maxlen && x[run] == y[run]) run++;
+            if (run) k = run << 16 | (65535u - d);
+        }
+#pragma unroll
+        for (int o = 32; o > 0; o >>= 1) k = max(k, (uint32_t)__shfl_xor((int)k, o, 64));
+        best = max(best, k);
+        if ((best >> 16) >= maxlen) break;
+    }
+    const uint32_t run = best >> 16;
+    return run >= g.min_run ? (run << 16 | ((65535u - (best & 0xFFFFu)) - 1)) : lit;
+}
+}  // namespace
+
 // ---- 3. parse + block encode ------------------------------------------------------------------
 namespace {
 struct LzEncArgs {
@@ -244,6 +487,8 @@ struct LzEncArgs {
     uint64_t* edge_w;
     uint32_t* edge_v;
     uint64_t* chunk_bits;     // optional [nchunks]: block bits
+    uint32_t* match_rw;       // = match: positions the parse reaches but the search skipped (LZP_NONE) are
+    LzGlob g;                 //   searched here from global memory (lz_match_global) and stored back
 };
 
 // Length symbol / extra of a run (D/comp/Lz77Huffman.java:92-111) and distance symbol / extra of
@@ -284,19 +529,29 @@ ndfl_lz_encode_kernel(LzEncArgs a) {
 
     // ---- parse: steps in LDS, one wave walks them (D/comp/Lz77Huffman.java:68-130) -----------
     for (uint32_t k = (uint32_t)tid; k < len_c; k += DT) {
-        const uint32_t m = mt[k] >> 16;
-        step[k] = (uint16_t)(m ? m : 1u);
+        const uint32_t mk = mt[k];
+        const uint32_t m = mk >> 16;
+        step[k] = (uint16_t)(mk == LZP_NONE ? 0u : m ? m : 1u);      // 0: not searched
     }
+    if (tid == 0) ps.P = 0;                                         // (repairs made; reset below)
     __syncthreads();
     if (wid == 0) {
-        uint32_t cur = 0;
+        uint32_t cur = 0, nrep = 0;
         while (cur < len_c) {
             const uint32_t s = cur + lane < len_c ? (uint32_t)step[cur + lane] : 64u;
             uint64_t mask = 0;
             uint32_t p = 0;
             while (p < 64 && cur + p < len_c) {
                 mask |= 1ull << p;
-                p += (uint32_t)__builtin_amdgcn_readlane((int)s, (int)p);
+                uint32_t sp = (uint32_t)__builtin_amdgcn_readlane((int)s, (int)p);
+                if (sp == 0) {
+                    // a position of the parse that the parse-driven search never reached
+                    const uint32_t m = lz_match_global(a.g, LZ_DS + cs + cur + p);
+                    if (lane == 0) a.match_rw[cs + cur + p - a.batch_x0] = m;
+                    sp = (m >> 16) ? (m >> 16) : 1u;
+                    nrep++;
+                }
+                p += sp;
             }
             // OR the 64-bit window mask into tokm at bit `cur` (3 words at most)
             const uint32_t sh = cur & 31, w0 = cur >> 5;
@@ -308,8 +563,10 @@ ndfl_lz_encode_kernel(LzEncArgs a) {
             }
             cur += p;
         }
+        if (nrep) { __threadfence(); if (lane == 0) ps.P = nrep; }
     }
     __syncthreads();
+    if (ps.P) __threadfence();                                      // the stored repairs, seen by every wave
 
     // ---- histograms --------------------------------------------------------------------------
     if (tid < 288) hlit[tid] = 0;
