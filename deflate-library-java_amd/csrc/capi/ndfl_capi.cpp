@@ -488,8 +488,8 @@ int ndfl_deflate_chunks_lz77(ndfl_ctx* c, const uint8_t* hist, uint32_t hist_len
     static const bool lz_stats = getenv("NDFL_LZ_STATS") != nullptr;
     la.stats = nullptr;
     if (lz_stats) {
-        HIPCHK(hipMalloc(&la.stats, 64));
-        HIPCHK(hipMemsetAsync(la.stats, 0, 64, s));
+        HIPCHK(hipMalloc(&la.stats, 128));
+        HIPCHK(hipMemsetAsync(la.stats, 0, 128, s));
     }
     LzEncArgs ea;
     ea.match = c->d_match.as<uint32_t>(); ea.n = len; ea.chunk_len = chunk_len; ea.nchunks = nch;
@@ -501,6 +501,7 @@ int ndfl_deflate_chunks_lz77(ndfl_ctx* c, const uint8_t* hist, uint32_t hist_len
     ea.g.buf = buf; ea.g.total = total; ea.g.vstart = la.vstart; ea.g.chunk_len = chunk_len;
     ea.g.parent_len = la.parent_len; ea.g.hist_limit = hist_limit; ea.g.min_run = la.min_run;
     ea.g.max_run = la.max_run; ea.g.min_dist = la.min_dist; ea.g.max_dist = la.max_dist;
+    ea.stats = la.stats;
     // match search: at the positions the greedy parse visits (default), or at every position by hash
     // chains (NDFL_LZ_SEARCH=chain, the round-3 search); NDFL_LZ_LEAD=0 drops the tiles' lead-in (so
     // the encode kernel's fallback search runs at most tile starts: a test of that path)
@@ -535,8 +536,8 @@ int ndfl_deflate_chunks_lz77(ndfl_ctx* c, const uint8_t* hist, uint32_t hist_len
     }
     HIPCHK(hipEventRecord(c->ev1, s));
     if (la.stats) {
-        unsigned long long st[4];
-        HIPCHK(hipMemcpyAsync(st, la.stats, 32, hipMemcpyDeviceToHost, s));
+        unsigned long long st[16];
+        HIPCHK(hipMemcpyAsync(st, la.stats, 128, hipMemcpyDeviceToHost, s));
         HIPCHK(hipStreamSynchronize(s));
         hipFree(la.stats);
         if (chain_search)
@@ -544,9 +545,20 @@ int ndfl_deflate_chunks_lz77(ndfl_ctx* c, const uint8_t* hist, uint32_t hist_len
                     st[0], (double)st[1] / std::max(1ull, st[0]), (double)st[2] / std::max(1ull, st[0]),
                     (double)st[3] / std::max(1ull, st[0]));
         else
-            fprintf(stderr, "[ndfl] lz parse-driven match: %llu searches for %llu positions (%.2f %%), %.2f bucket entries per search\n",
+            fprintf(stderr, "[ndfl] lz parse-driven match: %llu searches for %llu positions (%.2f %%), %.2f bucket entries per search, "
+                    "%llu fallback searches in the encode kernel\n",
                     st[0], (unsigned long long)len, 100.0 * (double)st[0] / std::max<double>(1.0, (double)len),
-                    (double)st[1] / std::max(1ull, st[0]));
+                    (double)st[1] / std::max(1ull, st[0]), st[2]);
+        if (!chain_search)
+            fprintf(stderr, "[ndfl] lz parse-driven tiles %llu: stage+sort %.1f us, paths %.1f us, entries %.1f us per tile\n",
+                    st[6], st[3] / 100.0 / std::max(1ull, st[6]), st[4] / 100.0 / std::max(1ull, st[6]),
+                    st[5] / 100.0 / std::max(1ull, st[6]));
+        {
+            const double k = 100.0 * (double)std::max(1ull, st[13]);
+            fprintf(stderr, "[ndfl] lz encode chunks %llu: fill+parse %.1f us (walks %.1f, true entries %.1f), histograms %.1f us, "
+                    "codes %.1f us, token bits %.1f us, look-back+store %.1f us per chunk\n", st[13], st[8] / k, st[14] / k,
+                    st[15] / k, st[9] / k, st[10] / k, st[11] / k, st[12] / k);
+        }
     }
     const uint32_t ne = 2 * nch;
     hipLaunchKernelGGL(ndfl_edge_fixup_kernel, dim3((ne + 255) / 256), dim3(256), 0, s,

@@ -250,7 +250,7 @@ ndfl_lz_match_kernel(LzArgs a) {
 namespace {
 constexpr int LZP_TILE = 8192;                     // positions written per tile
 constexpr int LZP_SEG = 512;                       // positions per wave (16 waves)
-constexpr int LZP_LEAD = 64;                       // lead-in of the first wave (tiles inside a chunk)
+constexpr int LZP_LEAD = 256;                      // lead-in of the first wave (tiles inside a chunk)
 constexpr int LZP_HBITS = 13;
 constexpr int LZP_NPOS = LZP_LEAD + LZ_WIN + LZP_TILE;          // window positions (sorted)
 constexpr int LZP_WWORDS = (LZP_NPOS + 272) / 4;                // window bytes as words (+ lookahead)
@@ -340,6 +340,7 @@ ndfl_lz_parse_match_kernel(LzArgs a, uint32_t lead_on) {
     const uint32_t ntile = (uint32_t)(p1 - p0);
     const int64_t wb0 = (int64_t)p0 - LZP_LEAD - LZ_WIN;
     uint32_t st[2] = {0u, 0u};                         // (NDFL_LZ_STATS: searches, bucket entries scanned)
+    const uint64_t tk0 = a.stats ? wall_clock64() : 0;
     // positions never searched read as the sentinel (the searched ones are stored over it below)
     for (uint32_t k = (uint32_t)tid; k < ntile; k += 1024) a.match[p0 + k - a.p_begin] = LZP_NONE;
     for (int k = tid; k < LZP_WWORDS + 4; k += 1024) {
@@ -380,6 +381,7 @@ ndfl_lz_parse_match_kernel(LzArgs a, uint32_t lead_on) {
         }
     }
     __syncthreads();
+    const uint64_t tk1 = a.stats ? wall_clock64() : 0;
     // chunk / parent chunk of the tile's lead-in start (positions step from them with 32-bit math)
     const uint64_t q00 = p0 - LZP_LEAD >= a.p_begin ? p0 - LZP_LEAD : p0;
     const uint64_t cs0 = LZ_DS + ((q00 - LZ_DS) / a.chunk_len) * a.chunk_len;
@@ -402,6 +404,7 @@ ndfl_lz_parse_match_kernel(LzArgs a, uint32_t lead_on) {
         if (lane == 0) S.xit[w] = (uint32_t)(q - p0);
     }
     __syncthreads();
+    const uint64_t tk2 = a.stats ? wall_clock64() : 0;
     // the true entry of each wave's segment, in order
     const int nw = (int)((ntile + LZP_SEG - 1) / LZP_SEG);
     for (int v = 1; v < nw; v++) {
@@ -425,6 +428,10 @@ ndfl_lz_parse_match_kernel(LzArgs a, uint32_t lead_on) {
         __syncthreads();
     }
     if (a.stats && lane == 0) { atomicAdd(&a.stats[0], (unsigned long long)st[0]); atomicAdd(&a.stats[1], (unsigned long long)st[1]); }
+    if (a.stats && tid == 0) {                         // tile phase times (wall clock, 100 MHz): stage + sort, paths, entries
+        atomicAdd(&a.stats[3], (unsigned long long)(tk1 - tk0)); atomicAdd(&a.stats[4], (unsigned long long)(tk2 - tk1));
+        atomicAdd(&a.stats[5], (unsigned long long)(wall_clock64() - tk2)); atomicAdd(&a.stats[6], 1ull);
+    }
 }
 
 // Exact search at one position from global memory (the encode kernel's rare fallback for a true-path
@@ -436,7 +443,7 @@ struct LzGlob {
     uint64_t total, vstart;
     uint32_t chunk_len, parent_len, hist_limit, min_run, max_run, min_dist, max_dist;
 };
-__device__ uint32_t lz_match_global(const LzGlob& g, uint64_t q) {
+__device__ __noinline__ uint32_t lz_match_global(const LzGlob& g, uint64_t q) {
     const int lane = threadIdx.x & 63;
     const uint64_t cs = LZ_DS + ((q - LZ_DS) / g.chunk_len) * g.chunk_len;
     const uint64_t e = min(cs + g.chunk_len, g.total);
@@ -489,6 +496,7 @@ struct LzEncArgs {
     uint64_t* chunk_bits;     // optional [nchunks]: block bits
     uint32_t* match_rw;       // = match: positions the parse reaches but the search skipped (LZP_NONE) are
     LzGlob g;                 //   searched here from global memory (lz_match_global) and stored back
+    unsigned long long* stats;// optional (NDFL_LZ_STATS): [2] fallback searches
 };
 
 // Length symbol / extra of a run (D/comp/Lz77Huffman.java:92-111) and distance symbol / extra of
@@ -508,6 +516,7 @@ ndfl_lz_encode_kernel(LzEncArgs a) {
     __shared__ __attribute__((aligned(16))) uint32_t big[32768];   // steps (u16) -> scratch -> bit buffer
     __shared__ uint32_t tokm[2048];                                 // token starts, 1 bit per position
     __shared__ Persist ps;
+    __shared__ uint32_t wexit[16];                                  // the parse walk's true exit per wave
     static_assert(OUTW <= 32768, "bit buffer must fit the step array");
     uint32_t* obuf = big;
     char* scr = (char*)big;
@@ -518,6 +527,7 @@ ndfl_lz_encode_kernel(LzEncArgs a) {
     const int tid = threadIdx.x;
     const int lane = tid & 63, wid = tid >> 6;
 
+    const uint64_t tq0 = a.stats ? wall_clock64() : 0;   // (NDFL_LZ_STATS: phase times of chunk workgroups)
     if (tid == 0) ps.chunk = a.chunk_base + atomicAdd(a.ticket, 1u);
     for (int k = tid; k < 2048; k += DT) tokm[k] = 0;
     __syncthreads();
@@ -528,30 +538,72 @@ ndfl_lz_encode_kernel(LzEncArgs a) {
     const uint32_t* mt = a.match + (cs - a.batch_x0);
 
     // ---- parse: steps in LDS, one wave walks them (D/comp/Lz77Huffman.java:68-130) -----------
-    for (uint32_t k = (uint32_t)tid; k < len_c; k += DT) {
-        const uint32_t mk = mt[k];
-        const uint32_t m = mk >> 16;
-        step[k] = (uint16_t)(mk == LZP_NONE ? 0u : m ? m : 1u);      // 0: not searched
+    // (1024: a position the match search did not reach).  16-byte loads, four in flight per thread
+    auto step_of = [](uint32_t mk) -> uint32_t { const uint32_t m = mk >> 16; return mk == LZP_NONE ? 1024u : m ? m : 1u; };
+    if ((((uintptr_t)mt) & 15) == 0) {
+        const uint32_t nq = len_c / 4;
+#pragma unroll 4
+        for (uint32_t k = (uint32_t)tid; k < nq; k += DT) {
+            const u32x4 v = *(const u32x4*)(mt + 4 * k);
+            *(uint2*)&step[4 * k] = make_uint2(step_of(v.x) | step_of(v.y) << 16, step_of(v.z) | step_of(v.w) << 16);
+        }
+        for (uint32_t k = 4 * nq + (uint32_t)tid; k < len_c; k += DT) step[k] = (uint16_t)step_of(mt[k]);
+    } else {
+#pragma unroll 4
+        for (uint32_t k = (uint32_t)tid; k < len_c; k += DT) step[k] = (uint16_t)step_of(mt[k]);
     }
-    if (tid == 0) ps.P = 0;                                         // (repairs made; reset below)
+    if (tid == 0) ps.P = 0;                                         // (repairs made)
     __syncthreads();
-    if (wid == 0) {
-        uint32_t cur = 0, nrep = 0;
-        while (cur < len_c) {
-            const uint32_t s = cur + lane < len_c ? (uint32_t)step[cur + lane] : 64u;
+    // The walk is split over the 16 waves: wave w walks its 1/16 of the chunk from the segment start
+    // (a multiple of 32 positions, so each wave owns whole words of tokm), as the match kernel's
+    // paths do; then, in order, wave w takes the true entry (wave w-1's true exit): its own walk
+    // visited it (the common case -- parses merge within a few tokens), or the wave re-walks from it
+    // one token at a time until it lands on its own walk.  Token bits its walk set before the entry or
+    // between true tokens are cleared.  A step of 1024 marks a position the match search skipped.
+    const uint64_t tqa = a.stats ? wall_clock64() : 0;
+    const uint32_t lenc = (uint32_t)__builtin_amdgcn_readfirstlane((int)len_c);
+    const uint32_t wv = (uint32_t)__builtin_amdgcn_readfirstlane(wid);
+    const uint32_t segw = ((lenc + 16 * 32 - 1) / (16 * 32)) * 32;
+    const uint32_t sg0 = min(wv * segw, lenc), sg1 = min(sg0 + segw, lenc);
+    uint32_t nrep = 0;
+    auto fallback = [&](uint32_t q) -> uint32_t {                   // (wave-uniform q) returns the step
+        const uint32_t m = lz_match_global(a.g, LZ_DS + cs + q);
+        if (lane == 0) a.match_rw[cs + q - a.batch_x0] = m;
+        if (lane == 0) step[q] = (uint16_t)((m >> 16) ? (m >> 16) : 1u);
+        nrep++;
+        return (m >> 16) ? (m >> 16) : 1u;
+    };
+    auto clear_bits = [&](uint32_t b0, uint32_t b1) {                // tokm bits [b0, b1) (inside this wave's words)
+        if (b0 >= b1) return;
+        for (uint32_t k = (b0 >> 5) + (uint32_t)lane; k <= ((b1 - 1) >> 5); k += 64) {
+            const uint32_t lo = max(b0, k << 5) - (k << 5), hi = min(b1, (k + 1) << 5) - (k << 5);
+            const uint32_t m = (hi >= 32 ? ~0u : ((1u << hi) - 1u)) & ~((1u << lo) - 1u);
+            tokm[k] &= ~m;
+        }
+    };
+    // the walk starts at the segment's first position the match search reached (a wave start of the
+    // match kernel for the default 64 KiB chunks), so it follows searched positions
+    uint32_t wst = sg1;
+    for (uint32_t b = sg0; b < sg1; b += 64) {
+        const uint64_t m = __ballot(b + lane < sg1 && step[b + lane] < 1024);
+        if (m) { wst = b + (uint32_t)__builtin_ctzll(m); break; }
+    }
+    wst = (uint32_t)__builtin_amdgcn_readfirstlane((int)wst);
+    uint32_t xspec = sg0;                                            // this wave's walk exit
+    if (wst < sg1) {
+        uint32_t cur = wst;
+        while (cur < sg1) {
+            const uint32_t s = cur + lane < lenc ? (uint32_t)step[cur + lane] : 64u;
+            const uint32_t lim = min(64u, sg1 - cur);
             uint64_t mask = 0;
             uint32_t p = 0;
-            while (p < 64 && cur + p < len_c) {
+            do {
                 mask |= 1ull << p;
-                uint32_t sp = (uint32_t)__builtin_amdgcn_readlane((int)s, (int)p);
-                if (sp == 0) {
-                    // a position of the parse that the parse-driven search never reached
-                    const uint32_t m = lz_match_global(a.g, LZ_DS + cs + cur + p);
-                    if (lane == 0) a.match_rw[cs + cur + p - a.batch_x0] = m;
-                    sp = (m >> 16) ? (m >> 16) : 1u;
-                    nrep++;
-                }
-                p += sp;
+                p += (uint32_t)__builtin_amdgcn_readlane((int)s, (int)p);
+            } while (p < lim);
+            if (p >= 1024) {
+                const uint32_t q = p - 1024;                         // (its token bit is in mask)
+                p = q + fallback(cur + q);
             }
             // OR the 64-bit window mask into tokm at bit `cur` (3 words at most)
             const uint32_t sh = cur & 31, w0 = cur >> 5;
@@ -562,12 +614,54 @@ ndfl_lz_encode_kernel(LzEncArgs a) {
                 if (piece && w0 + lane < 2048) tokm[w0 + lane] |= piece;
             }
             cur += p;
+            cur = (uint32_t)__builtin_amdgcn_readfirstlane((int)cur);
         }
-        if (nrep) { __threadfence(); if (lane == 0) ps.P = nrep; }
+        xspec = cur;
+    }
+    __syncthreads();
+    const uint64_t tqb = a.stats ? wall_clock64() : 0;
+    // true entries, in wave order (wexit[w]: wave w's true exit)
+    if (wid == 0 && lane == 0) wexit[0] = xspec;
+    __syncthreads();
+    for (int v = 1; v < 16; v++) {
+        if (wid == v && sg0 < sg1) {
+            const uint32_t e = wexit[v - 1];
+            uint32_t x = xspec;
+            if (e >= sg1) {
+                clear_bits(sg0, sg1);                                // the true parse passes over this segment
+                x = e;
+            } else {
+                clear_bits(sg0, e);
+                uint32_t t = e;
+                for (;;) {
+                    if (t >= sg1) { x = t; break; }
+                    if ((tokm[t >> 5] >> (t & 31)) & 1u) break;      // on this wave's walk: x = its exit
+                    if (lane == 0) tokm[t >> 5] |= 1u << (t & 31);
+                    uint32_t st = (uint32_t)__builtin_amdgcn_readfirstlane((int)step[t]);
+                    if (st >= 1024) st = fallback(t);
+                    clear_bits(t + 1, min(t + st, sg1));
+                    t += st;
+                }
+            }
+            if (lane == 0) wexit[v] = x;
+        } else if (wid == v && lane == 0) {
+            wexit[v] = wexit[v - 1];
+        }
+        __syncthreads();
+    }
+    if (a.stats && tid == 0) {
+        const uint64_t tqc = wall_clock64();
+        atomicAdd(&a.stats[14], tqb - tqa); atomicAdd(&a.stats[15], tqc - tqb);
+    }
+    if (nrep) {
+        __threadfence();
+        if (lane == 0) atomicAdd((unsigned long long*)&ps.P, (unsigned long long)nrep);
+        if (lane == 0 && a.stats) atomicAdd(&a.stats[2], (unsigned long long)nrep);
     }
     __syncthreads();
     if (ps.P) __threadfence();                                      // the stored repairs, seen by every wave
 
+    const uint64_t tq1 = a.stats ? wall_clock64() : 0;
     // ---- histograms --------------------------------------------------------------------------
     if (tid < 288) hlit[tid] = 0;
     if (tid < 32) hdist[tid] = 0;
@@ -594,10 +688,12 @@ ndfl_lz_encode_kernel(LzEncArgs a) {
     }
     __syncthreads();
 
+    const uint64_t tq2 = a.stats ? wall_clock64() : 0;
     // ---- codes ---------------------------------------------------------------------------------
     build_block_codes(a.dynamic != 0, scr, ps);
     const uint32_t packedLo = misc[4], packedHi = misc[5];
     __syncthreads();
+    const uint64_t tq3 = a.stats ? wall_clock64() : 0;
 
     // ---- token bits, block size ------------------------------------------------------------------
     uint32_t mybits = 0;
@@ -642,7 +738,13 @@ ndfl_lz_encode_kernel(LzEncArgs a) {
     }
 #undef NDFL_FOR_TOKENS
     __syncthreads();
+    const uint64_t tq4 = a.stats ? wall_clock64() : 0;
     block_lookback(c, a.base_bit, S, a.status, ps);
     block_store(obuf, ps.P, S, c, a.out, a.edge_w, a.edge_v);
+    if (a.stats && tid == 0) {
+        const uint64_t tq5 = wall_clock64();
+        atomicAdd(&a.stats[8], tq1 - tq0); atomicAdd(&a.stats[9], tq2 - tq1); atomicAdd(&a.stats[10], tq3 - tq2);
+        atomicAdd(&a.stats[11], tq4 - tq3); atomicAdd(&a.stats[12], tq5 - tq4); atomicAdd(&a.stats[13], 1ull);
+    }
     (void)lane;
 }
