@@ -259,6 +259,32 @@ constexpr int LZP_NEAR = 128;                      // buckets longer than this t
 
 __device__ __forceinline__ uint32_t lzp_hash(uint32_t k) { return (k * 2654435761u) >> (32 - LZP_HBITS); }
 
+// Wave maximum (all 64 lanes active): rotations within each row of 16 lanes by DPP, then the four
+// row maxima through readlane -- a uniform (scalar) result, no LDS crossbar round trips.
+__device__ __forceinline__ uint32_t wave_max_dpp(uint32_t x) {
+    x = max(x, (uint32_t)__builtin_amdgcn_mov_dpp((int)x, 0x128, 0xF, 0xF, false));   // row_ror:8
+    x = max(x, (uint32_t)__builtin_amdgcn_mov_dpp((int)x, 0x124, 0xF, 0xF, false));   // row_ror:4
+    x = max(x, (uint32_t)__builtin_amdgcn_mov_dpp((int)x, 0x122, 0xF, 0xF, false));   // row_ror:2
+    x = max(x, (uint32_t)__builtin_amdgcn_mov_dpp((int)x, 0x121, 0xF, 0xF, false));   // row_ror:1
+    const uint32_t r0 = (uint32_t)__builtin_amdgcn_readlane((int)x, 0), r1 = (uint32_t)__builtin_amdgcn_readlane((int)x, 16);
+    const uint32_t r2 = (uint32_t)__builtin_amdgcn_readlane((int)x, 32), r3 = (uint32_t)__builtin_amdgcn_readlane((int)x, 48);
+    return max(max(r0, r1), max(r2, r3));
+}
+
+// A wave's current chunk and parent chunk along its path (positions only grow): no division per
+// search.  All wave-uniform.
+struct LzpBnd {
+    uint64_t cs, ps;
+    __device__ __forceinline__ void init(const LzArgs& a, uint64_t q) {
+        cs = LZ_DS + ((q - LZ_DS) / a.chunk_len) * a.chunk_len;
+        ps = LZ_DS + ((q - LZ_DS) / a.parent_len) * a.parent_len;
+    }
+    __device__ __forceinline__ void advance(const LzArgs& a, uint64_t q) {
+        while (q >= cs + a.chunk_len) cs += a.chunk_len;
+        while (q >= ps + a.parent_len) ps += a.parent_len;
+    }
+};
+
 struct LzpS {
     uint32_t wb[LZP_WWORDS + 4];                   // window bytes [wb0, wb0 + 4 * LZP_WWORDS)
     uint16_t sorted[LZP_NPOS];                     // window offsets, grouped by hash bucket
@@ -270,15 +296,14 @@ struct LzpS {
 
 // Wave-cooperative exact search at buffer position q (window-relative rq).  All lanes call with the
 // same q; returns the match word (run << 16 | dist - 1, or the literal byte).
-__device__ __forceinline__ uint32_t lzp_search(const LzArgs& a, const LzpS& S, int64_t wb0, uint64_t q, uint64_t cs0,
-                                               uint64_t pps0, uint32_t* st) {
+__device__ __forceinline__ uint32_t lzp_search(const LzArgs& a, const LzpS& S, int64_t wb0, uint64_t q, LzpBnd& bd,
+                                               uint32_t* st) {
     const int lane = threadIdx.x & 63;
     const uint32_t rq = (uint32_t)((int64_t)q - wb0);
-    const uint64_t cs = cs0 + (uint64_t)(((uint32_t)(q - cs0) / a.chunk_len) * a.chunk_len);
-    const uint64_t e = min(cs + a.chunk_len, a.total);
+    bd.advance(a, q);
+    const uint64_t e = min(bd.cs + a.chunk_len, a.total);
     const uint32_t maxlen = (uint32_t)min((uint64_t)a.max_run, e - q);
-    const uint64_t ps = pps0 + (uint64_t)(((uint32_t)(q - pps0) / a.parent_len) * a.parent_len);
-    const uint64_t off = ps - min((uint64_t)a.hist_limit, ps - a.vstart);
+    const uint64_t off = bd.ps - min((uint64_t)a.hist_limit, bd.ps - a.vstart);
     const int64_t lo = max((int64_t)q - (int64_t)a.max_dist, (int64_t)off);
     const int64_t hi = (int64_t)q - (int64_t)a.min_dist;
     const uint32_t lit = lz_byte(S.wb, rq);
@@ -307,8 +332,7 @@ __device__ __forceinline__ uint32_t lzp_search(const LzArgs& a, const LzpS& S, i
         const uint32_t r = rhi - (uint32_t)lane;
         uint32_t k = 0;
         if ((int64_t)rhi - lane >= (int64_t)rlo) { const uint32_t run = run_of(r); if (run) k = run << 16 | r; }
-#pragma unroll
-        for (int o = 32; o > 0; o >>= 1) k = max(k, (uint32_t)__shfl_xor((int)k, o, 64));
+        k = wave_max_dpp(k);
         if ((k >> 16) >= maxlen) best = k;
         st[1] += 64u;
     }
@@ -321,8 +345,7 @@ __device__ __forceinline__ uint32_t lzp_search(const LzArgs& a, const LzpS& S, i
             }
             best = max(best, k);
         }
-#pragma unroll
-        for (int o = 32; o > 0; o >>= 1) best = max(best, (uint32_t)__shfl_xor((int)best, o, 64));
+        best = wave_max_dpp(best);
         st[1] += B1 - B0;
     }
     st[0]++;
@@ -384,8 +407,6 @@ ndfl_lz_parse_match_kernel(LzArgs a, uint32_t lead_on) {
     const uint64_t tk1 = a.stats ? wall_clock64() : 0;
     // chunk / parent chunk of the tile's lead-in start (positions step from them with 32-bit math)
     const uint64_t q00 = p0 - LZP_LEAD >= a.p_begin ? p0 - LZP_LEAD : p0;
-    const uint64_t cs0 = LZ_DS + ((q00 - LZ_DS) / a.chunk_len) * a.chunk_len;
-    const uint64_t pps0 = LZ_DS + ((q00 - LZ_DS) / a.parent_len) * a.parent_len;
     auto step_of = [&](uint32_t m) -> uint32_t { return (m >> 16) ? (m >> 16) : 1u; };
     // the waves' paths
     const uint64_t s_w = p0 + (uint64_t)w * LZP_SEG;
@@ -393,8 +414,10 @@ ndfl_lz_parse_match_kernel(LzArgs a, uint32_t lead_on) {
     if (s_w < p1) {
         const bool chunk_start = ((p0 - LZ_DS) % a.chunk_len) == 0;
         uint64_t q = (w == 0 && lead_on && !chunk_start) ? q00 : s_w;
+        LzpBnd bd;
+        bd.init(a, q);
         while (q < e_w) {
-            const uint32_t m = lzp_search(a, S, wb0, q, cs0, pps0, st);
+            const uint32_t m = lzp_search(a, S, wb0, q, bd, st);
             if (q >= s_w) {
                 const uint32_t t = (uint32_t)(q - p0);
                 if (lane == 0) { a.match[q - a.p_begin] = m; atomicOr(&S.vis[t >> 5], 1u << (t & 31)); }
@@ -415,9 +438,11 @@ ndfl_lz_parse_match_kernel(LzArgs a, uint32_t lead_on) {
             if (ent >= ev) x = ent;                     // the true path passes over this segment
             else if (!((S.vis[ent >> 5] >> (ent & 31)) & 1u)) {
                 uint32_t t = ent;
+                LzpBnd bd;
+                bd.init(a, p0 + t);
                 while (t < ev && !((S.vis[t >> 5] >> (t & 31)) & 1u)) {
                     const uint64_t q = p0 + t;
-                    const uint32_t m = lzp_search(a, S, wb0, q, cs0, pps0, st);
+                    const uint32_t m = lzp_search(a, S, wb0, q, bd, st);
                     if (lane == 0) { a.match[q - a.p_begin] = m; atomicOr(&S.vis[t >> 5], 1u << (t & 31)); }
                     t += step_of(m);
                 }
