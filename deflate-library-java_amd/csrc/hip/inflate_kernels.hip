@@ -409,6 +409,125 @@ __device__ __forceinline__ void find_word(const In& in, uint64_t t, uint64_t sca
     }
 }
 
+// Compacted Kraft test (NDFL_FIND_COMPACT, the default): the same survivors as find_word, for the
+// 64 words of a wave at once.  The cheap bit-sliced masks (BTYPE, BFINAL, HLIT/HDIST, stored LEN/NLEN)
+// stay per lane; the positions they leave for the code-length code's Kraft test -- about 1 in 9 --
+// are compacted into a wave list and tested one per lane: the HCLEN + 4 three-bit lengths as one
+// 57-bit field, summed by five lookups of a 4,096-entry table of the Kraft sums of four lengths
+// (kr4).  About 30 operations per such position instead of the bit-sliced test's 451 per 32
+// positions, which the finder's VALU-bound scan spends at every position.  A pass takes at most
+// FIND_TAKE positions per lane (a dense pattern takes more passes).
+#ifndef NDFL_FIND_COMPACT
+#define NDFL_FIND_COMPACT 1
+#endif
+constexpr uint32_t FIND_TAKE = 8;
+constexpr uint32_t FIND_CLIST = 64 * FIND_TAKE;
+struct FindWaveScratch {
+    uint32_t w[64 + 4];                            // the wave's words and the three after them
+    uint16_t list[FIND_CLIST];                     // lane << 5 | bit of each position to test
+};
+// (survivors go to the workgroup's LDS list as 32-bit offsets from bit `pb`, bit 31 set: dynamic)
+__device__ __forceinline__ void find_word_wave(const In& in, uint64_t t, uint64_t scan_end, uint32_t* cand,
+                                               uint32_t* ncand, FindWaveScratch& fw, const uint16_t* kr4, uint64_t pb) {
+    const uint64_t nbits = in.nbits;
+    const int lane = threadIdx.x & 63;
+    const uint64_t p0 = t * 32;
+    const uint32_t w0 = in.ld(t), w1 = in.ld(t + 1), w2 = in.ld(t + 2), w3 = in.ld(t + 3);
+    const uint64_t W = (uint64_t)w0 | ((uint64_t)w1 << 32);
+    const uint32_t b1 = (uint32_t)(W >> 1), b2 = (uint32_t)(W >> 2);
+    uint32_t valid = 0xFFFFFFFFu;
+    if (p0 + 35 > nbits) valid = (nbits >= p0 + 3) ? (uint32_t)((1ull << (nbits - p0 - 2)) - 1) : 0u;
+    if (p0 + 32 > scan_end) valid &= p0 < scan_end ? (uint32_t)((1ull << (scan_end - p0)) - 1) : 0u;
+#if NDFL_FIND_LASTBLK
+    const uint32_t notfinal = ~0u;
+#else
+    const uint32_t notfinal = ~w0;
+#endif
+    const uint32_t h4 = (uint32_t)(W >> 4), h5 = (uint32_t)(W >> 5), h6 = (uint32_t)(W >> 6),
+                   h7 = (uint32_t)(W >> 7), d9 = (uint32_t)(W >> 9), d10 = (uint32_t)(W >> 10),
+                   d11 = (uint32_t)(W >> 11), d12 = (uint32_t)(W >> 12);
+    const uint32_t big = (NDFL_BOP3(h4, h5, h6, 0x80) & h7) | (NDFL_BOP3(d9, d10, d11, 0x80) & d12);
+    const uint32_t pm = ~b1 & b2 & valid & notfinal & ~big;         // before the Kraft test
+    // stored headers: LEN == ~NLEN (as find_word)
+    const uint64_t W12 = (uint64_t)w1 | ((uint64_t)w2 << 32);
+    const uint32_t x1 = (uint32_t)(W >> 8), x2 = (uint32_t)(W >> 16), x3 = (uint32_t)(W >> 24), x4 = w1,
+                   x5 = (uint32_t)(W12 >> 8);
+#define NDFL_LENOK(x) ((((x) ^ ((x) >> 16)) & 0xFFFFu) == 0xFFFFu)
+    const uint32_t okm = (NDFL_LENOK(x1) ? 0x0000003Fu : 0u) | (NDFL_LENOK(x2) ? 0x00003FC0u : 0u) |
+                         (NDFL_LENOK(x3) ? 0x003FC000u : 0u) | (NDFL_LENOK(x4) ? 0x3FC00000u : 0u) |
+                         (NDFL_LENOK(x5) ? 0xC0000000u : 0u);
+#undef NDFL_LENOK
+    uint32_t m0 = ~b1 & ~b2 & valid & notfinal & okm;
+    while (m0) {
+        const uint32_t o = __builtin_ctz(m0);
+        m0 &= m0 - 1;
+        const uint32_t q = o + 3, al = (q + 7) & ~7u;
+        const uint32_t pad = al > q ? (uint32_t)(W >> q) & ((1u << (al - q)) - 1u) : 0u;
+        if (pad) continue;
+        const uint32_t ln = (al < 32 ? (uint32_t)(W >> al) : (uint32_t)(W12 >> (al - 32))) & 0xFFFFu;
+        if (p0 + al + 32 + 8ull * ln <= nbits) {
+            uint32_t k = atomicAdd(ncand, 1u);
+            if (k < 2048) cand[k] = (uint32_t)(p0 + o - pb);
+        }
+    }
+    // dynamic headers
+    fw.w[lane] = w0;
+    {
+        const uint32_t e1 = __shfl(w1, 63, 64), e2 = __shfl(w2, 63, 64), e3 = __shfl(w3, 63, 64);
+        if (lane < 3) fw.w[64 + lane] = lane == 0 ? e1 : lane == 1 ? e2 : e3;
+    }
+    const uint64_t tw0 = t - (uint64_t)lane;                        // the wave's first word
+    uint32_t rem = pm;
+    for (;;) {
+        const uint32_t cnt = min((uint32_t)__popc(rem), FIND_TAKE);
+        uint32_t incl = cnt;
+#pragma unroll
+        for (int o = 1; o < 64; o <<= 1) {
+            const uint32_t y = __shfl_up(incl, o, 64);
+            if (lane >= o) incl += y;
+        }
+        const uint32_t total = (uint32_t)__shfl(incl, 63, 64);
+        if (total == 0) break;                                       // (uniform)
+        {
+            uint32_t k = incl - cnt;
+            for (uint32_t i = 0; i < cnt; i++) {
+                fw.list[k++] = (uint16_t)((lane << 5) | __builtin_ctz(rem));
+                rem &= rem - 1;
+            }
+        }
+        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+        __builtin_amdgcn_wave_barrier();
+        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+        for (uint32_t j = (uint32_t)lane; j < total; j += 64) {
+            const uint32_t c = fw.list[j];
+            const uint32_t lw = c >> 5, o = c & 31;
+            const uint64_t A = (uint64_t)fw.w[lw] | ((uint64_t)fw.w[lw + 1] << 32);
+            const uint64_t B = (uint64_t)fw.w[lw + 2] | ((uint64_t)fw.w[lw + 3] << 32);
+            const uint32_t ncl = (uint32_t)((A >> (o + 13)) & 15u) + 4;
+            const uint32_t sh = o + 17;                              // 17..48
+            uint64_t F = (A >> sh) | (B << (64 - sh));
+            F &= (1ull << (3 * ncl)) - 1;                            // the HCLEN + 4 lengths (<= 57 bits)
+            const uint32_t ks = (uint32_t)kr4[F & 4095] + kr4[(F >> 12) & 4095] + kr4[(F >> 24) & 4095] +
+                                kr4[(F >> 36) & 4095] + kr4[(F >> 48) & 4095];
+            const uint64_t p = (tw0 + lw) * 32 + o;
+            if (ks == 128 && p + 17 + 3 * ncl <= nbits) {
+                uint32_t k = atomicAdd(ncand, 1u);
+                if (k < 2048) cand[k] = (uint32_t)(p - pb) | (1u << 31);
+            }
+        }
+        __builtin_amdgcn_wave_barrier();                             // (the list is rewritten next)
+    }
+}
+// Kraft sums of four 3-bit lengths (index: four fields, the first in the low bits), x 1/128
+__device__ __forceinline__ void kr4_fill(uint16_t* kr4) {
+    for (uint32_t i = threadIdx.x; i < 4096; i += blockDim.x) {
+        uint32_t s = 0;
+#pragma unroll
+        for (int f = 0; f < 4; f++) { const uint32_t l = (i >> (3 * f)) & 7u; s += l ? 128u >> l : 0u; }
+        kr4[i] = (uint16_t)s;
+    }
+}
+
 // the workgroup's LDS survivors -> the global survivor list (one global atomic)
 __device__ __forceinline__ void find_flush(const uint64_t* cand, const uint32_t* ncand, uint32_t* gbase,
                                            uint64_t* qlist, uint32_t* qcount, uint32_t qcap) {
@@ -440,6 +559,35 @@ ndfl_inflate_find_kernel(const uint32_t* w, uint64_t nwords, uint64_t nbits, uin
         find_word(in, t, scan_end, cand, &ncand);
     }
     find_flush(cand, &ncand, &gbase, qlist, qcount, qcap);
+}
+
+// The dense scan with the compacted Kraft test (find_word_wave): every position of [w_lo * 32, scan_end).
+extern "C" __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(NDFL_FIND_WPE)))
+ndfl_inflate_find_compact_kernel(const uint32_t* w, uint64_t nwords, uint64_t nbits, uint64_t* qlist, uint32_t* qcount,
+                                 uint32_t qcap, uint64_t w_lo, uint64_t scan_end) {
+    using namespace inf;
+    __shared__ uint32_t cand[2048];
+    __shared__ uint32_t ncand, gbase;
+    __shared__ uint16_t kr4[4096];
+    __shared__ FindWaveScratch fws[4];
+    kr4_fill(kr4);
+    if (threadIdx.x == 0) ncand = 0;
+    __syncthreads();
+    In in{w, nwords, nbits};
+    const uint64_t pb = (w_lo + (uint64_t)blockIdx.x * FIND_WPT * 256) * 32;    // the workgroup's first bit
+    for (uint32_t kk = 0; kk < FIND_WPT; kk++) {
+        const uint64_t tt = ((uint64_t)blockIdx.x * FIND_WPT + kk) * blockDim.x + threadIdx.x;
+        find_word_wave(in, w_lo + tt, scan_end, cand, &ncand, fws[threadIdx.x >> 6], kr4, pb);
+    }
+    // the workgroup's LDS survivors -> the global survivor list (one global atomic)
+    __syncthreads();
+    const uint32_t nc = min(ncand, 2048u);
+    if (threadIdx.x == 0) gbase = nc ? atomicAdd(qcount, nc) : 0u;
+    __syncthreads();
+    for (uint32_t k = threadIdx.x; k < nc; k += blockDim.x) {
+        const uint32_t c = cand[k];
+        if (gbase + k < qcap) qlist[gbase + k] = (pb + (c & 0x7FFFFFFFu)) | ((uint64_t)(c >> 31) << 63);
+    }
 }
 
 // Partitioned finder (long streams): the scanned range is cut into partitions of part_words input
@@ -1542,8 +1690,16 @@ static int inflate_run(InflateScratch& S, hipStream_t s, const uint8_t* in, uint
             S.find_parts = nparts;
             S.find_part_bits = part_words * 32;
         } else if (nthr) {
-            hipLaunchKernelGGL(ndfl_inflate_find_kernel, dim3((uint32_t)((nthr + 256 * FIND_WPT - 1) / (256 * FIND_WPT))), dim3(256), 0, s, d_w,
-                               nwords, nbits, d_qlist, d_qcount, qcap, win, period, w_lo, scan_end);
+            // every position (the default): the compacted Kraft test (NDFL_FIND_BITSLICED=1: the
+            // bit-sliced one, A/B); windows of the stream: the bit-sliced finder
+            static const bool bitsliced = getenv("NDFL_FIND_BITSLICED") != nullptr;
+            const uint32_t fgrid = (uint32_t)((nthr + 256 * FIND_WPT - 1) / (256 * FIND_WPT));
+            if (NDFL_FIND_COMPACT && win == period && !bitsliced)
+                hipLaunchKernelGGL(ndfl_inflate_find_compact_kernel, dim3(fgrid), dim3(256), 0, s, d_w, nwords, nbits, d_qlist,
+                                   d_qcount, qcap, w_lo, scan_end);
+            else
+                hipLaunchKernelGGL(ndfl_inflate_find_kernel, dim3(fgrid), dim3(256), 0, s, d_w,
+                                   nwords, nbits, d_qlist, d_qcount, qcap, win, period, w_lo, scan_end);
             INF_CHK(hipGetLastError());
             hipLaunchKernelGGL(ndfl_inflate_strict_kernel, dim3(strict_grid), dim3(256), 0, s, d_w, nwords, nbits,
                                (const uint64_t*)d_qlist, (const uint32_t*)d_qcount, qcap, d_cnt, d_list,
