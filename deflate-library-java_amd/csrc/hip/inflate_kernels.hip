@@ -422,6 +422,7 @@ __device__ __forceinline__ void find_word(const In& in, uint64_t t, uint64_t sca
 #endif
 constexpr uint32_t FIND_TAKE = 8;
 constexpr uint32_t FIND_CLIST = 64 * FIND_TAKE;
+constexpr uint32_t FIND_CCAP = 1024;               // survivors kept per workgroup (131,072 positions; ~65 on average)
 struct FindWaveScratch {
     uint32_t w[64 + 4];                            // the wave's words and the three after them
     uint16_t list[FIND_CLIST];                     // lane << 5 | bit of each position to test
@@ -467,7 +468,7 @@ __device__ __forceinline__ void find_word_wave(const In& in, uint64_t t, uint64_
         const uint32_t ln = (al < 32 ? (uint32_t)(W >> al) : (uint32_t)(W12 >> (al - 32))) & 0xFFFFu;
         if (p0 + al + 32 + 8ull * ln <= nbits) {
             uint32_t k = atomicAdd(ncand, 1u);
-            if (k < 2048) cand[k] = (uint32_t)(p0 + o - pb);
+            if (k < FIND_CCAP) cand[k] = (uint32_t)(p0 + o - pb);
         }
     }
     // dynamic headers
@@ -480,13 +481,15 @@ __device__ __forceinline__ void find_word_wave(const In& in, uint64_t t, uint64_
     uint32_t rem = pm;
     for (;;) {
         const uint32_t cnt = min((uint32_t)__popc(rem), FIND_TAKE);
+        // inclusive wave scan by DPP (row shifts, then the row totals broadcast across rows)
         uint32_t incl = cnt;
-#pragma unroll
-        for (int o = 1; o < 64; o <<= 1) {
-            const uint32_t y = __shfl_up(incl, o, 64);
-            if (lane >= o) incl += y;
-        }
-        const uint32_t total = (uint32_t)__shfl(incl, 63, 64);
+        incl += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)incl, 0x111, 0xF, 0xF, false);   // row_shr:1
+        incl += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)incl, 0x112, 0xF, 0xF, false);   // row_shr:2
+        incl += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)incl, 0x114, 0xF, 0xF, false);   // row_shr:4
+        incl += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)incl, 0x118, 0xF, 0xF, false);   // row_shr:8
+        incl += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)incl, 0x142, 0xA, 0xF, false);   // row_bcast:15
+        incl += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)incl, 0x143, 0xC, 0xF, false);   // row_bcast:31
+        const uint32_t total = (uint32_t)__builtin_amdgcn_readlane((int)incl, 63);
         if (total == 0) break;                                       // (uniform)
         {
             uint32_t k = incl - cnt;
@@ -512,7 +515,7 @@ __device__ __forceinline__ void find_word_wave(const In& in, uint64_t t, uint64_
             const uint64_t p = (tw0 + lw) * 32 + o;
             if (ks == 128 && p + 17 + 3 * ncl <= nbits) {
                 uint32_t k = atomicAdd(ncand, 1u);
-                if (k < 2048) cand[k] = (uint32_t)(p - pb) | (1u << 31);
+                if (k < FIND_CCAP) cand[k] = (uint32_t)(p - pb) | (1u << 31);
             }
         }
         __builtin_amdgcn_wave_barrier();                             // (the list is rewritten next)
@@ -566,7 +569,7 @@ extern "C" __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_pe
 ndfl_inflate_find_compact_kernel(const uint32_t* w, uint64_t nwords, uint64_t nbits, uint64_t* qlist, uint32_t* qcount,
                                  uint32_t qcap, uint64_t w_lo, uint64_t scan_end) {
     using namespace inf;
-    __shared__ uint32_t cand[2048];
+    __shared__ uint32_t cand[FIND_CCAP];
     __shared__ uint32_t ncand, gbase;
     __shared__ uint16_t kr4[4096];
     __shared__ FindWaveScratch fws[4];
@@ -581,7 +584,7 @@ ndfl_inflate_find_compact_kernel(const uint32_t* w, uint64_t nwords, uint64_t nb
     }
     // the workgroup's LDS survivors -> the global survivor list (one global atomic)
     __syncthreads();
-    const uint32_t nc = min(ncand, 2048u);
+    const uint32_t nc = min(ncand, FIND_CCAP);
     if (threadIdx.x == 0) gbase = nc ? atomicAdd(qcount, nc) : 0u;
     __syncthreads();
     for (uint32_t k = threadIdx.x; k < nc; k += blockDim.x) {
