@@ -96,6 +96,11 @@ struct In {
     uint64_t nwords;
     uint64_t nbits;
     __device__ __forceinline__ uint32_t ld(uint64_t i) const { return i < nwords ? w[i] : 0u; }
+    // the input from bit p on (at least 32 bits; zeros past the end)
+    __device__ __forceinline__ uint64_t win64(uint64_t p) const {
+        const uint64_t i = p >> 5;
+        return (((uint64_t)ld(i + 1) << 32) | ld(i)) >> (p & 31);
+    }
     // unchecked 16-byte group load; positions past the end are clamped into the zero padding
     __device__ __forceinline__ u32x4 ld4(uint64_t g) const {
         const uint64_t gmax = (nwords + 3) / 4 + 1;
@@ -1191,6 +1196,7 @@ struct InflateScratch {
     void* d_pend = nullptr; size_t d_pend_cap = 0;    // emit: pending bit per output byte
     void* d_rl = nullptr; size_t d_rl_cap = 0;        // resolve: two group lists + round bits
     void* d_ticket = nullptr;
+    void* d_slow = nullptr; size_t d_slow_cap = 0;    // emit: chains the fast emit pass leaves to the full one
     void* d_ph = nullptr;                             // count pass: phase-fallback slot per wave
     void* d_hrec = nullptr;                           // count pass: header records, one per candidate
     size_t d_hrec_cap = 0;
@@ -1212,7 +1218,7 @@ struct InflateScratch {
     uint64_t p_nbytes = 0;
     void release() {
         void** ps[] = {&d_in, &d_cand, &d_starts, &d_stops, &d_res, &d_cands, &d_stats, &d_q, &d_seg, &d_chains, &d_off,
-                       &d_ref, &d_pend, &d_rl, &d_ticket, &d_ph, &d_cticket, &d_out, &d_done, &d_hrec};
+                       &d_ref, &d_pend, &d_rl, &d_ticket, &d_ph, &d_cticket, &d_out, &d_done, &d_hrec, &d_slow};
         for (void** p : ps) { if (*p) hipFree(*p); *p = nullptr; }
         for (auto& e : ev) { if (e) hipEventDestroy(e); e = nullptr; }
         if (h_cnt) hipHostFree(h_cnt);
@@ -1525,12 +1531,37 @@ static int inflate_devlink(InflateScratch& S, hipStream_t s, const uint32_t* d_w
     INF_CHK(hipMemsetAsync(S.d_ticket, 0, 64, s));
     INF_CHK(hipEventRecord(S.ev[4], s));
     static const uint32_t emit_grid = wave_grid(ndfl_inflate_emit_wave_kernel, EMIT_WAVES, "NDFL_EMIT_WPC");
-    hipLaunchKernelGGL(ndfl_inflate_emit_wave_kernel, dim3(std::min<uint32_t>(ncand, emit_grid)), dim3(64), 0, s, d_w,
-                       nwords, nbits, (const EmitChain*)S.d_chains, ncand, (uint32_t*)S.d_ticket, d_out,
-                       (ChainRes*)S.d_res, (const uint64_t*)S.d_cands, ncand, (uint32_t*)S.d_ref, (uint32_t*)S.d_pend,
-                       S.pool, (wv::PhArr*)S.d_ph, stats_on ? (uint32_t*)S.d_stats : nullptr, (const uint64_t*)info,
-                       (const uint32_t*)d_order);
-    INF_CHK(hipGetLastError());
+    // NDFL_EMIT_FAST (default 1): the record-replay emit kernel first, the full one over what it leaves
+    const char* efe = getenv("NDFL_EMIT_FAST");
+    if (!efe || atoi(efe)) {
+        INF_CHK(inf_ensure(&S.d_slow, &S.d_slow_cap, (size_t)ncand * 4 + 64));
+        uint32_t* tk = (uint32_t*)S.d_ticket;             // [0] fast tickets, [4] full tickets, [8] slow count
+        static const uint32_t fast_grid = wave_grid(ndfl_inflate_emit_fast_kernel, EMIT_WAVES, "NDFL_EMITF_WPC");
+        hipLaunchKernelGGL(ndfl_inflate_emit_fast_kernel, dim3(std::min<uint32_t>(ncand, fast_grid)), dim3(64), 0, s, d_w,
+                           nwords, nbits, (const EmitChain*)S.d_chains, tk, d_out, (ChainRes*)S.d_res,
+                           (uint32_t*)S.d_ref, (uint32_t*)S.d_pend, S.pool, (const uint64_t*)info, (const uint32_t*)d_order,
+                           (uint32_t*)S.d_slow, tk + 8);
+        INF_CHK(hipGetLastError());
+        hipLaunchKernelGGL(ndfl_inflate_emit_wave_kernel, dim3(std::min<uint32_t>(ncand, emit_grid)), dim3(64), 0, s, d_w,
+                           nwords, nbits, (const EmitChain*)S.d_chains, ncand, tk + 4, d_out,
+                           (ChainRes*)S.d_res, (const uint64_t*)S.d_cands, ncand, (uint32_t*)S.d_ref, (uint32_t*)S.d_pend,
+                           S.pool, (wv::PhArr*)S.d_ph, stats_on ? (uint32_t*)S.d_stats : nullptr, (const uint64_t*)info,
+                           (const uint32_t*)S.d_slow, (const uint32_t*)(tk + 8));
+        INF_CHK(hipGetLastError());
+        if (stats_on) {
+            uint32_t nsl = 0;
+            INF_CHK(hipMemcpyAsync(&nsl, tk + 8, 4, hipMemcpyDeviceToHost, s));
+            INF_CHK(hipStreamSynchronize(s));
+            fprintf(stderr, "[ndfl] fast emit pass left %u chains to the full emit pass\n", nsl);
+        }
+    } else {
+        hipLaunchKernelGGL(ndfl_inflate_emit_wave_kernel, dim3(std::min<uint32_t>(ncand, emit_grid)), dim3(64), 0, s, d_w,
+                           nwords, nbits, (const EmitChain*)S.d_chains, ncand, (uint32_t*)S.d_ticket, d_out,
+                           (ChainRes*)S.d_res, (const uint64_t*)S.d_cands, ncand, (uint32_t*)S.d_ref, (uint32_t*)S.d_pend,
+                           S.pool, (wv::PhArr*)S.d_ph, stats_on ? (uint32_t*)S.d_stats : nullptr, (const uint64_t*)info,
+                           (const uint32_t*)d_order, (const uint32_t*)nullptr);
+        INF_CHK(hipGetLastError());
+    }
     INF_CHK(hipEventRecord(S.ev[5], s));
     hipLaunchKernelGGL(ndfl_inflate_summary_kernel, dim3(1), dim3(1024), 0, s, (const ChainRes*)S.d_res,
                        (const EmitChain*)S.d_chains, info, dict_len, partial ? 1u : 0u);
@@ -2001,7 +2032,7 @@ static int inflate_run(InflateScratch& S, hipStream_t s, const uint8_t* in, uint
                        nwords, nbits, (const EmitChain*)S.d_chains, nch, (uint32_t*)S.d_ticket, d_out,
                        (ChainRes*)S.d_res, (const uint64_t*)S.d_cands, ncand, (uint32_t*)S.d_ref, (uint32_t*)S.d_pend,
                        pool, (wv::PhArr*)S.d_ph, stats_on ? (uint32_t*)S.d_stats : nullptr, (const uint64_t*)nullptr,
-                       (const uint32_t*)nullptr);
+                       (const uint32_t*)nullptr, (const uint32_t*)nullptr);
     INF_CHK(hipGetLastError());
     INF_CHK(hipEventRecord(e3, s));
     std::vector<ChainRes> er(nch);

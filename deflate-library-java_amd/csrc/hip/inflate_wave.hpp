@@ -193,9 +193,24 @@ __device__ __forceinline__ void stage_round(const In& in, const Geo& g, Stage& s
 struct Lv {
     const uint32_t* p;     // &st.w[lane]
     uint32_t rw;           // region's first word (relative to base)
+    __device__ __forceinline__ uint32_t ld(uint32_t i) const { return p[i * 64]; }   // region word i
     __device__ __forceinline__ void win(uint32_t pos, uint32_t& lo, uint32_t& hi) const {
         const uint32_t* q = p + ((pos >> 5) - rw) * 64;
         const uint32_t a = q[0], b = q[64], c = q[128];
+        lo = __builtin_amdgcn_alignbit(b, a, pos & 31);
+        hi = __builtin_amdgcn_alignbit(c, b, pos & 31);
+    }
+};
+// The lane's view of a round read straight from the input in global memory (the fast emit pass):
+// the same region-relative words as Lv, through L1/L2 instead of an LDS stage.  Reads up to the
+// region's end plus the tail words, inside the IN_PAD zero bytes after the input (as the stage).
+struct Gv {
+    const uint32_t* q;     // the lane's region word 0 in the input
+    uint32_t rw;           // region's first word (relative to base)
+    __device__ __forceinline__ uint32_t ld(uint32_t i) const { return q[i]; }
+    __device__ __forceinline__ void win(uint32_t pos, uint32_t& lo, uint32_t& hi) const {
+        const uint32_t i = (pos >> 5) - rw;
+        const uint32_t a = q[i], b = q[i + 1], c = q[i + 2];
         lo = __builtin_amdgcn_alignbit(b, a, pos & 31);
         hi = __builtin_amdgcn_alignbit(c, b, pos & 31);
     }
@@ -216,8 +231,8 @@ __device__ __forceinline__ Lv make_lv(const Stage& st, const Geo& g, int lane) {
 template <bool CAREFUL>
 __device__ __forceinline__ void tok_e(uint32_t lo, uint32_t hi, uint32_t e, uint32_t& pos, const Tabs& t,
                                       bool empty_dist, uint32_t stop, uint32_t nb, Tok& tk);
-template <bool CAREFUL>
-__device__ __forceinline__ void tok(const Lv& v, uint32_t& pos, const Tabs& t, bool empty_dist, uint32_t stop,
+template <bool CAREFUL, class V>
+__device__ __forceinline__ void tok(const V& v, uint32_t& pos, const Tabs& t, bool empty_dist, uint32_t stop,
                                     uint32_t nb, Tok& tk) {
     // (the result goes through scalars and is stored into tk once: stores of different fields on
     // different paths made the compiler keep tk in scratch memory)
@@ -291,36 +306,49 @@ struct Bb {
     uint32_t nxt;      // that word
     uint32_t pos;      // round-relative bit position
 };
-__device__ __forceinline__ void bb_init(Bb& b, const Lv& v, uint32_t pos) {
+// (V: the staged round in LDS (Lv) or the input in global memory (Gv): region word i = v.ld(i))
+template <class V>
+__device__ __forceinline__ void bb_init(Bb& b, const V& v, uint32_t pos) {
     const uint32_t i = (pos >> 5) - v.rw, s = pos & 31;
-    const uint32_t* q = v.p + i * 64;
-    b.buf = ((uint64_t)q[0] | ((uint64_t)q[64] << 32)) >> s;
+    b.buf = ((uint64_t)v.ld(i) | ((uint64_t)v.ld(i + 1) << 32)) >> s;
     b.nb = 64 - s;
     b.wi = i + 2;
-    b.nxt = q[128];
+    b.nxt = v.ld(i + 2);
     b.pos = pos;
 }
-__device__ __forceinline__ void bb_refill(Bb& b, const Lv& v) {
+template <class V>
+__device__ __forceinline__ void bb_refill(Bb& b, const V& v) {
     if (b.nb < 32) {
         b.buf |= (uint64_t)b.nxt << b.nb;
         b.nb += 32;
         b.wi++;
-        b.nxt = v.p[b.wi * 64];
+        b.nxt = v.ld(b.wi);
     }
 }
 __device__ __forceinline__ void bb_skip(Bb& b, uint32_t n) {
     b.buf >>= n; b.nb -= n; b.pos += n;
 }
-// tok<false> on the bit buffer (the caller guarantees pos + 48 < stop <= nb)
-__device__ __forceinline__ void tok_bb(Bb& b, const Lv& v, const Tabs& t, bool empty_dist, Tok& tk) {
+// A token step on the bit buffer: the caller guarantees pos + 48 < nb (no token reaches the input
+// end, so none of its checks are needed).  STOP = false: also pos + 48 < stop (tok<false>);
+// STOP = true: any pos < stop -- a literal pair whose first literal reaches `stop` is split, as in
+// tok<true>, so the buffer carries a decode right up to a checkpoint or the segment end.
+template <bool STOP = false, class V>
+__device__ __forceinline__ void tok_bb(Bb& b, const V& v, const Tabs& t, bool empty_dist, Tok& tk, uint32_t stop = 0) {
     uint32_t lo = (uint32_t)b.buf;
     uint32_t e = t.lit[lo & ((1u << LB) - 1u)];
     uint32_t kind, val, n = 1, dist = 0;
     do {
         if (e >> 31) {
-            const uint32_t adv = e & 15;
-            bb_skip(b, adv);
-            kind = K_LIT; n = 1u + ((e >> 8) & 1u); val = (e >> 9) & (n == 2 ? 0xFFFFu : 0xFFu);
+            if (STOP) {
+                const uint32_t l1 = (e >> 4) & 15;
+                const bool two = ((e >> 8) & 1) && b.pos + l1 < stop;
+                bb_skip(b, two ? e & 15 : l1);
+                n = 1u + (uint32_t)two;
+            } else {
+                bb_skip(b, e & 15);
+                n = 1u + ((e >> 8) & 1u);
+            }
+            kind = K_LIT; val = (e >> 9) & (n == 2 ? 0xFFFFu : 0xFFu);
             break;
         }
         if (!(e & 31)) e = long_lit(e, lo, t);
@@ -353,14 +381,17 @@ __device__ __forceinline__ void tok_bb(Bb& b, const Lv& v, const Tabs& t, bool e
 __device__ __forceinline__ bool run_to(const Lv& v, uint32_t& pos, const Tabs& t, bool ed, uint32_t stop, uint32_t nb,
                                        uint32_t& cnt, Tok& tk) {
 #if NDFL_BITBUF
-    if (pos + 48 < stop) {
+    // the bit buffer up to the stop itself (pairs split there); only the input's last 48 bits go
+    // through the checked decoder
+    const uint32_t lim = min(stop, nb - min(nb, 48u));
+    if (pos < lim) {
         Bb b;
         bb_init(b, v, pos);
         do {
-            tok_bb(b, v, t, ed, tk);
+            tok_bb<true>(b, v, t, ed, tk, stop);
             if (tk.kind > K_LEN) { pos = b.pos; return true; }
             cnt += tk.n;
-        } while (b.pos + 48 < stop);
+        } while (b.pos < lim);
         pos = b.pos;
     }
 #else
@@ -668,8 +699,8 @@ __device__ int build_tables(Shared& S, int lane, bool& empty_dist) {
 }
 
 // ---- segmented speculative decode of one round ------------------------------------------------
-// Lane j owns [s_j, e_j) (round-relative bits) and checkpoints C1_j = s_j + min(128, len) and
-// C2_j = s_j + min(1024, len).  A speculative run from a start records, per checkpoint, its first
+// Lane j owns [s_j, e_j) (round-relative bits) and checkpoints C1_j = s_j + min(XCP1, len) and
+// C2_j = s_j + min(XCP2, len) (64 and 1024 bits; round 4: XCP1 128 -> 64, count 11.1 -> 10.8 ms).  A speculative run from a start records, per checkpoint, its first
 // token boundary at or past it (offset from s_j) and the output bytes before it, plus its end
 // state.  Two decodes that stand on the same boundary at a checkpoint agree from there on, so a
 // verify run from the TRUE start only decodes up to the first checkpoint where it meets its own
@@ -677,7 +708,7 @@ __device__ int build_tables(Shared& S, int lane, bool& empty_dist) {
 // multiples of 8 resynchronise slowly or never from a wrong bit phase; when several lanes fail the
 // fallback adds runs from s_j+1 .. s_j+7 (one per phase) compared at C1.
 #ifndef NDFL_XCP1
-#define NDFL_XCP1 128
+#define NDFL_XCP1 64
 #endif
 // The fallback phases 1..7 are decoded only when more than this many lanes of a round failed to
 // synchronise (a sign of phase-locked codes); fewer, isolated failures are resolved by the fix-up
@@ -1308,7 +1339,18 @@ __device__ __forceinline__ void wr_copy(gu8* out, uint64_t dst, uint32_t len, ui
     gu8* d = out + NDFL_OA(dst);
     const gu8* sp = out + NDFL_OA(dst - dist);
     if (dist == 1) {
+        // a run: 16-byte stores (the last one overlapping back), so the wave's store loop takes
+        // at most 17 trips for the longest run instead of 65
         const uint32_t v4 = lastb * 0x01010101u;
+#if NDFL_EMIT_W16
+        if (len >= 16) {
+            const u32x4v x = {v4, v4, v4, v4};
+            uint32_t k = 0;
+            for (; k + 16 <= len; k += 16) *(gu128*)(d + k) = x;
+            if (k < len) *(gu128*)(d + len - 16) = x;
+            return;
+        }
+#endif
         if (len >= 4) {
             uint32_t k = 0;
             for (; k + 4 <= len; k += 4) *(gu32*)(d + k) = v4;
@@ -1607,7 +1649,8 @@ extern "C" __global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per
 ndfl_inflate_emit_wave_kernel(const uint32_t* w, uint64_t nwords, uint64_t nbits, const EmitChain* chains,
                               uint32_t nlist, uint32_t* ticket, uint8_t* out, ChainRes* res, const uint64_t* cands,
                               uint32_t ncand, uint32_t* ref, uint32_t* pend, SegPool pool, wv::PhArr* ph_all,
-                              uint32_t* stats, const uint64_t* info, const uint32_t* eorder) {
+                              uint32_t* stats, const uint64_t* info, const uint32_t* eorder,
+                              const uint32_t* dnlist) {
     using namespace wv;
     __shared__ __attribute__((aligned(16))) Shared S;
     __shared__ Stage stg;
@@ -1620,6 +1663,7 @@ ndfl_inflate_emit_wave_kernel(const uint32_t* w, uint64_t nwords, uint64_t nbits
         if (info[LI_FLAGS]) return;             // to emit when the host has to step in (uniform)
         nlist = (uint32_t)info[LI_NCH];
     }
+    if (dnlist) nlist = *dnlist;                // (the chains the fast emit pass left: eorder lists them)
     for (;;) {
     __syncthreads();
     if (lane == 0) s_ticket = atomicAdd(ticket, 1u);
@@ -1723,26 +1767,28 @@ ndfl_inflate_emit_wave_kernel(const uint32_t* w, uint64_t nwords, uint64_t nbits
             uint32_t end = (uint32_t)(r.end - g.base);
             uint32_t kind = r.kind, rsn = r.reason;
             const uint64_t dst0 = base + pre;
-            uint64_t n = 0;                 // bytes produced
+            uint32_t n = 0;                 // bytes produced
             Wr wr;
             wr_init(wr, dst0);
             uint64_t dfr = ~0ull;           // first deferred byte of this lane (absolute)
-            uint64_t lastsrc = 0;           // a byte holding the value of the last output byte
+            uint64_t lastsrc = 0;           // a byte holding the value of the last output byte, when !lsp
+            bool lsp = false;               //   (lsp: the byte just before dst0 + n)
             uint32_t lastb = 0;             // the last output byte, when it is final (lastok)
             bool lastok = false;
             bool active = live;
 #if NDFL_BITBUF
             Bb bb;
-            bool fast = active && pos + 48 < end;     // (pos only grows: once false, it stays false)
+            const uint32_t lim = min(end, nb - min(nb, 48u));
+            bool fast = active && pos < lim;           // (pos only grows: once false, it stays false)
             if (fast) bb_init(bb, v, pos);
 #endif
             while (active && pos < end) {
                 Tok tk;
 #if NDFL_BITBUF
                 if (fast) {
-                    tok_bb(bb, v, S.t, ed, tk);
+                    tok_bb<true>(bb, v, S.t, ed, tk, end);
                     pos = bb.pos;
-                    fast = pos + 48 < end;
+                    fast = pos < lim;
                 } else {
                     tok<true>(v, pos, S.t, ed, end, nb, tk);
                 }
@@ -1753,7 +1799,7 @@ ndfl_inflate_emit_wave_kernel(const uint32_t* w, uint64_t nwords, uint64_t nbits
                 if (tk.kind == K_LIT) {
                     wr_lit(wr, gout, tk.val, tk.n);
                     n += tk.n;
-                    lastsrc = dst0 + n - 1;
+                    lsp = true;
                     lastb = tk.val >> (tk.n == 2 ? 8 : 0);
                     lastok = true;
                     continue;
@@ -1782,11 +1828,11 @@ ndfl_inflate_emit_wave_kernel(const uint32_t* w, uint64_t nwords, uint64_t nbits
                 if (!defer) {
                     wr_copy(gout, dst, len, dist, lastb);           // sources final and our own
                     lastok = true;
-                    lastsrc = dst + len - 1;
+                    lsp = true;
                 } else {
                     // deferred: back-references (a dist-1 run points at the byte its value comes
                     // from), pending bits; the bytes are written by the resolve rounds
-                    const uint64_t anchor = dist == 1 ? (n > 0 ? lastsrc : src) : 0;
+                    const uint64_t anchor = dist == 1 ? (n > 0 ? (lsp ? dst - 1 : lastsrc) : src) : 0;
                     for (uint32_t k = 0; k < len; k++) {
                         const uint64_t back = dst + k - anchor;     // a run > 4 GiB falls back to its previous byte
                         ref[dst + k] = dist == 1 ? (back < (1ull << 32) ? (uint32_t)back : 1u) : dist;
@@ -1796,7 +1842,8 @@ ndfl_inflate_emit_wave_kernel(const uint32_t* w, uint64_t nwords, uint64_t nbits
                         const uint32_t m = (uint32_t)(((1ull << (hi - lo)) - 1) << (lo & 31));
                         atomicOr(&pend[q], m);
                     }
-                    if (dist == 1) lastsrc = anchor; else lastsrc = dst + len - 1;
+                    lastsrc = anchor;
+                    lsp = dist != 1;
                     dfr = min(dfr, dst);
                     lastok = false;                 // the copy's bytes are pending
                 }
@@ -1842,6 +1889,219 @@ ndfl_inflate_emit_wave_kernel(const uint32_t* w, uint64_t nwords, uint64_t nbits
         atomicMax(&st64[17], t_end);
         atomicMax(&st64[18], ~t_begin);
         atomicAdd(&st64[19], 1ull);
+    }
+}
+
+// Fast emit pass (the common case): a chain whose every Huffman block has the count pass's table
+// record and every round its segment record is replayed from those records alone (no header parse,
+// no table build, no round decode), so the kernel holds the registers of the record replay only:
+// 128 VGPRs, 11.0 KB of LDS (tables + the staged round), 14 waves per CU where the full emit kernel
+// holds 12 (measured: emit 8.81 -> 8.41 ms).  NDFL_EMITF_STAGE=0 reads the input through L1/L2
+// instead of the LDS stage (4 waves per SIMD; measured slower, 10.3 ms).  A chain that needs anything else (a block without a table record, a round without a
+// segment record, a stored block that is invalid or runs past the input) is listed in `slow` for the
+// full kernel, which runs it from its start: the output this kernel wrote for the chain so far is
+// rewritten there identically (the same records give the same segments, deferral decisions, bytes,
+// back-references and pending bits).
+#ifndef NDFL_EMITF_STAGE
+#define NDFL_EMITF_STAGE 1
+#endif
+#ifndef NDFL_EMITF_WAVES_PER_SIMD
+#define NDFL_EMITF_WAVES_PER_SIMD 4
+#endif
+extern "C" __global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(NDFL_EMITF_WAVES_PER_SIMD)))
+ndfl_inflate_emit_fast_kernel(const uint32_t* w, uint64_t nwords, uint64_t nbits, const EmitChain* chains,
+                              uint32_t* ticket, uint8_t* out, ChainRes* res, uint32_t* ref, uint32_t* pend,
+                              SegPool pool, const uint64_t* info, const uint32_t* eorder, uint32_t* slow,
+                              uint32_t* nslow) {
+    using namespace wv;
+    __shared__ __attribute__((aligned(16))) Tabs T;
+#if NDFL_EMITF_STAGE
+    __shared__ Stage stg;
+#endif
+    const int lane = threadIdx.x;
+    gu8* gout = (gu8*)out;
+    if (info[LI_FLAGS]) return;                 // (the host steps in: nothing to emit)
+    const uint32_t nlist = (uint32_t)info[LI_NCH];
+    const In in{w, nwords, nbits};
+    for (;;) {
+    uint32_t tk0 = 0;
+    if (lane == 0) tk0 = atomicAdd(ticket, 1u);
+    const uint32_t t = __builtin_amdgcn_readfirstlane(tk0);
+    if (t >= nlist) break;
+    const uint32_t ci = eorder[t];              // (costliest chains first)
+    const EmitChain ch = chains[ci];
+    uint64_t cur = ch.start_bit, base = ch.out_off;
+    uint32_t status = ST_BOUNDARY, reason = 0;
+    uint64_t endpos = ch.start_bit;
+    bool abort = false;
+    uint32_t rec = ch.slot < pool.nslot ? pool.head[ch.slot] : NOREC;
+    SegMeta pm = {};
+    uint64_t pst = 0;
+    uint32_t pcn = 0;
+    if (rec != NOREC) { pm = pool.meta[rec]; pst = pool.start[(uint64_t)rec * 64 + lane]; pcn = pool.cnt[(uint64_t)rec * 64 + lane]; }
+    uint64_t bnd_bit = cur, bnd_out = base;
+    for (int blk = 0;; blk++) {
+        if (blk > 0 && cur == ch.end_bit) { status = ST_BOUNDARY; endpos = cur; break; }
+        bnd_bit = cur; bnd_out = base;
+        if (cur + 3 > nbits) { abort = true; break; }
+        const uint32_t hb = (uint32_t)(in.win64(cur)) & 7u;
+        if ((hb >> 1) == 0) {                   // stored block (D/decomp/Open.java:286-310)
+            const uint64_t hp = (cur + 3 + 7) & ~7ull;
+            if (hp + 32 > nbits) { abort = true; break; }
+            const uint32_t lw = (uint32_t)in.win64(hp);
+            if ((lw >> 16) != (~lw & 0xFFFFu)) { abort = true; break; }
+            const uint64_t ln = lw & 0xFFFFu, d0 = hp + 32;
+            if (d0 + 8 * ln > nbits) { abort = true; break; }
+            const uint64_t ib = d0 >> 3;
+            for (uint64_t i = (uint64_t)lane; i < ln; i += 64) {
+                const uint64_t b = ib + i;
+                out[base + i] = (uint8_t)(in.ld(b >> 2) >> (8 * (uint32_t)(b & 3)));
+            }
+            base += ln;
+            cur = d0 + 8 * ln;
+            if (hb & 1) { status = ST_FINAL; endpos = cur; break; }
+            continue;
+        }
+        const char* btr = (rec != NOREC && pm.pad < pool.nbt) ? pool.bt + (uint64_t)pm.pad * BT_BYTES : nullptr;
+        if (!btr || *(const uint64_t*)(btr + sizeof(Tabs)) != cur) { abort = true; break; }
+        __syncthreads();                        // the previous block's table reads are done
+        {
+            const uint4* src = (const uint4*)btr;
+            uint4* dst = (uint4*)&T;
+            for (uint32_t q = (uint32_t)lane; q < sizeof(Tabs) / 16; q += 64) dst[q] = src[q];
+        }
+        const uint64_t* h = (const uint64_t*)(btr + sizeof(Tabs));
+        const uint32_t* h32 = (const uint32_t*)(h + 2);
+        const bool bfinal = h32[0] != 0, ed = h32[2] != 0;
+        __syncthreads();
+        bool block_done = false, chain_done = false;
+        while (!block_done) {
+            if (rec == NOREC) { abort = true; chain_done = true; break; }
+            const SegMeta m = pm;
+            const uint32_t ft = m.ft;
+            const uint64_t rstart = pst;
+            const uint32_t rcnt = pcn;
+            rec = m.next;
+            if (rec != NOREC) { pm = pool.meta[rec]; pst = pool.start[(uint64_t)rec * 64 + lane]; pcn = pool.cnt[(uint64_t)rec * 64 + lane]; }
+            const uint64_t nx = __shfl_down((unsigned long long)rstart, 1, 64);
+            uint64_t rend = lane < 63 ? nx : m.exit63;
+            uint32_t kind = T_EXIT, rsn = 0;
+            if ((uint32_t)lane == ft) { rend = m.end_ft; kind = m.kind_ft; rsn = m.reason_ft; }
+            const Geo g = make_geo(in, m.rs, m.rs + 1, m.pw);      // the count pass's geometry
+            const bool live = (uint32_t)lane <= ft;
+            const uint64_t mycnt = live ? rcnt : 0ull;
+            const uint64_t pre = wave_excl_u64(mycnt, lane);
+            const uint64_t rsum = wave_sum_u64(mycnt);
+#if NDFL_EMITF_STAGE
+            stage_round(in, g, stg, lane);
+            const Lv v = make_lv(stg, g, lane);
+#else
+            Gv v;
+            v.rw = (uint32_t)lane * g.pw;
+            v.q = w + (g.base >> 5) + v.rw;
+#endif
+            const uint32_t nb = g.nb;
+            uint32_t pos = (uint32_t)(rstart - g.base);
+            uint32_t end = (uint32_t)(rend - g.base);
+            const uint64_t dst0 = base + pre;
+            uint32_t n = 0;
+            Wr wr;
+            wr_init(wr, dst0);
+            uint64_t dfr = ~0ull, lastsrc = 0;     // (lastsrc when !lsp; lsp: the byte before dst0 + n)
+            bool lsp = false;
+            uint32_t lastb = 0;
+            bool lastok = false;
+            Bb bb;
+            const uint32_t lim = min(end, nb - min(nb, 48u));
+            bool fast = live && pos < lim;
+            if (fast) bb_init(bb, v, pos);
+            while (live && pos < end) {
+                Tok tk;
+                if (fast) {
+                    tok_bb<true>(bb, v, T, ed, tk, end);
+                    pos = bb.pos;
+                    fast = pos < lim;
+                } else {
+                    tok<true>(v, pos, T, ed, end, nb, tk);
+                }
+                if (tk.kind == K_LIT) {
+                    wr_lit(wr, gout, tk.val, tk.n);
+                    n += tk.n;
+                    lsp = true;
+                    lastb = tk.val >> (tk.n == 2 ? 8 : 0);
+                    lastok = true;
+                    continue;
+                }
+                if (tk.kind != K_LEN) break;
+                const uint64_t dst = dst0 + n;
+                if ((uint64_t)tk.dist > dst) { kind = T_ERR; rsn = R_COPY_BEFORE; end = pos; break; }
+                const uint32_t len = tk.n, dist = tk.dist;
+                const uint64_t src = dst - dist;
+                const uint64_t src_end = src + min(len, dist);
+                bool defer = src < dst0;
+                if (!defer && src_end > dfr) {
+                    for (uint64_t q = src >> 5; q <= (src_end - 1) >> 5 && !defer; q++) {
+                        const uint64_t lo = max(src, q << 5), hi = min(src_end, (q + 1) << 5);
+                        const uint32_t mk = (uint32_t)(((1ull << (hi - lo)) - 1) << (lo & 31));
+                        defer = (__hip_atomic_load(&pend[q], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) & mk) != 0;
+                    }
+                }
+                wr_flush_word(wr, gout);
+                if (!defer && dist == 1 && !lastok) lastb = gout[dst - 1];
+                if (!defer) {
+                    wr_copy(gout, dst, len, dist, lastb);
+                    lastok = true;
+                    lsp = true;
+                } else {
+                    const uint64_t anchor = dist == 1 ? (n > 0 ? (lsp ? dst - 1 : lastsrc) : src) : 0;
+                    for (uint32_t k = 0; k < len; k++) {
+                        const uint64_t back = dst + k - anchor;
+                        ref[dst + k] = dist == 1 ? (back < (1ull << 32) ? (uint32_t)back : 1u) : dist;
+                    }
+                    for (uint64_t q = dst >> 5; q <= (dst + len - 1) >> 5; q++) {
+                        const uint64_t lo = max(dst, q << 5), hi = min(dst + len, (q + 1) << 5);
+                        const uint32_t mk = (uint32_t)(((1ull << (hi - lo)) - 1) << (lo & 31));
+                        atomicOr(&pend[q], mk);
+                    }
+                    lastsrc = anchor;
+                    lsp = dist != 1;
+                    dfr = min(dfr, dst);
+                    lastok = false;
+                }
+                n += len;
+                wr.dst = dst0 + n;
+            }
+            wr_flush_exact(wr, gout);
+            const uint64_t em = __ballot(live && kind == T_ERR);
+            if (em) {
+                const int fl = (int)__builtin_ctzll(em);
+                status = ST_ERROR;
+                reason = __shfl(rsn, fl, 64);
+                endpos = g.base + __shfl(end, fl, 64);
+                base = __shfl((unsigned long long)(dst0 + n), fl, 64);
+                chain_done = true;
+                break;
+            }
+            base += rsum;
+            if (ft < 64) {
+                block_done = true;
+                cur = __shfl((unsigned long long)rend, (int)ft, 64);
+                if (bfinal) { status = ST_FINAL; endpos = cur; chain_done = true; }
+            }
+        }
+        if (chain_done) break;
+    }
+    if (lane == 0) {
+        if (abort) {
+            slow[atomicAdd(nslow, 1u)] = ci;
+        } else {
+            ChainRes o;
+            o.end_bit = endpos; o.out_count = base - ch.out_off; o.status = status; o.reason = reason;
+            o.next = 0xFFFFFFFFu; o.pad = 0;
+            o.bnd_bit = bnd_bit; o.bnd_cnt = bnd_out - ch.out_off;
+            res[ci] = o;
+        }
+    }
     }
 }
 

@@ -1,0 +1,110 @@
+"""Record-replay fast emit pass (inflate_wave.hpp ndfl_inflate_emit_fast_kernel) and its hand-over
+to the full emit kernel: the decode must equal the oracle's -- output, consumed bits, Reason of the
+first error -- with the fast pass on (the default), off (NDFL_EMIT_FAST=0: the full kernel alone),
+and with no table records (NDFL_NO_BT=1: every chain reaching a Huffman block is listed for the full
+kernel, which runs it from its start again -- stored blocks the fast pass already wrote before the
+hand-over are rewritten identically).  Streams: the config-4 mix (RLE_DYNAMIC), zlib -6 text (LZ77
+distances, deferred copies across lanes and chains), zlib Z_FIXED text, the config-2 layout (stored
+and fixed-Huffman pieces alternating), stored blocks alone, the reference's 39 known-answer tests and
+corrupted streams.  Reference semantics: D/decomp/Open.java:83-618."""
+import os
+import random
+import zlib
+
+import numpy as np
+import pytest
+
+import corpus
+import oracle_lib as O
+from test_oracle_inflate import KAT
+
+pytestmark = pytest.mark.gpu
+
+
+@pytest.fixture(scope="module")
+def ctx():
+    import ndfl
+    return ndfl.Context(0)
+
+
+def _env(name, value):
+    old = os.environ.get(name)
+    if value is None:
+        os.environ.pop(name, None)
+    else:
+        os.environ[name] = str(value)
+    return old
+
+
+MODES = {"fast": {}, "full_only": {"NDFL_EMIT_FAST": "0"}, "hand_over": {"NDFL_NO_BT": "1"}}
+
+
+@pytest.fixture(params=list(MODES))
+def mode(request):
+    olds = {k: _env(k, v) for k, v in MODES[request.param].items()}
+    yield request.param
+    for k, v in olds.items():
+        _env(k, v)
+
+
+def _zraw(data, level, strategy=zlib.Z_DEFAULT_STRATEGY):
+    co = zlib.compressobj(level, zlib.DEFLATED, -15, 9, strategy)
+    return co.compress(data) + co.flush()
+
+
+STREAMS = {}
+
+
+def _streams():
+    if not STREAMS:
+        c4 = corpus.c4_mixed(4 << 20, seed=0x4F).numpy().tobytes()
+        text = corpus.c3_text(2 << 20).numpy().tobytes()
+        rng = np.random.default_rng(22)
+        rnd = rng.integers(0, 256, 300_000, dtype=np.uint8).tobytes()
+        _, c2raw, _ = corpus.c2_gzip(3 << 20, seed=0xC7)
+        STREAMS.update({
+            "rle_c4": O.deflate(c4),
+            "zlib6_text": _zraw(text, 6),
+            "zlib_fixed_text": _zraw(text, 6, zlib.Z_FIXED),
+            "c2_layout": c2raw,
+            "stored": _zraw(rnd, 0),
+        })
+    return STREAMS
+
+
+def _same(ctx, comp):
+    r, out, bits = ctx.inflate(comp)
+    oreason, oout, obits = O.inflate(comp)
+    assert (None if r is None else r.name) == oreason
+    assert out == oout
+    if oreason is None:
+        assert bits == obits
+
+
+@pytest.mark.parametrize("name", ["rle_c4", "zlib6_text", "zlib_fixed_text", "c2_layout", "stored"])
+def test_emit_modes_match_oracle(ctx, mode, name):
+    _same(ctx, _streams()[name])
+
+
+def test_emit_modes_known_answers(ctx, mode):
+    for kat in KAT:
+        rng = random.Random(kat["line"])
+        for pad in range(3):
+            data = O.bits_to_bytes(kat["bits"], pad, rng)
+            r, out, bits = ctx.inflate(data)
+            if kat["expect_reason"] is None:
+                assert r is None and out == bytes.fromhex(kat["expect_hex"]), kat["name"]
+                assert (bits + 7) // 8 == len(data)
+            else:
+                assert r is not None and r.name == kat["expect_reason"], kat["name"]
+
+
+@pytest.mark.parametrize("name", ["rle_c4", "c2_layout"])
+def test_emit_modes_first_error(ctx, mode, name):
+    comp = _streams()[name]
+    rng = np.random.default_rng(len(mode))
+    for _ in range(4):
+        bad = bytearray(comp)
+        k = int(rng.integers(len(bad) // 8, len(bad)))
+        bad[k] ^= 0x5A
+        _same(ctx, bytes(bad))
