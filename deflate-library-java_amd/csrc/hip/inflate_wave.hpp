@@ -47,6 +47,16 @@ struct Tabs {
     uint32_t dx[DX];
 };
 
+// The same tables split over two memories (the fast emit pass): the primary tables in LDS, the
+// extension areas -- read only for codes longer than the primary -- in the count pass's table
+// record in global memory.
+struct TabsG {
+    const uint32_t* lit;
+    const uint32_t* dst;
+    const uint32_t* lx;
+    const uint32_t* dx;
+};
+
 struct Shared {
     Tabs t;
     uint8_t lens[320];                       // literal/length 0..287, distance at 288..319
@@ -98,19 +108,23 @@ __device__ __forceinline__ uint32_t slow_entry(uint32_t p15, const uint32_t* lim
     const uint32_t idx = (c >> (15 - l)) - first[l];
     return ent[off[l] + idx];
 }
-__device__ __forceinline__ uint32_t slow_lit(uint32_t p15, const Tabs& t) {
+template <class TT>
+__device__ __forceinline__ uint32_t slow_lit(uint32_t p15, const TT& t) {
     return slow_entry<LB>(p15, t.lx + 288, (const uint16_t*)(t.lx + 304), (const uint16_t*)(t.lx + 312), t.lx);
 }
-__device__ __forceinline__ uint32_t slow_dist(uint32_t p15, const Tabs& t) {
+template <class TT>
+__device__ __forceinline__ uint32_t slow_dist(uint32_t p15, const TT& t) {
     return slow_entry<DB>(p15, t.dx + 32, (const uint16_t*)(t.dx + 48), (const uint16_t*)(t.dx + 56), t.dx);
 }
 // entry of a code longer than the primary (e: its primary entry; bits: the window from the code's start)
-__device__ __forceinline__ uint32_t long_lit(uint32_t e, uint32_t bits, const Tabs& t) {
+template <class TT>
+__device__ __forceinline__ uint32_t long_lit(uint32_t e, uint32_t bits, const TT& t) {
     const uint32_t sd = (e >> 5) & 15;
     if (sd) return t.lx[(e >> 16) + ((bits >> LB) & ((1u << sd) - 1u))];
     return slow_lit(bits & 0x7FFFu, t);
 }
-__device__ __forceinline__ uint32_t long_dist(uint32_t d, uint32_t bits, const Tabs& t) {
+template <class TT>
+__device__ __forceinline__ uint32_t long_dist(uint32_t d, uint32_t bits, const TT& t) {
     const uint32_t sd = (d >> 5) & 15;
     if (sd) return t.dx[(d >> 16) + ((bits >> DB) & ((1u << sd) - 1u))];
     return slow_dist(bits & 0x7FFFu, t);
@@ -228,11 +242,11 @@ __device__ __forceinline__ Lv make_lv(const Stage& st, const Geo& g, int lane) {
 // stands on the first token boundary at or past each stop, whatever its grouping before it.
 // CAREFUL = false: the caller guarantees pos + 48 < stop <= nb (no token can reach the stop or the
 // input end), so those checks are dropped.
-template <bool CAREFUL>
-__device__ __forceinline__ void tok_e(uint32_t lo, uint32_t hi, uint32_t e, uint32_t& pos, const Tabs& t,
+template <bool CAREFUL, class TT>
+__device__ __forceinline__ void tok_e(uint32_t lo, uint32_t hi, uint32_t e, uint32_t& pos, const TT& t,
                                       bool empty_dist, uint32_t stop, uint32_t nb, Tok& tk);
-template <bool CAREFUL, class V>
-__device__ __forceinline__ void tok(const V& v, uint32_t& pos, const Tabs& t, bool empty_dist, uint32_t stop,
+template <bool CAREFUL, class V, class TT>
+__device__ __forceinline__ void tok(const V& v, uint32_t& pos, const TT& t, bool empty_dist, uint32_t stop,
                                     uint32_t nb, Tok& tk) {
     // (the result goes through scalars and is stored into tk once: stores of different fields on
     // different paths made the compiler keep tk in scratch memory)
@@ -241,8 +255,8 @@ __device__ __forceinline__ void tok(const V& v, uint32_t& pos, const Tabs& t, bo
     tok_e<CAREFUL>(lo, hi, t.lit[lo & ((1u << LB) - 1u)], pos, t, empty_dist, stop, nb, tk);
 }
 // the rest of a token step once its window (lo, hi) and primary entry e are loaded
-template <bool CAREFUL>
-__device__ __forceinline__ void tok_e(uint32_t lo, uint32_t hi, uint32_t e, uint32_t& pos, const Tabs& t,
+template <bool CAREFUL, class TT>
+__device__ __forceinline__ void tok_e(uint32_t lo, uint32_t hi, uint32_t e, uint32_t& pos, const TT& t,
                                       bool empty_dist, uint32_t stop, uint32_t nb, Tok& tk) {
     uint32_t kind, val, n = 1, dist = 0;
     do {
@@ -332,8 +346,8 @@ __device__ __forceinline__ void bb_skip(Bb& b, uint32_t n) {
 // end, so none of its checks are needed).  STOP = false: also pos + 48 < stop (tok<false>);
 // STOP = true: any pos < stop -- a literal pair whose first literal reaches `stop` is split, as in
 // tok<true>, so the buffer carries a decode right up to a checkpoint or the segment end.
-template <bool STOP = false, class V>
-__device__ __forceinline__ void tok_bb(Bb& b, const V& v, const Tabs& t, bool empty_dist, Tok& tk, uint32_t stop = 0) {
+template <bool STOP = false, class V, class TT>
+__device__ __forceinline__ void tok_bb(Bb& b, const V& v, const TT& t, bool empty_dist, Tok& tk, uint32_t stop = 0) {
     uint32_t lo = (uint32_t)b.buf;
     uint32_t e = t.lit[lo & ((1u << LB) - 1u)];
     uint32_t kind, val, n = 1, dist = 0;
@@ -1905,6 +1919,9 @@ ndfl_inflate_emit_wave_kernel(const uint32_t* w, uint64_t nwords, uint64_t nbits
 #ifndef NDFL_EMITF_STAGE
 #define NDFL_EMITF_STAGE 1
 #endif
+#ifndef NDFL_EMITF_GX
+#define NDFL_EMITF_GX 1         // primary tables in LDS, extension areas read from the table record
+#endif
 #ifndef NDFL_EMITF_WAVES_PER_SIMD
 #define NDFL_EMITF_WAVES_PER_SIMD 4
 #endif
@@ -1914,7 +1931,14 @@ ndfl_inflate_emit_fast_kernel(const uint32_t* w, uint64_t nwords, uint64_t nbits
                               SegPool pool, const uint64_t* info, const uint32_t* eorder, uint32_t* slow,
                               uint32_t* nslow) {
     using namespace wv;
+#if NDFL_EMITF_GX
+    __shared__ __attribute__((aligned(16))) uint32_t Tp[(1u << LB) + (1u << DB)];     // primary tables
+    TabsG T;
+    T.lit = Tp;
+    T.dst = Tp + (1u << LB);
+#else
     __shared__ __attribute__((aligned(16))) Tabs T;
+#endif
 #if NDFL_EMITF_STAGE
     __shared__ Stage stg;
 #endif
@@ -1967,8 +1991,15 @@ ndfl_inflate_emit_fast_kernel(const uint32_t* w, uint64_t nwords, uint64_t nbits
         __syncthreads();                        // the previous block's table reads are done
         {
             const uint4* src = (const uint4*)btr;
+#if NDFL_EMITF_GX
+            uint4* dst = (uint4*)Tp;
+            for (uint32_t q = (uint32_t)lane; q < sizeof(Tp) / 16; q += 64) dst[q] = src[q];
+            T.lx = (const uint32_t*)btr + offsetof(Tabs, lx) / 4;
+            T.dx = (const uint32_t*)btr + offsetof(Tabs, dx) / 4;
+#else
             uint4* dst = (uint4*)&T;
             for (uint32_t q = (uint32_t)lane; q < sizeof(Tabs) / 16; q += 64) dst[q] = src[q];
+#endif
         }
         const uint64_t* h = (const uint64_t*)(btr + sizeof(Tabs));
         const uint32_t* h32 = (const uint32_t*)(h + 2);
