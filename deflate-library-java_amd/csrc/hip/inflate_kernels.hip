@@ -1013,24 +1013,58 @@ ndfl_inflate_cand_slice_kernel(const uint64_t* sorted, uint64_t* info, uint64_t 
         cands[1 + k] = sorted[lo + k];
 }
 
+// Stored-header aliases: a stored block's header can be read at up to 8 bit positions before its
+// byte-aligned LEN (the padding between the 3 header bits and the byte boundary is not checked, so
+// a header with zero bits before it is also found one, two, ... bits earlier).  Candidates with the
+// same BFINAL bit and the same LEN position decode identically from there on, so the count pass
+// counts one of them (the first) and the others take its result (ndfl_inflate_alias_copy_kernel).
+// Config 2's sync-flush empty stored blocks have ~6 aliases each, each of which otherwise counts
+// the whole next piece again.
+__device__ __forceinline__ uint64_t stored_key(const inf::In& in, uint64_t p) {
+    const uint32_t h = (uint32_t)in.win64(p) & 7u;
+    if ((h >> 1) != 0 || p + 3 > in.nbits) return ~0ull;                 // (not a stored header)
+    return (((p + 3 + 7) & ~7ull) << 1) | (h & 1u);
+}
+
 // Claim order of the count pass: longest first by the bits to the next start (24 buckets of 32
-// Kibit), so that no long chain is left for the end of the launch.  One workgroup.
+// Kibit), so that no long chain is left for the end of the launch.  One workgroup.  With `rep`,
+// stored-header aliases are left out of the order (rep[k] = the candidate counted for k; *nord = the
+// chains to count).
 extern "C" __global__ void __launch_bounds__(1024)
-ndfl_inflate_order_kernel(const uint64_t* cands, uint32_t n, uint64_t end_bit, uint32_t* order) {
+ndfl_inflate_order_kernel(const uint64_t* cands, uint32_t n, uint64_t end_bit, uint32_t* order, const uint32_t* w,
+                          uint64_t nwords, uint64_t nbits, uint32_t* rep, uint32_t* nord) {
     constexpr uint32_t NB = 24;
     __shared__ uint32_t bc[NB + 1];
     if (threadIdx.x <= NB) bc[threadIdx.x] = 0;
     __syncthreads();
+    const inf::In in{w, nwords, nbits};
     auto bucket = [&](uint32_t k) -> uint32_t {
         const uint64_t nx = k + 1 < n ? cands[k + 1] : end_bit;
         const uint64_t len = nx > cands[k] ? nx - cands[k] : 0;
         return NB - 1 - (uint32_t)min<uint64_t>(NB - 1, len >> 15);
     };
-    for (uint32_t k = threadIdx.x; k < n; k += blockDim.x) atomicAdd(&bc[bucket(k) + 1], 1u);
+    auto alias_of = [&](uint32_t k) -> uint32_t {
+        if (!rep) return k;
+        const uint64_t p = cands[k], key = stored_key(in, p);
+        uint32_t r = k;
+        if (key != ~0ull)
+            for (uint32_t j = k; j > 0 && cands[j - 1] + 10 >= p; j--)
+                if (stored_key(in, cands[j - 1]) == key) r = j - 1;
+        return r;
+    };
+    for (uint32_t k = threadIdx.x; k < n; k += blockDim.x) {
+        const uint32_t r = alias_of(k);
+        if (rep) rep[k] = r;
+        if (r == k) atomicAdd(&bc[bucket(k) + 1], 1u);
+    }
     __syncthreads();
-    if (threadIdx.x == 0) for (uint32_t b = 0; b < NB; b++) bc[b + 1] += bc[b];
+    if (threadIdx.x == 0) {
+        for (uint32_t b = 0; b < NB; b++) bc[b + 1] += bc[b];
+        if (nord) *nord = bc[NB];
+    }
     __syncthreads();
-    for (uint32_t k = threadIdx.x; k < n; k += blockDim.x) order[atomicAdd(&bc[bucket(k)], 1u)] = k;
+    for (uint32_t k = threadIdx.x; k < n; k += blockDim.x)
+        if (!rep || rep[k] == k) order[atomicAdd(&bc[bucket(k)], 1u)] = k;
 }
 
 // The emit pass's claim order over the linked chain list (info[LI_NCH] chains): costliest first, by
@@ -1177,6 +1211,17 @@ constexpr uint32_t BT_BYTES = 6720;   // wv::Tabs (6656) + hdr bit, data bit (u6
 #include "inflate_wave.hpp"
 #include "inflate_wg.hpp"
 
+// Aliases take the result (and the segment records) of the candidate counted for them.
+extern "C" __global__ void __launch_bounds__(256)
+ndfl_inflate_alias_copy_kernel(const uint32_t* rep, uint32_t n, ChainRes* res, SegPool pool) {
+    for (uint32_t k = blockIdx.x * 256 + threadIdx.x; k < n; k += gridDim.x * 256) {
+        const uint32_t r = rep[k];
+        if (r == k) continue;
+        res[k] = res[r];
+        if (k < pool.nslot) pool.head[k] = r < pool.nslot ? pool.head[r] : NOREC;
+    }
+}
+
 // ---- host orchestration ---------------------------------------------------------------------
 
 struct InflateScratch {
@@ -1197,6 +1242,7 @@ struct InflateScratch {
     void* d_rl = nullptr; size_t d_rl_cap = 0;        // resolve: two group lists + round bits
     void* d_ticket = nullptr;
     void* d_slow = nullptr; size_t d_slow_cap = 0;    // emit: chains the fast emit pass leaves to the full one
+    void* d_rep = nullptr; size_t d_rep_cap = 0;      // count: the candidate counted for each (stored-header aliases)
     void* d_ph = nullptr;                             // count pass: phase-fallback slot per wave
     void* d_hrec = nullptr;                           // count pass: header records, one per candidate
     size_t d_hrec_cap = 0;
@@ -1218,7 +1264,7 @@ struct InflateScratch {
     uint64_t p_nbytes = 0;
     void release() {
         void** ps[] = {&d_in, &d_cand, &d_starts, &d_stops, &d_res, &d_cands, &d_stats, &d_q, &d_seg, &d_chains, &d_off,
-                       &d_ref, &d_pend, &d_rl, &d_ticket, &d_ph, &d_cticket, &d_out, &d_done, &d_hrec, &d_slow};
+                       &d_ref, &d_pend, &d_rl, &d_ticket, &d_ph, &d_cticket, &d_out, &d_done, &d_hrec, &d_slow, &d_rep};
         for (void** p : ps) { if (*p) hipFree(*p); *p = nullptr; }
         for (auto& e : ev) { if (e) hipEventDestroy(e); e = nullptr; }
         if (h_cnt) hipHostFree(h_cnt);
@@ -1453,12 +1499,20 @@ static int inflate_devlink(InflateScratch& S, hipStream_t s, const uint32_t* d_w
     INF_CHK(inf_ensure(&S.d_stops, &S.d_stops_cap, n * 12));
     INF_CHK(inf_ensure(&S.d_res, &S.d_res_cap, n * sizeof(ChainRes)));
     uint32_t* d_order = (uint32_t*)((char*)S.d_stops + n * 8);
-    hipLaunchKernelGGL(ndfl_inflate_order_kernel, dim3(1), dim3(1024), 0, s, (const uint64_t*)S.d_cands, ncand, end_bit,
-                       d_order);
-    INF_CHK(hipGetLastError());
-    if (!S.d_ph) INF_CHK(hipMalloc(&S.d_ph, (size_t)std::max(COUNT_WAVES, EMIT_WAVES) * sizeof(wv::PhArr)));
     if (!S.d_cticket) INF_CHK(hipMalloc(&S.d_cticket, 64));
     INF_CHK(hipMemsetAsync(S.d_cticket, 0, 4, s));
+    // stored-header aliases counted once (NDFL_NO_ALIAS: every candidate counted)
+    const bool alias_on = !getenv("NDFL_NO_ALIAS");
+    uint32_t* d_rep = nullptr;
+    uint32_t* d_nord = (uint32_t*)S.d_cticket + 8;
+    if (alias_on) {
+        INF_CHK(inf_ensure(&S.d_rep, &S.d_rep_cap, (size_t)ncand * 4 + 64));
+        d_rep = (uint32_t*)S.d_rep;
+    }
+    hipLaunchKernelGGL(ndfl_inflate_order_kernel, dim3(1), dim3(1024), 0, s, (const uint64_t*)S.d_cands, ncand, end_bit,
+                       d_order, d_w, nwords, nbits, d_rep, alias_on ? d_nord : (uint32_t*)nullptr);
+    INF_CHK(hipGetLastError());
+    if (!S.d_ph) INF_CHK(hipMalloc(&S.d_ph, (size_t)std::max(COUNT_WAVES, EMIT_WAVES) * sizeof(wv::PhArr)));
     static const bool stats_on = getenv("NDFL_STATS") != nullptr;
     const uint64_t limit = std::min(end_bit, nbits);
     INF_CHK(hipEventRecord(S.ev[2], s));
@@ -1474,9 +1528,30 @@ static int inflate_devlink(InflateScratch& S, hipStream_t s, const uint32_t* d_w
                        (const uint64_t*)S.d_cands, ncand, limit, (ChainRes*)S.d_res,
                        stats_on ? (uint32_t*)S.d_stats : nullptr, (uint64_t)0, S.pool, (uint32_t*)S.d_cticket,
                        (wv::PhArr*)S.d_ph, (const uint32_t*)d_order, end_bit,
-                       hrec_on ? (const wv::HdrRec*)S.d_hrec : nullptr);
+                       hrec_on ? (const wv::HdrRec*)S.d_hrec : nullptr, alias_on ? (const uint32_t*)d_nord : nullptr);
     INF_CHK(hipGetLastError());
+    if (alias_on) {
+        hipLaunchKernelGGL(ndfl_inflate_alias_copy_kernel, dim3(std::min<uint32_t>(1024, (ncand + 255) / 256)), dim3(256), 0, s,
+                           (const uint32_t*)d_rep, ncand, (ChainRes*)S.d_res, S.pool);
+        INF_CHK(hipGetLastError());
+    }
     INF_CHK(hipEventRecord(S.ev[3], s));
+    if (stats_on) {                             // the count pass's chains by outcome (wave time in 10 us units)
+        std::vector<ChainRes> cr(ncand);
+        INF_CHK(hipMemcpyAsync(cr.data(), S.d_res, ncand * sizeof(ChainRes), hipMemcpyDeviceToHost, s));
+        INF_CHK(hipStreamSynchronize(s));
+        uint64_t cnt[3] = {0, 0, 0}, tsum[3] = {0, 0, 0}, tmax[3] = {0, 0, 0}, blk[3] = {0, 0, 0}, bits[3] = {0, 0, 0};
+        for (uint32_t k = 0; k < ncand; k++) {
+            const uint32_t st = std::min<uint32_t>(cr[k].status, 2u), t = cr[k].pad >> 16;
+            cnt[st]++; tsum[st] += t; tmax[st] = std::max<uint64_t>(tmax[st], t); blk[st] += cr[k].pad & 0xFFFFu;
+            bits[st] += cr[k].end_bit - std::min(cr[k].end_bit, (uint64_t)0) ;
+        }
+        const char* nm[3] = {"boundary", "final", "error"};
+        for (int k = 0; k < 3; k++)
+            fprintf(stderr, "[ndfl] count chains %s: %llu, wave time %.2f ms (max %.3f ms), blocks %llu\n", nm[k],
+                    (unsigned long long)cnt[k], tsum[k] * 1e-2, tmax[k] * 1e-2, (unsigned long long)blk[k]);
+        (void)bits;
+    }
     // linking: J levels (u32), S and D double-buffered
     uint32_t nlev = 1;
     while ((1ull << nlev) < n) nlev++;
@@ -1575,6 +1650,17 @@ static int inflate_devlink(InflateScratch& S, hipStream_t s, const uint32_t* d_w
     }
     INF_CHK(hipMemcpyAsync((void*)hinfo, info, LI_WORDS * 8, hipMemcpyDeviceToHost, s));
     INF_CHK(hipStreamSynchronize(s));                          // (2) the summary
+    if (stats_on) {
+        uint32_t st[64] = {0};
+        INF_CHK(hipMemcpy(st, S.d_stats, 256, hipMemcpyDeviceToHost));
+        const uint64_t* t64 = (const uint64_t*)(st + 32);
+        fprintf(stderr, "[ndfl] device link: chains %llu of %u candidates; count pass: slow-verify lanes %u fixups %u "
+                "rounds %u\n", (unsigned long long)hinfo[LI_NCH], ncand, st[0], st[1], st[2]);
+        const double span = (double)(t64[9] - ~t64[10]);
+        fprintf(stderr, "[ndfl] count waves %llu: busy %.1f ms x waves, span %.3f ms, occupancy %.3f, longest chain %.3f ms\n",
+                (unsigned long long)t64[11], t64[8] * 1e-5, span * 1e-5, t64[11] ? t64[8] / (span * t64[11]) : 0.0,
+                t64[12] * 1e-5);
+    }
     const uint64_t lflags = hinfo[LI_FLAGS];
     if (lflags & LF_REPAIR) return LINK_FALLBACK;
     if (lflags & LF_RANGE) return -1;                          // the range end is no block boundary
@@ -1847,7 +1933,7 @@ static int inflate_run(InflateScratch& S, hipStream_t s, const uint8_t* in, uint
                            (const uint64_t*)S.d_starts, (const uint64_t*)S.d_stops, (uint32_t)n,
                            (const uint64_t*)S.d_cands, ncand, limit, (ChainRes*)S.d_res, stats_on ? (uint32_t*)S.d_stats : nullptr,
                            slot_base, pool, (uint32_t*)S.d_cticket, (wv::PhArr*)S.d_ph, (const uint32_t*)d_order,
-                           end_bit, (const wv::HdrRec*)nullptr);
+                           end_bit, (const wv::HdrRec*)nullptr, (const uint32_t*)nullptr);
         INF_CHK(hipGetLastError());
         if (S.count_first) { INF_CHK(hipEventRecord(S.ev[3], s)); S.count_first = false; }
         r.resize(n);

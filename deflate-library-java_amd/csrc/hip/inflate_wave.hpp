@@ -1446,9 +1446,10 @@ ndfl_inflate_count_wave_kernel(const uint32_t* w, uint64_t nwords, uint64_t nbit
                                const uint64_t* stops, uint32_t nchains, const uint64_t* cands, uint32_t ncand,
                                uint64_t limit, ChainRes* res, uint32_t* stats, uint64_t slot_base, SegPool pool,
                                uint32_t* ticket, wv::PhArr* ph_all, const uint32_t* order, uint64_t stop_all,
-                               const wv::HdrRec* hrec) {
+                               const wv::HdrRec* hrec, const uint32_t* nord) {
     using namespace wv;
     __shared__ __attribute__((aligned(16))) Shared S;
+    if (nord) nchains = *nord;                  // (stored-header aliases left out of the order)
     __shared__ Stage stg;
     __shared__ uint32_t s_ticket;
     const int lane = threadIdx.x;

@@ -1,9 +1,11 @@
 """Record-replay fast emit pass (inflate_wave.hpp ndfl_inflate_emit_fast_kernel) and its hand-over
 to the full emit kernel: the decode must equal the oracle's -- output, consumed bits, Reason of the
 first error -- with the fast pass on (the default), off (NDFL_EMIT_FAST=0: the full kernel alone),
-and with no table records (NDFL_NO_BT=1: every chain reaching a Huffman block is listed for the full
+with no table records (NDFL_NO_BT=1: every chain reaching a Huffman block is listed for the full
 kernel, which runs it from its start again -- stored blocks the fast pass already wrote before the
-hand-over are rewritten identically).  Streams: the config-4 mix (RLE_DYNAMIC), zlib -6 text (LZ77
+hand-over are rewritten identically), and with every stored-header alias counted on its own
+(NDFL_NO_ALIAS=1; by default the count pass counts one of the candidates that share a stored
+block's LEN position and BFINAL bit and copies its result and records to the others).  Streams: the config-4 mix (RLE_DYNAMIC), zlib -6 text (LZ77
 distances, deferred copies across lanes and chains), zlib Z_FIXED text, the config-2 layout (stored
 and fixed-Huffman pieces alternating), stored blocks alone, the reference's 39 known-answer tests and
 corrupted streams.  Reference semantics: D/decomp/Open.java:83-618."""
@@ -36,7 +38,8 @@ def _env(name, value):
     return old
 
 
-MODES = {"fast": {}, "full_only": {"NDFL_EMIT_FAST": "0"}, "hand_over": {"NDFL_NO_BT": "1"}}
+MODES = {"fast": {}, "full_only": {"NDFL_EMIT_FAST": "0"}, "hand_over": {"NDFL_NO_BT": "1"},
+         "no_alias": {"NDFL_NO_ALIAS": "1"}}
 
 
 @pytest.fixture(params=list(MODES))
