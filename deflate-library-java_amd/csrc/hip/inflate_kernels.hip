@@ -972,7 +972,7 @@ struct EmitChain {
 // ---- device-side candidate list and chain linking (one host synchronization per decode) ----------
 // Link summary (DevLink::info, u64): the decode's results the host reads once at the end.
 enum : uint32_t { LI_NCAND = 0, LI_NCH, LI_TOTAL, LI_FLAGS, LI_STOP, LI_CODE, LI_OUTLEN, LI_CONSUMED, LI_NCAND_ALL,
-                  LI_LO, LI_WORDS = 16 };
+                  LI_LO, LI_NREP, LI_WORDS = 16 };
 enum : uint64_t { LF_REPAIR = 1, LF_RANGE = 2, LF_CAPACITY = 4 };
 constexpr uint32_t NOLINK = 0xFFFFFFFFu;
 
@@ -1026,37 +1026,49 @@ __device__ __forceinline__ uint64_t stored_key(const inf::In& in, uint64_t p) {
     return (((p + 3 + 7) & ~7ull) << 1) | (h & 1u);
 }
 
+// rep[k] = the candidate counted for candidate k (the first of its aliases, else k) over the
+// info[LI_NCAND] candidates; info[LI_NREP] += the candidates counted (the host reads it with the
+// candidate count and picks the count pass's width from it).
+extern "C" __global__ void __launch_bounds__(256)
+ndfl_inflate_alias_mark_kernel(const uint64_t* cands, uint64_t* info, const uint32_t* w, uint64_t nwords, uint64_t nbits,
+                               uint32_t* rep) {
+    const inf::In in{w, nwords, nbits};
+    const uint32_t n = (uint32_t)min<uint64_t>(info[LI_NCAND], 0xFFFFFFFFull);
+    for (uint32_t k0 = blockIdx.x * 256; k0 < n; k0 += gridDim.x * 256) {
+        const uint32_t k = k0 + threadIdx.x;
+        bool own = false;
+        if (k < n) {
+            const uint64_t p = cands[k], key = stored_key(in, p);
+            uint32_t r = k;
+            if (key != ~0ull)
+                for (uint32_t j = k; j > 0 && cands[j - 1] + 10 >= p; j--)
+                    if (stored_key(in, cands[j - 1]) == key) r = j - 1;
+            rep[k] = r;
+            own = r == k;
+        }
+        const uint32_t c = (uint32_t)__popcll(__ballot(own));
+        if ((threadIdx.x & 63) == 0 && c) atomicAdd((unsigned long long*)&info[LI_NREP], (unsigned long long)c);
+    }
+}
+
 // Claim order of the count pass: longest first by the bits to the next start (24 buckets of 32
-// Kibit), so that no long chain is left for the end of the launch.  One workgroup.  With `rep`,
-// stored-header aliases are left out of the order (rep[k] = the candidate counted for k; *nord = the
+// Kibit), so that no long chain is left for the end of the launch.  One workgroup.  With `rep`
+// (ndfl_inflate_alias_mark_kernel), stored-header aliases are left out of the order (*nord = the
 // chains to count).
 extern "C" __global__ void __launch_bounds__(1024)
-ndfl_inflate_order_kernel(const uint64_t* cands, uint32_t n, uint64_t end_bit, uint32_t* order, const uint32_t* w,
-                          uint64_t nwords, uint64_t nbits, uint32_t* rep, uint32_t* nord) {
+ndfl_inflate_order_kernel(const uint64_t* cands, uint32_t n, uint64_t end_bit, uint32_t* order, const uint32_t* rep,
+                          uint32_t* nord) {
     constexpr uint32_t NB = 24;
     __shared__ uint32_t bc[NB + 1];
     if (threadIdx.x <= NB) bc[threadIdx.x] = 0;
     __syncthreads();
-    const inf::In in{w, nwords, nbits};
     auto bucket = [&](uint32_t k) -> uint32_t {
         const uint64_t nx = k + 1 < n ? cands[k + 1] : end_bit;
         const uint64_t len = nx > cands[k] ? nx - cands[k] : 0;
         return NB - 1 - (uint32_t)min<uint64_t>(NB - 1, len >> 15);
     };
-    auto alias_of = [&](uint32_t k) -> uint32_t {
-        if (!rep) return k;
-        const uint64_t p = cands[k], key = stored_key(in, p);
-        uint32_t r = k;
-        if (key != ~0ull)
-            for (uint32_t j = k; j > 0 && cands[j - 1] + 10 >= p; j--)
-                if (stored_key(in, cands[j - 1]) == key) r = j - 1;
-        return r;
-    };
-    for (uint32_t k = threadIdx.x; k < n; k += blockDim.x) {
-        const uint32_t r = alias_of(k);
-        if (rep) rep[k] = r;
-        if (r == k) atomicAdd(&bc[bucket(k) + 1], 1u);
-    }
+    for (uint32_t k = threadIdx.x; k < n; k += blockDim.x)
+        if (!rep || rep[k] == k) atomicAdd(&bc[bucket(k) + 1], 1u);
     __syncthreads();
     if (threadIdx.x == 0) {
         for (uint32_t b = 0; b < NB; b++) bc[b + 1] += bc[b];
@@ -1310,8 +1322,7 @@ static uint32_t wg_grid(K kernel, uint32_t threads, uint32_t cap) {
     return std::min<uint32_t>(cap, (uint32_t)(ncu * per));
 }
 template <typename... A>
-static void launch_count(hipStream_t s, uint32_t nchains, A... args) {
-    const uint32_t W = count_w();
+static void launch_count(hipStream_t s, uint32_t W, uint32_t nchains, A... args) {
     if (W == 1) {
         static const uint32_t g1 = wave_grid(ndfl_inflate_count_wave_kernel, inf::COUNT_WAVES, "NDFL_COUNT_WPC");
         hipLaunchKernelGGL(ndfl_inflate_count_wave_kernel, dim3(std::min(nchains, g1)), dim3(64), 0, s, args...);
@@ -1488,9 +1499,28 @@ static int inflate_devlink(InflateScratch& S, hipStream_t s, const uint32_t* d_w
     hipLaunchKernelGGL(ndfl_inflate_cand_slice_kernel, dim3((uint32_t)std::min<uint64_t>(4096, (cap_all + 255) / 256)),
                        dim3(256), 0, s, (const uint64_t*)d_sorted, info, start_bit, end_bit, (uint64_t*)S.d_cands);
     INF_CHK(hipGetLastError());
-    INF_CHK(hipMemcpyAsync((void*)hinfo, info, 8, hipMemcpyDeviceToHost, s));
+    // stored-header aliases counted once (NDFL_NO_ALIAS: every candidate counted)
+    const bool alias_on = !getenv("NDFL_NO_ALIAS");
+    uint32_t* d_rep = nullptr;
+    if (alias_on) {
+        INF_CHK(inf_ensure(&S.d_rep, &S.d_rep_cap, (size_t)cap_all * 4 + 64));
+        d_rep = (uint32_t*)S.d_rep;
+        hipLaunchKernelGGL(ndfl_inflate_alias_mark_kernel, dim3((uint32_t)std::min<uint64_t>(1024, (cap_all + 255) / 256)),
+                           dim3(256), 0, s, (const uint64_t*)S.d_cands, info, d_w, nwords, nbits, d_rep);
+        INF_CHK(hipGetLastError());
+    }
+    INF_CHK(hipMemcpyAsync((void*)hinfo, info, (LI_NREP + 1) * 8, hipMemcpyDeviceToHost, s));
     INF_CHK(hipStreamSynchronize(s));                          // (1) the number of chain starts
     const uint64_t n = hinfo[LI_NCAND];
+    // the count pass's width: one wave per chain, unless the chains to count are few against the
+    // count waves (fewer than 4 per wave), where a chain's rounds in sequence bound the pass (config
+    // 2: fixed-Huffman pieces between stored blocks: 4 waves per chain count it in 2.0 ms instead of
+    // 4.0; the bench's 66,770 chains: one wave each) -- NDFL_COUNT_W overrides
+    const uint64_t nrep = alias_on ? hinfo[LI_NREP] : n;
+    static const uint32_t count_waves = wave_grid(ndfl_inflate_count_wave_kernel, COUNT_WAVES, "NDFL_COUNT_WPC");
+    const uint32_t W = getenv("NDFL_COUNT_W") ? count_w() : (nrep < 4ull * count_waves && nbits >= (1ull << 24)) ? 4u : 1u;
+    if (getenv("NDFL_STATS")) fprintf(stderr, "[ndfl] count pass: %llu candidates, %llu counted, width %u\n",
+                                      (unsigned long long)n, (unsigned long long)nrep, W);
     if (n == 0 || n > (1ull << 24)) return LINK_FALLBACK;
     const uint32_t ncand = (uint32_t)n;
     int rc = setup_pool(S, s, n, nbits);
@@ -1501,16 +1531,9 @@ static int inflate_devlink(InflateScratch& S, hipStream_t s, const uint32_t* d_w
     uint32_t* d_order = (uint32_t*)((char*)S.d_stops + n * 8);
     if (!S.d_cticket) INF_CHK(hipMalloc(&S.d_cticket, 64));
     INF_CHK(hipMemsetAsync(S.d_cticket, 0, 4, s));
-    // stored-header aliases counted once (NDFL_NO_ALIAS: every candidate counted)
-    const bool alias_on = !getenv("NDFL_NO_ALIAS");
-    uint32_t* d_rep = nullptr;
     uint32_t* d_nord = (uint32_t*)S.d_cticket + 8;
-    if (alias_on) {
-        INF_CHK(inf_ensure(&S.d_rep, &S.d_rep_cap, (size_t)ncand * 4 + 64));
-        d_rep = (uint32_t*)S.d_rep;
-    }
     hipLaunchKernelGGL(ndfl_inflate_order_kernel, dim3(1), dim3(1024), 0, s, (const uint64_t*)S.d_cands, ncand, end_bit,
-                       d_order, d_w, nwords, nbits, d_rep, alias_on ? d_nord : (uint32_t*)nullptr);
+                       d_order, (const uint32_t*)d_rep, alias_on ? d_nord : (uint32_t*)nullptr);
     INF_CHK(hipGetLastError());
     if (!S.d_ph) INF_CHK(hipMalloc(&S.d_ph, (size_t)std::max(COUNT_WAVES, EMIT_WAVES) * sizeof(wv::PhArr)));
     static const bool stats_on = getenv("NDFL_STATS") != nullptr;
@@ -1523,7 +1546,7 @@ static int inflate_devlink(InflateScratch& S, hipStream_t s, const uint32_t* d_w
                            (const uint64_t*)S.d_cands, ncand, (wv::HdrRec*)S.d_hrec);
         INF_CHK(hipGetLastError());
     }
-    launch_count(s, ncand,
+    launch_count(s, W, ncand,
                        d_w, nwords, nbits, (const uint64_t*)S.d_cands, (const uint64_t*)nullptr, ncand,
                        (const uint64_t*)S.d_cands, ncand, limit, (ChainRes*)S.d_res,
                        stats_on ? (uint32_t*)S.d_stats : nullptr, (uint64_t)0, S.pool, (uint32_t*)S.d_cticket,
@@ -1928,7 +1951,7 @@ static int inflate_run(InflateScratch& S, hipStream_t s, const uint8_t* in, uint
         if (!S.d_cticket) INF_CHK(hipMalloc(&S.d_cticket, 64));
         INF_CHK(hipMemsetAsync(S.d_cticket, 0, 4, s));
         if (S.count_first) INF_CHK(hipEventRecord(S.ev[2], s));
-        launch_count(s, (uint32_t)n,
+        launch_count(s, count_w(), (uint32_t)n,
                            d_w, nwords, nbits,
                            (const uint64_t*)S.d_starts, (const uint64_t*)S.d_stops, (uint32_t)n,
                            (const uint64_t*)S.d_cands, ncand, limit, (ChainRes*)S.d_res, stats_on ? (uint32_t*)S.d_stats : nullptr,

@@ -2138,11 +2138,16 @@ ndfl_inflate_emit_fast_kernel(const uint32_t* w, uint64_t nwords, uint64_t nbits
 }
 
 // ---- resolve rounds -------------------------------------------------------------------------------
+#ifndef NDFL_RESOLVE_HOPS
+#define NDFL_RESOLVE_HOPS 4
+#endif
 // Pending bytes form 32-byte groups (one bitmap word each) listed in `list`.  A wave takes two
 // groups, a lane one byte i: with p = i - ref[i], a final p gives out[i] = out[p]; a pending p makes
 // i jump (ref[i] += ref[p]), so the remaining distance to a final byte halves each round.  Bits and
 // bytes read here were settled by earlier launches; ref[p] may be updated concurrently, but both its
-// old and new values point at a byte of the same value.
+// old and new values point at a byte of the same value.  A lane follows up to NDFL_RESOLVE_HOPS
+// pending targets in one launch before it jumps (fewer rounds for deep chains of copies of copies,
+// as in LZ77 text).
 extern "C" __global__ void __launch_bounds__(256)
 ndfl_inflate_resolve_kernel(const uint32_t* list, const uint32_t* nlist, const uint32_t* pend, uint32_t* ref,
                             uint8_t* out, uint32_t* newbits) {
@@ -2153,12 +2158,24 @@ ndfl_inflate_resolve_kernel(const uint32_t* list, const uint32_t* nlist, const u
         const uint32_t bits = pend[wd];
         bool still = false;
         if ((bits >> b) & 1) {
+            // follow up to NDFL_RESOLVE_HOPS references in this launch (each keeps the value: every
+            // ref, old or new, points at a byte of the same value); a final target copies, else the
+            // byte keeps the distance reached
             const uint64_t i = wd * 32 + b;
-            const uint32_t d = ref[i];
-            const uint64_t p = i - d;
-            if ((pend[p >> 5] >> (p & 31)) & 1) {
-                const uint64_t nd = (uint64_t)d + ref[p];
-                if (nd < (1ull << 32)) ref[i] = (uint32_t)nd;     // else keep d: p still leads to the value
+            uint64_t d = ref[i];
+            uint64_t p = i - d;
+            bool pending = (pend[p >> 5] >> (p & 31)) & 1;
+#pragma unroll 1
+            for (int h = 1; h < NDFL_RESOLVE_HOPS && pending; h++) {
+                const uint64_t nd = d + ref[p];
+                if (nd >= (1ull << 32)) break;                     // (keep d: p still leads to the value)
+                d = nd;
+                p = i - d;
+                pending = (pend[p >> 5] >> (p & 31)) & 1;
+            }
+            if (pending) {
+                const uint64_t nd = d + ref[p];
+                ref[i] = (uint32_t)(nd < (1ull << 32) ? nd : d);
                 still = true;
             } else {
                 out[i] = out[p];
