@@ -1678,7 +1678,10 @@ ndfl_inflate_emit_wave_kernel(const uint32_t* w, uint64_t nwords, uint64_t nbits
         if (info[LI_FLAGS]) return;             // to emit when the host has to step in (uniform)
         nlist = (uint32_t)info[LI_NCH];
     }
-    if (dnlist) nlist = *dnlist;                // (the chains the fast emit pass left: eorder lists them)
+    if (dnlist) {                               // the chains the fast emit pass left (eorder lists them):
+        nlist = *dnlist;                        // usually none, and then no wave takes a ticket
+        if (nlist == 0) return;
+    }
     for (;;) {
     __syncthreads();
     if (lane == 0) s_ticket = atomicAdd(ticket, 1u);
