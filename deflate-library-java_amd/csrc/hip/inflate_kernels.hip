@@ -1512,6 +1512,11 @@ static int inflate_devlink(InflateScratch& S, hipStream_t s, const uint32_t* d_w
     INF_CHK(hipMemcpyAsync((void*)hinfo, info, (LI_NREP + 1) * 8, hipMemcpyDeviceToHost, s));
     INF_CHK(hipStreamSynchronize(s));                          // (1) the number of chain starts
     const uint64_t n = hinfo[LI_NCAND];
+    if (const char* dump = getenv("NDFL_DUMP_CANDS")) {        // (diagnostics: the sorted candidate list)
+        std::vector<uint64_t> hc(n);
+        INF_CHK(hipMemcpy(hc.data(), S.d_cands, n * 8, hipMemcpyDeviceToHost));
+        if (FILE* f = fopen(dump, "wb")) { fwrite(hc.data(), 8, n, f); fclose(f); }
+    }
     // the count pass's width: one wave per chain, unless the chains to count are few against the
     // count waves (fewer than 4 per wave), where a chain's rounds in sequence bound the pass (config
     // 2: fixed-Huffman pieces between stored blocks: 4 waves per chain count it in 2.0 ms instead of
