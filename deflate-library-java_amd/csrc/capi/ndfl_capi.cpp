@@ -75,9 +75,7 @@ struct ndfl_ctx {
     uint32_t parent_len = 0;        // internal: history rule of BinarySplit sub-blocks (0: chunk_len)
     InflateScratch inf;
     uint32_t* h_pinned = nullptr;   // small pinned area for results
-    // encoder slab pipeline: a second stream and its events (created on first use)
-    hipStream_t aux = nullptr;
-    hipEvent_t ev_fork = nullptr, ev_join = nullptr, ev_off[2] = {nullptr, nullptr};
+    Knobs knobs;                    // switches read once at ndfl_ctx_create (ndfl_common.hpp)
 };
 
 #define HIPCHK(x) do { hipError_t _e = (x); if (_e != hipSuccess) return NDFL_E_DEVICE; } while (0)
@@ -144,6 +142,8 @@ int ndfl_ctx_create(ndfl_ctx** out, int device, uint32_t flags) {
     init_host_tables();
     ndfl_ctx* c = new ndfl_ctx();
     c->device = device;
+    c->knobs.read();
+    c->inf.knobs = c->knobs;
     if (hipStreamCreateWithFlags(&c->own, hipStreamDefault) != hipSuccess) { delete c; return NDFL_E_DEVICE; }
     c->stream = c->own;
     hipEventCreate(&c->ev0);
@@ -173,8 +173,6 @@ int ndfl_ctx_destroy(ndfl_ctx* c) {
     if (c->ev0) hipEventDestroy(c->ev0);
     if (c->ev1) hipEventDestroy(c->ev1);
     if (c->ev_order) hipEventDestroy(c->ev_order);
-    for (hipEvent_t e : {c->ev_fork, c->ev_join, c->ev_off[0], c->ev_off[1]}) if (e) hipEventDestroy(e);
-    if (c->aux) hipStreamDestroy(c->aux);
     if (c->own) hipStreamDestroy(c->own);
     delete c;
     return NDFL_OK;
@@ -284,20 +282,18 @@ int ndfl_deflate_chunks(ndfl_ctx* c, const uint8_t* hist, uint32_t hist_len, uin
     a.crc_tab = c->d_tabs.as<uint32_t>();
     a.crc_x = c->d_tabs.as<uint32_t>() + 1024;
     a.prof = nullptr;
-    const bool prof = getenv("NDFL_DEFLATE_PROFILE") != nullptr;
+    const bool prof = c->knobs.deflate_profile;
     if (prof) { HIPCHK(hipMalloc(&a.prof, (size_t)nch * 128)); HIPCHK(hipMemsetAsync(a.prof, 0, (size_t)nch * 128, s)); }
     a.hist_out = nullptr; a.codes = nullptr; a.chunk_off = nullptr;
     {
         // next generation of resident split-pass workgroups: 2 per CU (1024 threads, <= 75 KB LDS)
         static int ncu = 0;
         if (!ncu && hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, c->device) != hipSuccess) ncu = 0;
-        const char* pe = getenv("NDFL_DEFLATE_PF");        // A/B knob: 0 turns the L2 touch off
-        a.pf_dist = (pe && atoi(pe) == 0) ? 0u : 2u * (uint32_t)ncu;
+        a.pf_dist = c->knobs.deflate_pf ? 2u * (uint32_t)ncu : 0u;     // (NDFL_DEFLATE_PF=0: no L2 touch)
     }
-    // split pipeline by default (deflate_split.hip); NDFL_DEFLATE_FUSED=1 selects the one-kernel encoder
-    const char* fenv = getenv("NDFL_DEFLATE_FUSED");      // read per call (tests switch it)
-    const bool fused = fenv != nullptr && atoi(fenv) != 0;
-    const bool split = !fused && !prof;
+    // split pipeline by default (deflate_split.hip); NDFL_DEFLATE_FUSED=1 (or the per-phase profile)
+    // selects the one-kernel encoder
+    const bool split = !c->knobs.deflate_fused && !prof;
     uint64_t* d_total = nullptr;
     if (split) {
         HIPCHK(c->d_hist.ensure((size_t)nch * HREC * 4));
@@ -309,51 +305,8 @@ int ndfl_deflate_chunks(ndfl_ctx* c, const uint8_t* hist, uint32_t hist_len, uin
         d_total = c->d_off.as<uint64_t>() + nch;
     }
     a.c0 = 0;
-    // Slab pipeline (split passes): the chunks go in slabs of `slab` chunks, alternately on the
-    // context's stream and a second one, so one slab's code construction (one wave per chunk, a
-    // latency-bound pass that leaves most of each CU idle) runs beside the next slab's histogram pass
-    // and the previous slab's emit pass, and a slab's emit re-reads data that its histogram pass has
-    // just brought into the last-level cache.  Slab k's offsets start at slab k-1's end bit, which that
-    // slab's offsets launch leaves on the device (ev_off orders the two).  NDFL_DEFLATE_SLAB: chunks
-    // per slab (0, the default: one launch per pass; measured on the 4 GiB bench: 1024 / 2048 / 4096
-    // chunks per slab 10.32 / 9.49 / 8.84 ms against 7.96 ms in one launch per pass).
-    uint32_t slab = 0;
-    if (split) {
-        const char* se = getenv("NDFL_DEFLATE_SLAB");     // read per call (tests switch it)
-        slab = se ? (uint32_t)atoi(se) : 0u;
-        if (slab >= nch) slab = 0;
-    }
-    if (slab && !c->aux) {
-        HIPCHK(hipStreamCreateWithFlags(&c->aux, hipStreamNonBlocking));
-        for (hipEvent_t* e : {&c->ev_fork, &c->ev_join, &c->ev_off[0], &c->ev_off[1]})
-            HIPCHK(hipEventCreateWithFlags(e, hipEventDisableTiming));
-    }
     HIPCHK(hipEventRecord(c->ev0, s));
-    if (split && slab) {
-        HIPCHK(hipEventRecord(c->ev_fork, s));
-        HIPCHK(hipStreamWaitEvent(c->aux, c->ev_fork, 0));
-        const uint32_t ns = (nch + slab - 1) / slab;
-        for (uint32_t k = 0; k < ns; k++) {
-            hipStream_t hs = (k & 1) ? c->aux : s;
-            Args b = a;
-            b.c0 = k * slab;
-            const uint32_t nk = std::min(slab, nch - b.c0);
-            hipLaunchKernelGGL(ndfl_deflate_hist_kernel, dim3(nk), dim3(1024), 0, hs, b);
-            HIPCHK(hipGetLastError());
-            hipLaunchKernelGGL(ndfl_deflate_codes_kernel, dim3(nk), dim3(64), 0, hs, b);
-            HIPCHK(hipGetLastError());
-            if (k > 0) HIPCHK(hipStreamWaitEvent(hs, c->ev_off[(k - 1) & 1], 0));
-            hipLaunchKernelGGL(ndfl_deflate_offsets_kernel, dim3(1), dim3(1024), 0, hs, (const uint64_t*)a.status + b.c0,
-                               nk, (uint64_t)start_bitpos, c->d_off.as<uint64_t>() + b.c0, d_total,
-                               k > 0 ? (const uint64_t*)d_total : nullptr);
-            HIPCHK(hipGetLastError());
-            HIPCHK(hipEventRecord(c->ev_off[k & 1], hs));
-            hipLaunchKernelGGL(ndfl_deflate_emit_kernel, dim3(nk), dim3(1024), 0, hs, b);
-            HIPCHK(hipGetLastError());
-        }
-        HIPCHK(hipEventRecord(c->ev_join, c->aux));
-        HIPCHK(hipStreamWaitEvent(s, c->ev_join, 0));
-    } else if (split) {
+    if (split) {
         hipLaunchKernelGGL(ndfl_deflate_hist_kernel, dim3(nch), dim3(1024), 0, s, a);
         HIPCHK(hipGetLastError());
         hipLaunchKernelGGL(ndfl_deflate_codes_kernel, dim3(nch), dim3(64), 0, s, a);
@@ -485,7 +438,7 @@ int ndfl_deflate_chunks_lz77(ndfl_ctx* c, const uint8_t* hist, uint32_t hist_len
     la.hist_limit = hist_limit; la.min_run = (uint32_t)min_run; la.max_run = (uint32_t)max_run;
     la.min_dist = (uint32_t)min_dist; la.max_dist = (uint32_t)max_dist;
     la.link = c->d_link.as<uint16_t>(); la.match = c->d_match.as<uint32_t>();
-    static const bool lz_stats = getenv("NDFL_LZ_STATS") != nullptr;
+    const bool lz_stats = c->knobs.lz_stats;
     la.stats = nullptr;
     if (lz_stats) {
         HIPCHK(hipMalloc(&la.stats, 128));
@@ -505,10 +458,8 @@ int ndfl_deflate_chunks_lz77(ndfl_ctx* c, const uint8_t* hist, uint32_t hist_len
     // match search: at the positions the greedy parse visits (default), or at every position by hash
     // chains (NDFL_LZ_SEARCH=chain, the round-3 search); NDFL_LZ_LEAD=0 drops the tiles' lead-in (so
     // the encode kernel's fallback search runs at most tile starts: a test of that path)
-    const char* se = getenv("NDFL_LZ_SEARCH");                 // read per call (tests switch them)
-    const bool chain_search = se && !strcmp(se, "chain");
-    const char* le = getenv("NDFL_LZ_LEAD");
-    const uint32_t lead_on = (le && atoi(le) == 0) ? 0u : 1u;
+    const bool chain_search = c->knobs.lz_chain;
+    const uint32_t lead_on = c->knobs.lz_lead == 0 ? 0u : 1u;
 
     HIPCHK(hipEventRecord(c->ev0, s));
     for (uint32_t cb = 0; cb < nch; cb += batch_ch) {
@@ -1055,6 +1006,15 @@ int ndfl_inflate_sync(ndfl_ctx* c, const uint8_t* in, uint64_t in_len, uint64_t 
     return inflate_sync(c->inf, ordered_stream(c), in, in_len, from_bit, window_bits, flags, sync_bit, &c->last_ms);
 }
 
+int ndfl_inflate_headers(ndfl_ctx* c, const uint8_t* in, uint64_t in_len, uint32_t flags, uint64_t* headers,
+                         uint64_t cap, uint64_t* n_headers, uint64_t* survivors, uint64_t surv_cap, uint64_t* stats) {
+    if (!c || !n_headers || (!in && in_len) || (!headers && cap) || (!survivors && surv_cap)) return NDFL_E_ARG;
+    HIPCHK(hipSetDevice(c->device));
+    const int r = inflate_headers(c->inf, ordered_stream(c), in, in_len, flags, headers, cap, n_headers, survivors,
+                                  surv_cap, stats);
+    return r == -4 ? NDFL_E_DEVICE : r < 0 ? NDFL_E_INTERNAL : r;
+}
+
 int ndfl_inflate_resolve(ndfl_ctx* c, uint64_t* n_reemitted) {
     if (!c || !n_reemitted) return NDFL_E_ARG;
     HIPCHK(hipSetDevice(c->device));
@@ -1065,6 +1025,13 @@ int ndfl_inflate_tail(ndfl_ctx* c, uint64_t tail_len, uint8_t* dst) {
     if (!c || (!dst && tail_len)) return NDFL_E_ARG;
     HIPCHK(hipSetDevice(c->device));
     const int r = inflate_tail(c->inf, ordered_stream(c), tail_len, dst);
+    return r == -5 ? NDFL_E_STATE : r == -6 ? NDFL_E_UNSUPPORTED : r == -1 ? NDFL_E_ARG : r;
+}
+
+int ndfl_inflate_tail_map(ndfl_ctx* c, uint64_t tail_len, uint32_t* dst) {
+    if (!c || (!dst && tail_len)) return NDFL_E_ARG;
+    HIPCHK(hipSetDevice(c->device));
+    const int r = inflate_tail_map(c->inf, ordered_stream(c), tail_len, dst);
     return r == -5 ? NDFL_E_STATE : r == -6 ? NDFL_E_UNSUPPORTED : r == -1 ? NDFL_E_ARG : r;
 }
 

@@ -25,7 +25,6 @@
 // first error in stream order wins.
 // D/ = /root/reference/src/io/nayuki/deflate/
 #pragma once
-#include "kraft_bits.hpp"
 #include "ndfl_common.hpp"
 #include "../../../include/ndfl.h"
 #include <vector>
@@ -49,6 +48,8 @@ enum : int { R_UEOS = 1, R_RESERVED_BLOCK_TYPE, R_LEN_MISMATCH, R_UNDER_FULL, R_
              R_INTERNAL = 100 };
 
 constexpr int CLO[19] = {16, 17, 18, 0, 8, 7, 9, 6, 10, 5, 11, 4, 12, 3, 13, 2, 14, 1, 15};
+// position of code-length symbol sy in CLO (its 3-bit length's index in the header)
+constexpr int CLO_INV[19] = {3, 17, 15, 13, 11, 9, 7, 5, 4, 6, 8, 10, 12, 14, 16, 18, 0, 1, 2};
 
 // RUN_LENGTH_TABLE / DISTANCE_TABLE of D/decomp/Open.java:841-886 in closed form.
 __device__ __forceinline__ void run_base(uint32_t i, uint32_t& base, uint32_t& ne) {
@@ -68,12 +69,6 @@ static_assert(IN_PAD == NDFL_IN_PAD_BYTES, "kernel pad and the NDFL_IN_PADDED co
 // staging (wv::stage_round) clamps word indices at nwords + 60, i.e. nwords * 4 + 244 bytes
 static_assert(3 * 4 + 2 * 16 + 16 <= IN_PAD, "16-byte prefetch clamp must stay inside the zero padding");
 static_assert((60 + 1) * 4 <= IN_PAD, "round staging clamp must stay inside the zero padding");
-// header finder scan pattern (32-bit words): FIND_WIN_WORDS of every FIND_PERIOD_WORDS.  Dense
-// (every position) by default: sparse windows make chains span several blocks, which costs more
-// in the count/emit passes' load balance than it saves here.
-constexpr uint32_t PART_EXPENSIVE = 1u << 30;     // partitioned finder: expensive first block (state flag)
-constexpr uint32_t FIND_WIN_WORDS = 32768;
-constexpr uint32_t FIND_PERIOD_WORDS = 32768;
 #ifndef NDFL_FIND_WPT
 #define NDFL_FIND_WPT 16
 #endif
@@ -304,8 +299,9 @@ __device__ bool strict_dynamic(const In& in, uint64_t p) {
 }
 
 // A stored block at p (LEN == ~NLEN already checked) must be final or be followed by a plausible
-// header: not btype 3; stored -> LEN == ~NLEN; dynamic -> complete code-length code.
-__device__ __noinline__ bool strict_stored(const In& in, uint64_t p) {
+// header: not btype 3; stored -> LEN == ~NLEN; dynamic -> complete code-length code.  (Inlined: the
+// strict stage must not use scratch memory, see there.)
+__device__ __forceinline__ bool strict_stored(const In& in, uint64_t p) {
     Rd rd; rd.init(in, p);
     const uint32_t bf = rd.get(in, 1);
     const uint64_t al = (p + 3 + 7) & ~7ull;
@@ -336,12 +332,10 @@ __device__ __noinline__ bool strict_stored(const In& in, uint64_t p) {
 
 }  // namespace inf
 
-// Header finder over every bit position, stage 1 (quick filter).  Each thread tests 32 consecutive
-// positions at once, bit-sliced (bit i of every vector = position p0 + i): BTYPE from two shifts of
-// the input; dynamic headers need a complete code-length code (Kraft sum exactly 1 over the
-// HCLEN+4 3-bit lengths -- kraft_bits.hpp, generated); stored headers need LEN == ~NLEN at the
-// next byte boundary (one test per byte position) and zero padding.  Survivors (about 1 in 1000
-// positions) go to a global list for the strict stage.
+// Header finder over every bit position, stage 1 (quick filter): BTYPE from two shifts of the
+// input; dynamic headers need a complete code-length code (Kraft sum exactly 1 over the HCLEN+4
+// 3-bit lengths); stored headers need LEN == ~NLEN at the next byte boundary and zero padding.
+// Survivors (about 1 in 1000 positions) go to a global list for the strict stage.
 #ifndef NDFL_FIND_WPE
 #define NDFL_FIND_WPE 3
 #endif
@@ -349,92 +343,35 @@ __device__ __noinline__ bool strict_stored(const In& in, uint64_t p) {
 #define NDFL_FIND_LASTBLK 0
 #endif
 #ifndef NDFL_STRICT_WPE
-#define NDFL_STRICT_WPE 4
+#define NDFL_STRICT_WPE 5
 #endif
 namespace inf {
-// Stage-1 test of the 32 bit positions of input word t below scan_end; survivors go to the
-// workgroup's LDS list (bit 63 set: dynamic header, clear: stored).
-__device__ __forceinline__ void find_word(const In& in, uint64_t t, uint64_t scan_end, uint64_t* cand,
-                                          uint32_t* ncand) {
-    const uint64_t nbits = in.nbits;
-    const uint64_t p0 = t * 32;
-    if (p0 >= scan_end) return;
-    const uint32_t w0 = in.ld(t), w1 = in.ld(t + 1), w2 = in.ld(t + 2), w3 = in.ld(t + 3);
-    const uint64_t W = (uint64_t)w0 | ((uint64_t)w1 << 32);
-    const uint32_t b1 = (uint32_t)(W >> 1), b2 = (uint32_t)(W >> 2);
-    uint32_t valid = 0xFFFFFFFFu;
-    if (p0 + 35 > nbits) valid = (nbits >= p0 + 3) ? (uint32_t)((1ull << (nbits - p0 - 2)) - 1) : 0u;
-    if (p0 + 32 > scan_end) valid &= (uint32_t)((1ull << (scan_end - p0)) - 1);
-    // Candidates are chain starts, not a decoding decision: a block header that is no candidate is
-    // decoded by the chain before it, so the filter may pass over headers no encoder writes before a
-    // stream's last block -- BFINAL = 1 (the final block is the one block after which nothing needs a
-    // chain of its own) and HLIT or HDIST of 30 or 31 (287/288 literal/length or 31/32 distance
-    // codes: never written, the symbols past 285 / 29 are invalid) -- about a dozen operations per
-    // 32 positions, for half the strict stage's work.  NDFL_FIND_LASTBLK=1 keeps final headers (A/B).
-#if NDFL_FIND_LASTBLK
-    const uint32_t notfinal = ~0u;
-#else
-    const uint32_t notfinal = ~w0;
-#endif
-    const uint32_t h4 = (uint32_t)(W >> 4), h5 = (uint32_t)(W >> 5), h6 = (uint32_t)(W >> 6),
-                   h7 = (uint32_t)(W >> 7), d9 = (uint32_t)(W >> 9), d10 = (uint32_t)(W >> 10),
-                   d11 = (uint32_t)(W >> 11), d12 = (uint32_t)(W >> 12);
-    const uint32_t big = (NDFL_BOP3(h4, h5, h6, 0x80) & h7) | (NDFL_BOP3(d9, d10, d11, 0x80) & d12);
-    uint32_t m2 = ~b1 & b2 & valid & notfinal & ~big & kraft_complete_mask(w0, w1, w2, w3);
-    // LEN == ~NLEN at byte positions p0 + 8j, j = 1..5; position i pads to j = (i + 10) / 8
-    const uint64_t W12 = (uint64_t)w1 | ((uint64_t)w2 << 32);
-    const uint32_t x1 = (uint32_t)(W >> 8), x2 = (uint32_t)(W >> 16), x3 = (uint32_t)(W >> 24), x4 = w1,
-                   x5 = (uint32_t)(W12 >> 8);
-#define NDFL_LENOK(x) ((((x) ^ ((x) >> 16)) & 0xFFFFu) == 0xFFFFu)
-    const uint32_t okm = (NDFL_LENOK(x1) ? 0x0000003Fu : 0u) | (NDFL_LENOK(x2) ? 0x00003FC0u : 0u) |
-                         (NDFL_LENOK(x3) ? 0x003FC000u : 0u) | (NDFL_LENOK(x4) ? 0x3FC00000u : 0u) |
-                         (NDFL_LENOK(x5) ? 0xC0000000u : 0u);
-#undef NDFL_LENOK
-    uint32_t m0 = ~b1 & ~b2 & valid & notfinal & okm;
-    while (m2) {
-        const uint32_t o = __builtin_ctz(m2);
-        m2 &= m2 - 1;
-        const uint32_t nf3 = 3 * (((uint32_t)(W >> (o + 13)) & 15u) + 4);
-        if (p0 + o + 17 + nf3 <= nbits) {
-            uint32_t k = atomicAdd(ncand, 1u);
-            if (k < 2048) cand[k] = (p0 + o) | (1ull << 63);
-        }
-    }
-    while (m0) {
-        const uint32_t o = __builtin_ctz(m0);
-        m0 &= m0 - 1;
-        const uint32_t q = o + 3, al = (q + 7) & ~7u;            // al <= 40
-        const uint32_t pad = al > q ? (uint32_t)(W >> q) & ((1u << (al - q)) - 1u) : 0u;
-        if (pad) continue;
-        const uint32_t ln = (al < 32 ? (uint32_t)(W >> al) : (uint32_t)(W12 >> (al - 32))) & 0xFFFFu;
-        if (p0 + al + 32 + 8ull * ln <= nbits) {
-            uint32_t k = atomicAdd(ncand, 1u);
-            if (k < 2048) cand[k] = p0 + o;
-        }
-    }
-}
-
-// Compacted Kraft test (NDFL_FIND_COMPACT, the default): the same survivors as find_word, for the
-// 64 words of a wave at once.  The cheap bit-sliced masks (BTYPE, BFINAL, HLIT/HDIST, stored LEN/NLEN)
-// stay per lane; the positions they leave for the code-length code's Kraft test -- about 1 in 9 --
-// are compacted into a wave list and tested one per lane: the HCLEN + 4 three-bit lengths as one
-// 57-bit field, summed by five lookups of a 4,096-entry table of the Kraft sums of four lengths
-// (kr4).  About 30 operations per such position instead of the bit-sliced test's 451 per 32
-// positions, which the finder's VALU-bound scan spends at every position.  A pass takes at most
-// FIND_TAKE positions per lane (a dense pattern takes more passes).
-#ifndef NDFL_FIND_COMPACT
-#define NDFL_FIND_COMPACT 1
-#endif
+// The 32 positions of each input word, for the 64 words of a wave at once.  The cheap masks
+// (BTYPE, BFINAL, HLIT/HDIST, stored LEN/NLEN) are bit-sliced per lane (bit i = position p0 + i);
+// the positions they leave for the code-length code's Kraft test -- about 1 in 9 -- are compacted
+// into a wave list and tested one per lane: the HCLEN + 4 three-bit lengths as one 57-bit field,
+// summed by five lookups of a 4,096-entry table of the Kraft sums of four lengths (kr4).  About 30
+// operations per such position (round 4; a bit-sliced Kraft test at every position took 451 per
+// 32 positions).  A pass takes at most FIND_TAKE positions per lane (a dense pattern takes more
+// passes).
 constexpr uint32_t FIND_TAKE = 8;
 constexpr uint32_t FIND_CLIST = 64 * FIND_TAKE;
-constexpr uint32_t FIND_CCAP = 1024;               // survivors kept per workgroup (131,072 positions; ~65 on average)
+constexpr uint32_t FIND_CCAP = 1024;               // survivors listed in LDS per workgroup (131,072 positions; ~65 on average)
 struct FindWaveScratch {
     uint32_t w[64 + 4];                            // the wave's words and the three after them
     uint16_t list[FIND_CLIST];                     // lane << 5 | bit of each position to test
 };
 // (survivors go to the workgroup's LDS list as 32-bit offsets from bit `pb`, bit 31 set: dynamic)
+// (a workgroup's survivors past the LDS list's FIND_CCAP go straight to the global list, one global
+// atomic each -- periodic bit patterns can pass the filters every few bits, and a dropped survivor
+// would be a real header lost at random)
+__device__ __forceinline__ void find_spill(uint64_t v, uint64_t* qlist, uint32_t* qcount, uint32_t qcap) {
+    const uint32_t g = atomicAdd(qcount, 1u);
+    if (g < qcap) qlist[g] = v;
+}
 __device__ __forceinline__ void find_word_wave(const In& in, uint64_t t, uint64_t scan_end, uint32_t* cand,
-                                               uint32_t* ncand, FindWaveScratch& fw, const uint16_t* kr4, uint64_t pb) {
+                                               uint32_t* ncand, FindWaveScratch& fw, const uint16_t* kr4, uint64_t pb,
+                                               uint64_t* qlist, uint32_t* qcount, uint32_t qcap) {
     const uint64_t nbits = in.nbits;
     const int lane = threadIdx.x & 63;
     const uint64_t p0 = t * 32;
@@ -452,7 +389,7 @@ __device__ __forceinline__ void find_word_wave(const In& in, uint64_t t, uint64_
     const uint32_t h4 = (uint32_t)(W >> 4), h5 = (uint32_t)(W >> 5), h6 = (uint32_t)(W >> 6),
                    h7 = (uint32_t)(W >> 7), d9 = (uint32_t)(W >> 9), d10 = (uint32_t)(W >> 10),
                    d11 = (uint32_t)(W >> 11), d12 = (uint32_t)(W >> 12);
-    const uint32_t big = (NDFL_BOP3(h4, h5, h6, 0x80) & h7) | (NDFL_BOP3(d9, d10, d11, 0x80) & d12);
+    const uint32_t big = (h4 & h5 & h6 & h7) | (d9 & d10 & d11 & d12);     // HLIT or HDIST >= 30
     const uint32_t pm = ~b1 & b2 & valid & notfinal & ~big;         // before the Kraft test
     // stored headers: LEN == ~NLEN (as find_word)
     const uint64_t W12 = (uint64_t)w1 | ((uint64_t)w2 << 32);
@@ -474,6 +411,7 @@ __device__ __forceinline__ void find_word_wave(const In& in, uint64_t t, uint64_
         if (p0 + al + 32 + 8ull * ln <= nbits) {
             uint32_t k = atomicAdd(ncand, 1u);
             if (k < FIND_CCAP) cand[k] = (uint32_t)(p0 + o - pb);
+            else find_spill(p0 + o, qlist, qcount, qcap);
         }
     }
     // dynamic headers
@@ -521,6 +459,7 @@ __device__ __forceinline__ void find_word_wave(const In& in, uint64_t t, uint64_
             if (ks == 128 && p + 17 + 3 * ncl <= nbits) {
                 uint32_t k = atomicAdd(ncand, 1u);
                 if (k < FIND_CCAP) cand[k] = (uint32_t)(p - pb) | (1u << 31);
+                else find_spill(p | (1ull << 63), qlist, qcount, qcap);
             }
         }
         __builtin_amdgcn_wave_barrier();                             // (the list is rewritten next)
@@ -536,38 +475,7 @@ __device__ __forceinline__ void kr4_fill(uint16_t* kr4) {
     }
 }
 
-// the workgroup's LDS survivors -> the global survivor list (one global atomic)
-__device__ __forceinline__ void find_flush(const uint64_t* cand, const uint32_t* ncand, uint32_t* gbase,
-                                           uint64_t* qlist, uint32_t* qcount, uint32_t qcap) {
-    __syncthreads();
-    const uint32_t nc = min(*ncand, 2048u);
-    if (threadIdx.x == 0) *gbase = nc ? atomicAdd(qcount, nc) : 0u;
-    __syncthreads();
-    for (uint32_t k = threadIdx.x; k < nc; k += blockDim.x)
-        if (*gbase + k < qcap) qlist[*gbase + k] = cand[k];
-}
 }  // namespace inf
-
-extern "C" __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(NDFL_FIND_WPE)))
-ndfl_inflate_find_kernel(const uint32_t* w, uint64_t nwords, uint64_t nbits, uint64_t* qlist, uint32_t* qcount,
-                         uint32_t qcap, uint32_t win_words, uint32_t period_words, uint64_t w_lo, uint64_t scan_end) {
-    using namespace inf;
-    __shared__ uint64_t cand[2048];
-    __shared__ uint32_t ncand, gbase;
-    if (threadIdx.x == 0) ncand = 0;
-    __syncthreads();
-    // scanned windows: win_words of every period_words input words (win == period: every position)
-    // (FIND_WPT words per thread, so that one group's survivors cost one global atomic)
-    In in{w, nwords, nbits};
-    for (uint32_t kk = 0; kk < FIND_WPT; kk++) {
-        const uint64_t tt = ((uint64_t)blockIdx.x * FIND_WPT + kk) * blockDim.x + threadIdx.x;
-        // input word index; the scan covers bit positions [w_lo * 32, scan_end) of the stream
-        const uint64_t t = win_words == period_words ? w_lo + tt    // every position (the default): no division
-                                                     : w_lo + (tt / win_words) * period_words + tt % win_words;
-        find_word(in, t, scan_end, cand, &ncand);
-    }
-    find_flush(cand, &ncand, &gbase, qlist, qcount, qcap);
-}
 
 // The dense scan with the compacted Kraft test (find_word_wave): every position of [w_lo * 32, scan_end).
 extern "C" __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(NDFL_FIND_WPE)))
@@ -585,7 +493,7 @@ ndfl_inflate_find_compact_kernel(const uint32_t* w, uint64_t nwords, uint64_t nb
     const uint64_t pb = (w_lo + (uint64_t)blockIdx.x * FIND_WPT * 256) * 32;    // the workgroup's first bit
     for (uint32_t kk = 0; kk < FIND_WPT; kk++) {
         const uint64_t tt = ((uint64_t)blockIdx.x * FIND_WPT + kk) * blockDim.x + threadIdx.x;
-        find_word_wave(in, w_lo + tt, scan_end, cand, &ncand, fws[threadIdx.x >> 6], kr4, pb);
+        find_word_wave(in, w_lo + tt, scan_end, cand, &ncand, fws[threadIdx.x >> 6], kr4, pb, qlist, qcount, qcap);
     }
     // the workgroup's LDS survivors -> the global survivor list (one global atomic)
     __syncthreads();
@@ -598,86 +506,7 @@ ndfl_inflate_find_compact_kernel(const uint32_t* w, uint64_t nwords, uint64_t nb
     }
 }
 
-// Partitioned finder (long streams): the scanned range is cut into partitions of part_words input
-// words, and launch `iter` scans window `iter` (FIND_WPT * 256 words) of every partition that has
-// no accepted header yet (done[], set by the strict stage).  So each partition is scanned only up to
-// its first block header -- about half a block on average -- instead of every bit position, and the
-// decode chains start at those headers (a chain decodes on through the block boundaries that are not
-// candidates, to the next partition's header).  One workgroup per partition and window.
-extern "C" __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(NDFL_FIND_WPE)))
-ndfl_inflate_find_sparse_kernel(const uint32_t* w, uint64_t nwords, uint64_t nbits, uint64_t* qlist, uint32_t* qcount,
-                                uint32_t qcap, uint64_t w_lo, uint64_t scan_end, uint32_t part_words, uint32_t iter,
-                                const uint32_t* done, uint32_t* last_win) {
-    using namespace inf;
-    __shared__ uint64_t cand[2048];
-    __shared__ uint32_t ncand, gbase;
-    const uint32_t part = blockIdx.x;
-    if (done[part]) return;                                    // workgroup-uniform
-    if (threadIdx.x == 0) last_win[part] = iter;
-    const uint64_t pw0 = w_lo + (uint64_t)part * part_words;
-    const uint64_t wb = pw0 + (uint64_t)iter * FIND_WPT * 256;
-    const uint64_t we = min(pw0 + part_words, (scan_end + 31) / 32);
-    if (wb >= we) return;
-    if (threadIdx.x == 0) ncand = 0;
-    __syncthreads();
-    In in{w, nwords, nbits};
-    for (uint32_t kk = 0; kk < FIND_WPT; kk++) {
-        const uint64_t t = wb + (uint64_t)kk * blockDim.x + threadIdx.x;
-        if (t < we) find_word(in, t, scan_end, cand, &ncand);
-    }
-    find_flush(cand, &ncand, &gbase, qlist, qcount, qcap);
-}
-
-// Completion of the partitioned scan: a partition is scanned in full after all when the window in
-// which its first header was found holds two or more (short blocks: a chain through the partition
-// would decode many blocks one after another), or when that header's block is expensive --
-// phase-locked literal codes (the count pass decodes such blocks from all 8 bit phases) or a high
-// expansion.  Its blocks then become chains of their own, so the chains' costs stay balanced; such
-// regions are cheap to scan (few bits per block, or a small share of the stream).  Workgroup
-// (partition, window).
-extern "C" __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(NDFL_FIND_WPE)))
-ndfl_inflate_find_fill_kernel(const uint32_t* w, uint64_t nwords, uint64_t nbits, uint64_t* qlist, uint32_t* qcount,
-                              uint32_t qcap, uint64_t w_lo, uint64_t scan_end, uint32_t part_words, uint32_t wpp,
-                              const uint32_t* done, const uint32_t* last_win) {
-    using namespace inf;
-    __shared__ uint64_t cand[2048];
-    __shared__ uint32_t ncand, gbase;
-    const uint32_t part = blockIdx.x / wpp, win = blockIdx.x % wpp;
-    const uint32_t st = done[part];
-    if (!((st & PART_EXPENSIVE) || (st & 0xFFFFu) >= 2u) || win <= last_win[part]) return;   // workgroup-uniform
-    const uint64_t pw0 = w_lo + (uint64_t)part * part_words;
-    const uint64_t wb = pw0 + (uint64_t)win * FIND_WPT * 256;
-    const uint64_t we = min(pw0 + part_words, (scan_end + 31) / 32);
-    if (wb >= we) return;
-    if (threadIdx.x == 0) ncand = 0;
-    __syncthreads();
-    In in{w, nwords, nbits};
-    for (uint32_t kk = 0; kk < FIND_WPT; kk++) {
-        const uint64_t t = wb + (uint64_t)kk * blockDim.x + threadIdx.x;
-        if (t < we) find_word(in, t, scan_end, cand, &ncand);
-    }
-    find_flush(cand, &ncand, &gbase, qlist, qcount, qcap);
-}
-
 namespace inf {
-// Prefix sums over the length symbols 257 + k (k = 0..28) of their run base (RUN_LENGTH_TABLE,
-// D/decomp/Open.java:841-850) and extra-bit counts: the strict stage's expansion estimate of a
-// header (expected output bytes per stream bit under the code's own symbol probabilities 2^-len).
-struct LenPrefix { uint32_t base[30], extra[30]; };
-constexpr LenPrefix make_len_prefix() {
-    LenPrefix t{};
-    uint32_t b = 0, x = 0;
-    for (uint32_t k = 0; k < 29; k++) {
-        t.base[k] = b; t.extra[k] = x;
-        const uint32_t ne = k < 8 || k == 28 ? 0u : (k >> 2) - 1;
-        const uint32_t base = k < 8 ? k + 3 : k == 28 ? 258u : ((4u + (k & 3)) << ne) + 3;
-        b += base; x += ne;
-    }
-    t.base[29] = b; t.extra[29] = x;
-    return t;
-}
-__device__ constexpr LenPrefix LEN_PREFIX = make_len_prefix();
-
 // strict-stage reader: 64-bit buffer, the next 16-byte group always in flight
 struct SRd {
     uint64_t bb, pos, qw;
@@ -728,15 +557,17 @@ struct SRd {
 // through a per-lane 128-entry table of the code-length code (LDS, indexed by the next 7 bits
 // MSB first: canonical codes fill it in (length, symbol) order).  Accepted headers go to their
 // 64 KiB segment's list.
-// PART: the partitioned finder's variant (done != nullptr: per-partition header counts and cost
-// classes); the dense scan's variant keeps no class state (its registers would spill).
-template <bool PART>
-__device__ __forceinline__ void strict_stage(const uint32_t* w, uint64_t nwords, uint64_t nbits, const uint64_t* qlist,
-                                             const uint32_t* qcount, uint32_t qcap, uint32_t* seg_cnt,
-                                             uint64_t* seg_list, uint32_t* ticket, unsigned long long* sst,
-                                             uint32_t* done, uint64_t part_base, uint64_t part_bits) {
+// No scratch memory (tests/test_kernel_resources.py checks it): builds that used scratch here -- a
+// call to a non-inlined strict_stored (its stack), or register spills at 5 waves/SIMD -- rejected
+// 2-4 % of the real headers at full load, a different set on every run, while the same builds
+// without scratch accepted exactly the oracle's set in every run.  Hence
+// strict_stored is inlined, the code-length code's lengths travel as one 57-bit field, and the
+// table build is a rolled loop: 94 VGPRs, no spills, 5 waves/SIMD.
+extern "C" __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(NDFL_STRICT_WPE)))
+ndfl_inflate_strict_kernel(const uint32_t* w, uint64_t nwords, uint64_t nbits, const uint64_t* qlist,
+                           const uint32_t* qcount, uint32_t qcap, uint32_t* seg_cnt, uint64_t* seg_list,
+                           uint32_t* ticket, unsigned long long* sst) {
     using namespace inf;
-    if (!PART) done = nullptr;
     __shared__ uint4 tabs[256 * 8];                          // 128 bytes per lane
     uint8_t* tab = (uint8_t*)&tabs[threadIdx.x * 8];
     const uint32_t n = min(*qcount, qcap);
@@ -751,7 +582,6 @@ __device__ __forceinline__ void strict_stage(const uint32_t* w, uint64_t nwords,
         const uint32_t seg = (uint32_t)(p / ((uint64_t)SEG_BYTES * 8));
         const uint32_t idx = atomicAdd(&seg_cnt[seg], 1u);
         if (idx < SEG_CAP) seg_list[(uint64_t)seg * SEG_CAP + idx] = p;
-        if (done) atomicAdd(&done[(p - part_base) / part_bits], 1u);  // partitioned finder: headers found
     };
     bool active = false;
     uint64_t p = 0;
@@ -759,9 +589,6 @@ __device__ __forceinline__ void strict_stage(const uint32_t* w, uint64_t nwords,
     rd.bb = 0; rd.pos = 0; rd.qw = 0; rd.bn = 0; rd.ci = 0;
     uint32_t i = 0, total = 0, numLit = 0, numDist = 0, litK = 0, distK = 0, ones = 0, other = 0, eob = 0, d0 = 0,
              d31 = 0;
-    // partitioned finder: the header's cost class -- phase-locked literal codes (the count pass's
-    // 8-phase rounds) or a high expansion (many blocks / many output bytes per stream bit)
-    uint32_t n8 = 0, e_bytes = 0, e_bits = 0;
     int runVal = -1;
     uint64_t n_iter = 0, n_refill = 0, n_steps = 0;      // NDFL_STATS (sst != nullptr)
     for (;;) {
@@ -789,12 +616,12 @@ __device__ __forceinline__ void strict_stage(const uint32_t* w, uint64_t nwords,
                         const uint32_t hlit = rd.get(in, 5), hdist = rd.get(in, 5), hclen = rd.get(in, 4);
                         numLit = hlit + 257; numDist = hdist + 1; total = numLit + numDist;
                         const uint32_t numCl = hclen + 4;
-                        uint32_t cl[19];
-#pragma unroll
-                        for (int j = 0; j < 19; j++) cl[j] = 0;
+                        // the numCl 3-bit code-length code lengths in stream (CLO) order as one field
+                        // (two registers where a per-symbol array held 19 at the refill's peak)
+                        uint64_t F = 0;
 #pragma unroll
                         for (int j = 0; j < 19; j++)
-                            if ((uint32_t)j < numCl) cl[CLO[j]] = rd.get(in, 3);
+                            if ((uint32_t)j < numCl) F |= (uint64_t)rd.get(in, 3) << (3 * j);
                         // the stage-1 test guarantees a complete code: the runs fill all 128 entries
                         // canonical (length, symbol) order without a pass per length: each length's
                         // first entry is the byte-wise exclusive prefix sum of count x run, all seven
@@ -803,17 +630,18 @@ __device__ __forceinline__ void strict_stage(const uint32_t* w, uint64_t nwords,
                         uint32_t kraft = 0;
 #pragma unroll
                         for (int sy = 0; sy < 19; sy++) {
-                            wp += cl[sy] ? ((uint64_t)(128u >> cl[sy]) << (8 * cl[sy])) : 0ull;
-                            kraft += cl[sy] ? (128u >> cl[sy]) : 0u;
+                            const uint32_t l = (uint32_t)(F >> (3 * CLO_INV[sy])) & 7u;
+                            wp += l ? ((uint64_t)(128u >> l) << (8 * l)) : 0ull;
+                            kraft += l ? (128u >> l) : 0u;
                         }
                         // the byte-wise sums only hold for a complete code (every prefix <= 128): a
                         // stage-1 regression must not let an incomplete code scribble over the
                         // neighbouring lanes' tables, so such a survivor is dropped here
                         const bool complete = kraft == 128u;
                         uint64_t off = (wp * 0x0101010101010101ull) << 8;
-#pragma unroll
+#pragma unroll 1
                         for (int sy = 0; sy < 19; sy++) {
-                            const uint32_t l = cl[sy];
+                            const uint32_t l = (uint32_t)(F >> (3 * CLO_INV[sy])) & 7u;
                             if (l && complete) {
                                 const uint32_t sh = 8 * l, run = 128u >> l;
                                 const uint32_t pos = (uint32_t)(off >> sh) & 255u;
@@ -833,7 +661,6 @@ __device__ __forceinline__ void strict_stage(const uint32_t* w, uint64_t nwords,
                             }
                         }
                         i = 0; runVal = -1; litK = 0; distK = 0; ones = 0; other = 0; eob = 0; d0 = 0; d31 = 0;
-                        n8 = 0; e_bytes = 0; e_bits = 0;
                         active = complete;
                     }
                 }
@@ -870,16 +697,6 @@ __device__ __forceinline__ void strict_stage(const uint32_t* w, uint64_t nwords,
             const uint32_t v = (uint32_t)runVal;
             const uint32_t wt = v ? (32768u >> v) : 0u;
             litK += (min(en, numLit) - min(i, numLit)) * wt;
-            if (PART) {
-                // symbols [i, min(en, numLit)) of the literal/length code, all of length v
-                const uint32_t a = min(i, numLit), b = min(en, numLit);
-                const uint32_t nl = min(b, 256u) - min(a, 256u);
-                const uint32_t la = min(max(a, 257u), 286u) - 257u, lb = min(max(b, 257u), 286u) - 257u;
-                const uint32_t w8 = wt >> 4;                          // 2^-v in units of 2^-11
-                n8 += v == 8 ? b - a : 0u;
-                e_bytes += w8 * (nl + LEN_PREFIX.base[lb] - LEN_PREFIX.base[la]);
-                e_bits += w8 * (v * (b - a) + LEN_PREFIX.extra[lb] - LEN_PREFIX.extra[la] + 5u * (lb - la));
-            }
             const uint32_t da = max(i, numLit) - numLit, db = max(en, numLit) - numLit, cd = db - da;
             distK += cd * wt;
             ones += v == 1 ? cd : 0u;
@@ -896,12 +713,7 @@ __device__ __forceinline__ void strict_stage(const uint32_t* w, uint64_t nwords,
                 else if (numDist == 1 && d0 == 0) ok = true;
                 else if (ones == 1 && other == 0) ok = !(numDist == 32 && d31 == 1);
                 else ok = distK == 32768u;
-                if (ok) {
-                    record(p);
-                    // phase-locked literal codes, or more than 2 output bytes per stream bit
-                    if (PART && (n8 >= 192u || e_bytes > 2u * e_bits))
-                        atomicOr(&done[(p - part_base) / part_bits], PART_EXPENSIVE);
-                }
+                if (ok) record(p);
             }
         }
         const uint64_t am = __ballot(active);
@@ -917,21 +729,6 @@ __device__ __forceinline__ void strict_stage(const uint32_t* w, uint64_t nwords,
         atomicAdd(&sst[3], 1ull);
     }
 }
-extern "C" __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(NDFL_STRICT_WPE)))
-ndfl_inflate_strict_kernel(const uint32_t* w, uint64_t nwords, uint64_t nbits, const uint64_t* qlist,
-                           const uint32_t* qcount, uint32_t qcap, uint32_t* seg_cnt, uint64_t* seg_list,
-                           uint32_t* ticket, unsigned long long* sst) {
-    strict_stage<false>(w, nwords, nbits, qlist, qcount, qcap, seg_cnt, seg_list, ticket, sst, nullptr, 0, 1);
-}
-extern "C" __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(NDFL_STRICT_WPE)))
-ndfl_inflate_strict_part_kernel(const uint32_t* w, uint64_t nwords, uint64_t nbits, const uint64_t* qlist,
-                                const uint32_t* qcount, uint32_t qcap, uint32_t* seg_cnt, uint64_t* seg_list,
-                                uint32_t* ticket, unsigned long long* sst, uint32_t* done, uint64_t part_base,
-                                uint64_t part_bits) {
-    strict_stage<true>(w, nwords, nbits, qlist, qcount, qcap, seg_cnt, seg_list, ticket, sst, done, part_base,
-                       part_bits);
-}
-
 // Sort each segment's candidates (arrival order is arbitrary) and compact them into one sorted
 // list at the offsets of an exclusive scan of the segment counts.
 extern "C" __global__ void __launch_bounds__(256)
@@ -1260,8 +1057,8 @@ struct InflateScratch {
     size_t d_hrec_cap = 0;
     void* d_cticket = nullptr;                        // count pass: chain tickets (one per launch)
     void* d_out = nullptr; size_t d_out_cap = 0;
-    void* d_done = nullptr; size_t d_done_cap = 0;    // partitioned finder: header found per partition
-    uint64_t find_parts = 0, find_part_bits = 0;
+    Knobs knobs;                                       // the context's switches (ndfl_common.hpp)
+    uint32_t q_cap = 0, q_min = 0;                    // finder survivor list: capacity of the last scan / asked minimum
     double last_ms_find = 0, last_ms_count = 0, last_ms_emit = 0, last_ms_wall = 0;
     hipEvent_t ev[6] = {nullptr, nullptr, nullptr, nullptr, nullptr, nullptr};
     uint64_t repairs = 0, chains = 0, candidates = 0, resolved_groups = 0;
@@ -1273,10 +1070,10 @@ struct InflateScratch {
     // state kept for ndfl_inflate_resolve after a deferred-window range decode
     bool pending = false;
     uint8_t* p_out = nullptr;
-    uint64_t p_nbytes = 0;
+    uint64_t p_nbytes = 0, p_dict_len = 0;
     void release() {
         void** ps[] = {&d_in, &d_cand, &d_starts, &d_stops, &d_res, &d_cands, &d_stats, &d_q, &d_seg, &d_chains, &d_off,
-                       &d_ref, &d_pend, &d_rl, &d_ticket, &d_ph, &d_cticket, &d_out, &d_done, &d_hrec, &d_slow, &d_rep};
+                       &d_ref, &d_pend, &d_rl, &d_ticket, &d_ph, &d_cticket, &d_out, &d_hrec, &d_slow, &d_rep};
         for (void** p : ps) { if (*p) hipFree(*p); *p = nullptr; }
         for (auto& e : ev) { if (e) hipEventDestroy(e); e = nullptr; }
         if (h_cnt) hipHostFree(h_cnt);
@@ -1288,7 +1085,7 @@ struct InflateScratch {
         if (d_link) hipFree(d_link);
         d_link = nullptr; d_link_cap = 0;
         d_in_cap = d_cand_cap = d_starts_cap = d_stops_cap = d_res_cap = d_cands_cap = d_seg_cap = d_q_cap = d_chains_cap = 0;
-        d_off_cap = d_ref_cap = d_pend_cap = d_rl_cap = d_out_cap = d_done_cap = d_hrec_cap = 0;
+        d_off_cap = d_ref_cap = d_pend_cap = d_rl_cap = d_out_cap = d_hrec_cap = 0;
         pending = false;
     }
 };
@@ -1308,9 +1105,8 @@ static uint32_t wave_grid(K kernel, uint32_t cap, const char* env = nullptr) {
 // The count pass: one wave per chain (W = 1) or W waves per chain (workgroup rounds,
 // inflate_wg.hpp); NDFL_COUNT_W selects W (1, 2, 4, 8).  Persistent grid sized by occupancy; the
 // phase-fallback slots (d_ph) cover COUNT_WAVES waves.
-static uint32_t count_w() {                    // (read per decode: the tests switch it)
-    const char* e = getenv("NDFL_COUNT_W");
-    const uint32_t v = e ? (uint32_t)atoi(e) : (uint32_t)NDFL_COUNT_W_DEFAULT;
+static uint32_t count_w(const Knobs& k) {
+    const uint32_t v = k.count_w ? k.count_w : (uint32_t)NDFL_COUNT_W_DEFAULT;
     return (v == 2 || v == 4 || v == 8) ? v : 1u;
 }
 template <typename K>
@@ -1353,6 +1149,7 @@ static bool inf_debug() { static const bool d = getenv("NDFL_DEBUG") != nullptr;
         if (inf_debug()) fprintf(stderr, "[ndfl] HIP error %d (%s) at inflate_kernels.hip:%d\n", (int)_e,     \
                                  hipGetErrorString(_e), __LINE__);                                              \
         return -4; } } while (0)
+#define INF_RC(x) do { const int _r = (x); if (_r) return _r; } while (0)
 
 // Resolve the deferred copies of an emit pass: pointer-jumping rounds over the pending 32-byte
 // groups of out[0, nbytes) until none is left.  *groups = pending groups at the start.
@@ -1379,7 +1176,7 @@ static int resolve_rounds(InflateScratch& S, hipStream_t s, uint8_t* d_out, uint
     int cur = 0;
     uint32_t n = 0;
     for (int round = 0;; round++) {
-        static const bool rstats = getenv("NDFL_STATS") != nullptr;
+        const bool rstats = S.knobs.stats;
         if ((round & 3) == 0 || rstats) {
             INF_CHK(hipMemcpyAsync(h, cnt + cur, 4, hipMemcpyDeviceToHost, s));
             if (rstats) INF_CHK(hipMemcpyAsync(h + 1, cnt + 2 + cur, 4, hipMemcpyDeviceToHost, s));
@@ -1411,7 +1208,7 @@ static int setup_pool(InflateScratch& S, hipStream_t s, uint64_t nstarts, uint64
     const uint64_t nslot = nstarts + std::max<uint64_t>(4096, nstarts / 2);
     const uint64_t nrec = std::min<uint64_t>(0xFFFFFFF0ull, 2 * nstarts + nbits / (wv::MAX_SPAN / 2) + 65536);
     // table records: at most one per block; bounded (a stream of tiny blocks parses the rest again)
-    const uint64_t nbt = std::min<uint64_t>(nrec, getenv("NDFL_NO_BT") ? 0 : (1u << 18));
+    const uint64_t nbt = std::min<uint64_t>(nrec, S.knobs.no_bt ? 0 : (1u << 18));
     const uint64_t seg_bytes = nrec * (64 * 8 + 64 * 4 + sizeof(SegMeta)) + nslot * 4 + 64 + nbt * BT_BYTES;
     INF_CHK(inf_ensure(&S.d_seg, &S.d_seg_cap, seg_bytes));
     SegPool pool;
@@ -1468,6 +1265,8 @@ static int resolve_rounds_dev(InflateScratch& S, hipStream_t s, uint8_t* d_out, 
 }
 
 constexpr int LINK_FALLBACK = 1000;      // the device-side path hands over to the host path
+constexpr int FIND_OVERFLOW = 1001;      // more finder survivors than the list held: scan again
+constexpr uint32_t LI_QCOUNT = 14;       // (host copy only: the finder's survivor count)
 
 // The decode after the header finder with everything on the device and ONE host synchronization
 // in the middle (the number of chain starts, which sizes the record pool and the grids) and one at
@@ -1500,7 +1299,7 @@ static int inflate_devlink(InflateScratch& S, hipStream_t s, const uint32_t* d_w
                        dim3(256), 0, s, (const uint64_t*)d_sorted, info, start_bit, end_bit, (uint64_t*)S.d_cands);
     INF_CHK(hipGetLastError());
     // stored-header aliases counted once (NDFL_NO_ALIAS: every candidate counted)
-    const bool alias_on = !getenv("NDFL_NO_ALIAS");
+    const bool alias_on = !S.knobs.no_alias;
     uint32_t* d_rep = nullptr;
     if (alias_on) {
         INF_CHK(inf_ensure(&S.d_rep, &S.d_rep_cap, (size_t)cap_all * 4 + 64));
@@ -1510,21 +1309,19 @@ static int inflate_devlink(InflateScratch& S, hipStream_t s, const uint32_t* d_w
         INF_CHK(hipGetLastError());
     }
     INF_CHK(hipMemcpyAsync((void*)hinfo, info, (LI_NREP + 1) * 8, hipMemcpyDeviceToHost, s));
+    hinfo[LI_QCOUNT] = 0;
+    INF_CHK(hipMemcpyAsync((void*)(hinfo + LI_QCOUNT), (const uint32_t*)S.d_stats + 8, 4, hipMemcpyDeviceToHost, s));
     INF_CHK(hipStreamSynchronize(s));                          // (1) the number of chain starts
+    if ((uint32_t)hinfo[LI_QCOUNT] > S.q_cap) { S.q_min = (uint32_t)hinfo[LI_QCOUNT] + 65536; return FIND_OVERFLOW; }
     const uint64_t n = hinfo[LI_NCAND];
-    if (const char* dump = getenv("NDFL_DUMP_CANDS")) {        // (diagnostics: the sorted candidate list)
-        std::vector<uint64_t> hc(n);
-        INF_CHK(hipMemcpy(hc.data(), S.d_cands, n * 8, hipMemcpyDeviceToHost));
-        if (FILE* f = fopen(dump, "wb")) { fwrite(hc.data(), 8, n, f); fclose(f); }
-    }
     // the count pass's width: one wave per chain, unless the chains to count are few against the
     // count waves (fewer than 4 per wave), where a chain's rounds in sequence bound the pass (config
     // 2: fixed-Huffman pieces between stored blocks: 4 waves per chain count it in 2.0 ms instead of
     // 4.0; the bench's 66,770 chains: one wave each) -- NDFL_COUNT_W overrides
     const uint64_t nrep = alias_on ? hinfo[LI_NREP] : n;
     static const uint32_t count_waves = wave_grid(ndfl_inflate_count_wave_kernel, COUNT_WAVES, "NDFL_COUNT_WPC");
-    const uint32_t W = getenv("NDFL_COUNT_W") ? count_w() : (nrep < 4ull * count_waves && nbits >= (1ull << 24)) ? 4u : 1u;
-    if (getenv("NDFL_STATS")) fprintf(stderr, "[ndfl] count pass: %llu candidates, %llu counted, width %u\n",
+    const uint32_t W = S.knobs.count_w ? count_w(S.knobs) : (nrep < 4ull * count_waves && nbits >= (1ull << 24)) ? 4u : 1u;
+    if (S.knobs.stats) fprintf(stderr, "[ndfl] count pass: %llu candidates, %llu counted, width %u\n",
                                       (unsigned long long)n, (unsigned long long)nrep, W);
     if (n == 0 || n > (1ull << 24)) return LINK_FALLBACK;
     const uint32_t ncand = (uint32_t)n;
@@ -1541,10 +1338,10 @@ static int inflate_devlink(InflateScratch& S, hipStream_t s, const uint32_t* d_w
                        d_order, (const uint32_t*)d_rep, alias_on ? d_nord : (uint32_t*)nullptr);
     INF_CHK(hipGetLastError());
     if (!S.d_ph) INF_CHK(hipMalloc(&S.d_ph, (size_t)std::max(COUNT_WAVES, EMIT_WAVES) * sizeof(wv::PhArr)));
-    static const bool stats_on = getenv("NDFL_STATS") != nullptr;
+    const bool stats_on = S.knobs.stats;
     const uint64_t limit = std::min(end_bit, nbits);
     INF_CHK(hipEventRecord(S.ev[2], s));
-    static const bool hrec_on = !getenv("NDFL_NO_HDRREC");
+    const bool hrec_on = !S.knobs.no_hdrrec;
     if (hrec_on) {
         INF_CHK(inf_ensure(&S.d_hrec, &S.d_hrec_cap, (size_t)ncand * sizeof(wv::HdrRec)));
         hipLaunchKernelGGL(ndfl_inflate_hdr_kernel, dim3((ncand + 63) / 64), dim3(64), 0, s, d_w, nwords, nbits,
@@ -1568,17 +1365,15 @@ static int inflate_devlink(InflateScratch& S, hipStream_t s, const uint32_t* d_w
         std::vector<ChainRes> cr(ncand);
         INF_CHK(hipMemcpyAsync(cr.data(), S.d_res, ncand * sizeof(ChainRes), hipMemcpyDeviceToHost, s));
         INF_CHK(hipStreamSynchronize(s));
-        uint64_t cnt[3] = {0, 0, 0}, tsum[3] = {0, 0, 0}, tmax[3] = {0, 0, 0}, blk[3] = {0, 0, 0}, bits[3] = {0, 0, 0};
+        uint64_t cnt[3] = {0, 0, 0}, tsum[3] = {0, 0, 0}, tmax[3] = {0, 0, 0}, blk[3] = {0, 0, 0};
         for (uint32_t k = 0; k < ncand; k++) {
             const uint32_t st = std::min<uint32_t>(cr[k].status, 2u), t = cr[k].pad >> 16;
             cnt[st]++; tsum[st] += t; tmax[st] = std::max<uint64_t>(tmax[st], t); blk[st] += cr[k].pad & 0xFFFFu;
-            bits[st] += cr[k].end_bit - std::min(cr[k].end_bit, (uint64_t)0) ;
         }
         const char* nm[3] = {"boundary", "final", "error"};
         for (int k = 0; k < 3; k++)
             fprintf(stderr, "[ndfl] count chains %s: %llu, wave time %.2f ms (max %.3f ms), blocks %llu\n", nm[k],
                     (unsigned long long)cnt[k], tsum[k] * 1e-2, tmax[k] * 1e-2, (unsigned long long)blk[k]);
-        (void)bits;
     }
     // linking: J levels (u32), S and D double-buffered
     uint32_t nlev = 1;
@@ -1634,9 +1429,9 @@ static int inflate_devlink(InflateScratch& S, hipStream_t s, const uint32_t* d_w
     INF_CHK(hipMemsetAsync(S.d_ticket, 0, 64, s));
     INF_CHK(hipEventRecord(S.ev[4], s));
     static const uint32_t emit_grid = wave_grid(ndfl_inflate_emit_wave_kernel, EMIT_WAVES, "NDFL_EMIT_WPC");
-    // NDFL_EMIT_FAST (default 1): the record-replay emit kernel first, the full one over what it leaves
-    const char* efe = getenv("NDFL_EMIT_FAST");
-    if (!efe || atoi(efe)) {
+    // the record-replay emit kernel first, the full one over what it leaves (NDFL_EMIT_FAST=0: the
+    // full one alone)
+    if (S.knobs.emit_fast) {
         INF_CHK(inf_ensure(&S.d_slow, &S.d_slow_cap, (size_t)ncand * 4 + 64));
         uint32_t* tk = (uint32_t*)S.d_ticket;             // [0] fast tickets, [4] full tickets, [8] slow count
         static const uint32_t fast_grid = wave_grid(ndfl_inflate_emit_fast_kernel, EMIT_WAVES, "NDFL_EMITF_WPC");
@@ -1709,7 +1504,7 @@ static int inflate_devlink(InflateScratch& S, hipStream_t s, const uint32_t* d_w
         hipEventElapsedTime(&c, S.ev[4], S.ev[5]);
         S.last_ms_find = a; S.last_ms_count = b; S.last_ms_emit = c;
     }
-    if (deferred) { S.pending = true; S.p_out = d_out; S.p_nbytes = dict_len + hinfo[LI_TOTAL]; }
+    if (deferred) { S.pending = true; S.p_out = d_out; S.p_nbytes = dict_len + hinfo[LI_TOTAL]; S.p_dict_len = dict_len; }
     INF_CHK(hipEventRecord(S.ev[5], s));
     INF_CHK(hipStreamSynchronize(s));
     float w = 0;
@@ -1722,6 +1517,118 @@ static int inflate_devlink(InflateScratch& S, hipStream_t s, const uint32_t* d_w
     *out_len = produced;
     *consumed_bits = hinfo[LI_CONSUMED];
     return code;
+}
+
+// The decoder's input words: staged into a zero-padded scratch copy, so the decode lanes' 16-byte
+// prefetches (up to IN_PAD bytes past the end) need no bounds checks -- unless the caller says its
+// device buffer already is one (NDFL_IN_PADDED: 16-byte aligned, IN_PAD zero bytes after the data),
+// in which case it is read in place.
+static int stage_input(InflateScratch& S, hipStream_t s, const uint8_t* in, uint64_t in_len, uint32_t flags,
+                       const uint32_t** d_w) {
+    using namespace inf;
+    const uint64_t nwords = (in_len + 3) / 4;
+    const bool in_place = in_len && (flags & 1u) && (flags & 8u) && ((uintptr_t)in & 15u) == 0;
+    *d_w = (const uint32_t*)in;
+    if (!in_place) {
+        INF_CHK(inf_ensure(&S.d_in, &S.d_in_cap, nwords * 4 + IN_PAD));
+        if (in_len) INF_CHK(hipMemcpyAsync(S.d_in, in, in_len, (flags & 1u) ? hipMemcpyDeviceToDevice : hipMemcpyHostToDevice, s));
+        INF_CHK(hipMemsetAsync((char*)S.d_in + in_len, 0, nwords * 4 + IN_PAD - in_len, s));
+        *d_w = (const uint32_t*)S.d_in;
+    }
+    return 0;
+}
+
+// The header finder phase: every bit position of [start_bit, min(end_bit, nbits)) tested for a
+// block header (finder: cheap masks + the code-length code's Kraft test), the survivors checked by
+// the reference's own header rules (strict stage), the accepted ones into the per-segment lists
+// d_list / d_cnt (SEG_BYTES of input each).  S.d_stats and d_cnt must be zeroed.
+static int find_headers(InflateScratch& S, hipStream_t s, const uint32_t* d_w, uint64_t nwords, uint64_t nbits,
+                        uint64_t start_bit, uint64_t end_bit, uint32_t* d_cnt, uint64_t* d_list) {
+    using namespace inf;
+    // only the range's own bits are scanned: candidates outside [start_bit, end_bit) are dropped
+    // later anyway (a range decode of one stream shard, or a sync probe)
+    const uint64_t scan_end = std::min(end_bit, nbits);
+    const uint64_t w_lo = start_bit >> 5;
+    const uint64_t nw32 = scan_end > w_lo * 32 ? (scan_end + 31) / 32 - w_lo : 0;
+    // (about one survivor per 1,000 positions on real streams; a longer list is scanned again
+    // with room for all of it, so no survivor is dropped: FIND_OVERFLOW)
+    const uint32_t qcap = (uint32_t)std::min<uint64_t>(0x7FFFFFFFull, std::max<uint64_t>(nbits / 256 + 65536, S.q_min));
+    S.q_cap = qcap;
+    INF_CHK(inf_ensure(&S.d_q, &S.d_q_cap, (uint64_t)qcap * 8 + 64));
+    uint32_t* d_qcount = (uint32_t*)S.d_stats + 8;
+    uint64_t* d_qlist = (uint64_t*)((char*)S.d_q + 64);
+    static const uint32_t strict_grid = [] {
+        int dev = 0, ncu = 0, per = 0;
+        if (hipGetDevice(&dev) != hipSuccess ||
+            hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess ||
+            hipOccupancyMaxActiveBlocksPerMultiprocessor(&per, ndfl_inflate_strict_kernel, 256, 0) != hipSuccess ||
+            ncu <= 0 || per <= 0)
+            return 1280u;
+        return (uint32_t)(ncu * per);
+    }();
+    unsigned long long* sst = S.knobs.stats ? (unsigned long long*)((uint32_t*)S.d_stats + 16) : nullptr;
+    if (nw32) {
+        const uint32_t fgrid = (uint32_t)((nw32 + 256 * FIND_WPT - 1) / (256 * FIND_WPT));
+        hipLaunchKernelGGL(ndfl_inflate_find_compact_kernel, dim3(fgrid), dim3(256), 0, s, d_w, nwords, nbits, d_qlist,
+                           d_qcount, qcap, w_lo, scan_end);
+        INF_CHK(hipGetLastError());
+        hipLaunchKernelGGL(ndfl_inflate_strict_kernel, dim3(strict_grid), dim3(256), 0, s, d_w, nwords, nbits,
+                           (const uint64_t*)d_qlist, (const uint32_t*)d_qcount, qcap, d_cnt, d_list,
+                           (uint32_t*)S.d_stats + 10, sst);
+        INF_CHK(hipGetLastError());
+    }
+    return 0;
+}
+
+// Diagnostics (ndfl_inflate_headers): the finder phase alone over a whole stream.  out = the accepted
+// headers in ascending order (the per-segment lists, each capped at SEG_CAP, as the decode sees
+// them); surv = the finder's survivors (unsorted, bit 63 = dynamic); stats[0] survivors found,
+// [1] headers accepted before the cap, [2] segments over SEG_CAP, [3] survivors past the list's
+// capacity (dropped).
+static int inflate_headers(InflateScratch& S, hipStream_t s, const uint8_t* in, uint64_t in_len, uint32_t flags,
+                           uint64_t* out, uint64_t cap, uint64_t* n_out, uint64_t* surv, uint64_t surv_cap,
+                           uint64_t* stats) {
+    using namespace inf;
+    const uint64_t nbits = in_len * 8, nwords = (in_len + 3) / 4;
+    const uint32_t* d_w = nullptr;
+    INF_RC(stage_input(S, s, in, in_len, flags, &d_w));
+    if (!S.d_stats) INF_CHK(hipMalloc(&S.d_stats, 512));
+    const uint32_t nseg = (uint32_t)std::max<uint64_t>(1, (in_len + SEG_BYTES - 1) / SEG_BYTES);
+    INF_CHK(inf_ensure(&S.d_cand, &S.d_cand_cap, (uint64_t)nseg * SEG_CAP * 8ull + (uint64_t)nseg * 4 + 64));
+    uint64_t* d_list = (uint64_t*)S.d_cand;
+    uint32_t* d_cnt = (uint32_t*)((char*)S.d_cand + (uint64_t)nseg * SEG_CAP * 8ull);
+    std::vector<uint32_t> cnt(nseg);
+    std::vector<uint64_t> lists((uint64_t)nseg * SEG_CAP);
+    uint32_t qc = 0;
+    for (int finds = 0; finds < 2; finds++) {                   // (as inflate_run: FIND_OVERFLOW scans again)
+        INF_CHK(hipMemsetAsync(S.d_stats, 0, 512, s));
+        INF_CHK(hipMemsetAsync(d_cnt, 0, (uint64_t)nseg * 4, s));
+        INF_RC(find_headers(S, s, d_w, nwords, nbits, 0, NONE, d_cnt, d_list));
+        INF_CHK(hipMemcpyAsync(&qc, (uint32_t*)S.d_stats + 8, 4, hipMemcpyDeviceToHost, s));
+        INF_CHK(hipStreamSynchronize(s));
+        if (qc <= S.q_cap) break;
+        S.q_min = qc + 65536;
+    }
+    INF_CHK(hipMemcpyAsync(cnt.data(), d_cnt, nseg * 4ull, hipMemcpyDeviceToHost, s));
+    INF_CHK(hipMemcpyAsync(lists.data(), d_list, lists.size() * 8, hipMemcpyDeviceToHost, s));
+    INF_CHK(hipStreamSynchronize(s));
+    const uint32_t qcap = S.q_cap;
+    std::vector<uint64_t> acc;
+    uint64_t total = 0, over = 0;
+    for (uint32_t k = 0; k < nseg; k++) {
+        total += cnt[k];
+        over += cnt[k] > SEG_CAP;
+        for (uint32_t i = 0; i < std::min(cnt[k], SEG_CAP); i++) acc.push_back(lists[(uint64_t)k * SEG_CAP + i]);
+    }
+    std::sort(acc.begin(), acc.end());
+    *n_out = acc.size();
+    if (out) memcpy(out, acc.data(), std::min<uint64_t>(cap, acc.size()) * 8);
+    if (surv && surv_cap) {
+        const uint64_t ns = std::min<uint64_t>(std::min<uint64_t>(qc, qcap), surv_cap);
+        if (ns) INF_CHK(hipMemcpy(surv, (const char*)S.d_q + 64, ns * 8, hipMemcpyDeviceToHost));
+    }
+    if (stats) { stats[0] = qc; stats[1] = total; stats[2] = over; stats[3] = qc > qcap ? qc - qcap : 0; }
+    return 0;
 }
 
 // Decode one raw DEFLATE stream, or the block-aligned range [start_bit, end_bit) of one.
@@ -1737,137 +1644,43 @@ static int inflate_run(InflateScratch& S, hipStream_t s, const uint8_t* in, uint
     *out_len = 0;
     *consumed_bits = 0;
     S.pending = false;
-    static const bool htime = getenv("NDFL_HOST_TIMES") != nullptr;
+    const bool htime = S.knobs.host_times;
     auto hnow = []() { return std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now().time_since_epoch()).count(); };
     double ht[8] = {hnow(), 0, 0, 0, 0, 0, 0, 0};
     const uint64_t nbits = in_len * 8;
     const uint64_t nwords = (in_len + 3) / 4;
     if (start_bit > nbits) return -1;
-    // input words: staged into a zero-padded scratch copy, so the decode lanes' 16-byte prefetches
-    // (up to IN_PAD bytes past the end) need no bounds checks -- unless the caller says its device
-    // buffer already is one (NDFL_IN_PADDED: 16-byte aligned, IN_PAD zero bytes after the data),
-    // in which case it is read in place
-    const bool in_place = in_len && (flags & 1u) && (flags & 8u) && ((uintptr_t)in & 15u) == 0;
-    const uint32_t* d_w = (const uint32_t*)in;
-    if (!in_place) {
-        INF_CHK(inf_ensure(&S.d_in, &S.d_in_cap, nwords * 4 + IN_PAD));
-        if (in_len) INF_CHK(hipMemcpyAsync(S.d_in, in, in_len, (flags & 1u) ? hipMemcpyDeviceToDevice : hipMemcpyHostToDevice, s));
-        INF_CHK(hipMemsetAsync((char*)S.d_in + in_len, 0, nwords * 4 + IN_PAD - in_len, s));
-        d_w = (const uint32_t*)S.d_in;
-    }
+    const uint32_t* d_w = nullptr;
+    INF_RC(stage_input(S, s, in, in_len, flags, &d_w));
     if (!S.d_stats) INF_CHK(hipMalloc(&S.d_stats, 512));
-    INF_CHK(hipMemsetAsync(S.d_stats, 0, 512, s));
     if (!S.ev[0]) for (auto& e : S.ev) INF_CHK(hipEventCreate(&e));
+    int finds = 0;
+refind:
+    INF_CHK(hipMemsetAsync(S.d_stats, 0, 512, s));
     const uint32_t nseg = (uint32_t)std::max<uint64_t>(1, (in_len + SEG_BYTES - 1) / SEG_BYTES);
     INF_CHK(inf_ensure(&S.d_cand, &S.d_cand_cap, (uint64_t)nseg * SEG_CAP * 8ull + (uint64_t)nseg * 4 + 64));
     uint64_t* d_list = (uint64_t*)S.d_cand;
     uint32_t* d_cnt = (uint32_t*)((char*)S.d_cand + (uint64_t)nseg * SEG_CAP * 8ull);
     INF_CHK(hipMemsetAsync(d_cnt, 0, (uint64_t)nseg * 4, s));
     INF_CHK(hipEventRecord(S.ev[0], s));
-    {
-        // sparse windows: chains then span a few blocks (the count pass decodes on through
-        // boundaries that are not candidates); every window holds a block start unless blocks
-        // are longer than the gap, in which case chains just get longer
-        // only the range's own bits are scanned: candidates outside [start_bit, end_bit) are
-        // dropped below anyway (a range decode of one stream shard, or a sync probe)
-        const uint64_t scan_end = std::min(end_bit, nbits);
-        const uint64_t w_lo = start_bit >> 5;
-        const uint64_t nw32 = scan_end > w_lo * 32 ? (scan_end + 31) / 32 - w_lo : 0;
-        static const uint32_t env_win = getenv("NDFL_FIND_WIN") ? (uint32_t)atoi(getenv("NDFL_FIND_WIN")) : 0;
-        static const uint32_t env_per = getenv("NDFL_FIND_PERIOD") ? (uint32_t)atoi(getenv("NDFL_FIND_PERIOD")) : 0;
-        const uint32_t period = env_per ? env_per : FIND_PERIOD_WORDS, win = env_win ? env_win : FIND_WIN_WORDS;
-        const uint64_t nwin = (nw32 + period - 1) / period;
-        const uint64_t nthr = nw32 <= (uint64_t)period ? nw32 : (nwin - 1) * win + std::min<uint64_t>(win, nw32 - (nwin - 1) * period);
-        const uint32_t qcap = (uint32_t)std::min<uint64_t>(0x7FFFFFFFull, nbits / 256 + 65536);
-        INF_CHK(inf_ensure(&S.d_q, &S.d_q_cap, (uint64_t)qcap * 8 + 64));
-        uint32_t* d_qcount = (uint32_t*)S.d_stats + 8;
-        uint64_t* d_qlist = (uint64_t*)((char*)S.d_q + 64);
-        static const uint32_t strict_grid = [] {
-            int dev = 0, ncu = 0, per = 0;
-            if (hipGetDevice(&dev) != hipSuccess ||
-                hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess ||
-                hipOccupancyMaxActiveBlocksPerMultiprocessor(&per, ndfl_inflate_strict_kernel, 256, 0) != hipSuccess ||
-                ncu <= 0 || per <= 0)
-                return 1280u;
-            return (uint32_t)(ncu * per);
-        }();
-        unsigned long long* sst = getenv("NDFL_STATS") ? (unsigned long long*)((uint32_t*)S.d_stats + 16) : nullptr;
-        // partitioned scan (opt-in, NDFL_FIND_PART_BITS = partition bits or "auto"): each partition is
-        // scanned only up to its first header, plus the rest of it where blocks are short or expensive.
-        // Not the default: a decode chain's cost goes with its blocks and output bytes, not its bits,
-        // and chains through partitions ran up to 20 ms against 4.5 ms for one block
-        const uint64_t wg_words = (uint64_t)FIND_WPT * 256;
-        uint64_t part_words = 0;
-        {
-            static const uint32_t count_waves = wave_grid(ndfl_inflate_count_wave_kernel, COUNT_WAVES, "NDFL_COUNT_WPC");
-            const char* pe = getenv("NDFL_FIND_PART_BITS");               // read per call (tests switch it)
-            if (pe && !strcmp(pe, "auto")) part_words = nw32 / (4ull * count_waves);
-            else if (pe) part_words = (uint64_t)strtoull(pe, nullptr, 10) / 32;
-            part_words = part_words / wg_words * wg_words;
-            if (part_words < 2 * wg_words || part_words >= nw32) part_words = 0;    // dense
-        }
-        S.find_parts = 0;
-        if (nthr && part_words) {
-            const uint64_t nparts = (nw32 + part_words - 1) / part_words;
-            if (nparts > 0x7FFFFFFFull) return -2;
-            INF_CHK(inf_ensure(&S.d_done, &S.d_done_cap, nparts * 8 + 64));
-            INF_CHK(hipMemsetAsync(S.d_done, 0, nparts * 4, s));
-            const uint32_t iters = (uint32_t)((part_words + wg_words - 1) / wg_words);
-            uint32_t* d_last = (uint32_t*)S.d_done + nparts;
-            for (uint32_t it = 0; it < iters; it++) {
-                INF_CHK(hipMemsetAsync(d_qcount, 0, 12, s));              // survivor count, (pad), strict ticket
-                hipLaunchKernelGGL(ndfl_inflate_find_sparse_kernel, dim3((uint32_t)nparts), dim3(256), 0, s, d_w, nwords,
-                                   nbits, d_qlist, d_qcount, qcap, w_lo, scan_end, (uint32_t)part_words, it,
-                                   (const uint32_t*)S.d_done, d_last);
-                INF_CHK(hipGetLastError());
-                hipLaunchKernelGGL(ndfl_inflate_strict_part_kernel, dim3(strict_grid), dim3(256), 0, s, d_w, nwords, nbits,
-                                   (const uint64_t*)d_qlist, (const uint32_t*)d_qcount, qcap, d_cnt, d_list,
-                                   (uint32_t*)S.d_stats + 10, sst, (uint32_t*)S.d_done, w_lo * 32, part_words * 32);
-                INF_CHK(hipGetLastError());
-            }
-            // short-block / expensive partitions: the rest of their windows
-            INF_CHK(hipMemsetAsync(d_qcount, 0, 12, s));
-            hipLaunchKernelGGL(ndfl_inflate_find_fill_kernel, dim3((uint32_t)(nparts * iters)), dim3(256), 0, s, d_w,
-                               nwords, nbits, d_qlist, d_qcount, qcap, w_lo, scan_end, (uint32_t)part_words, iters,
-                               (const uint32_t*)S.d_done, (const uint32_t*)d_last);
-            INF_CHK(hipGetLastError());
-            hipLaunchKernelGGL(ndfl_inflate_strict_kernel, dim3(strict_grid), dim3(256), 0, s, d_w, nwords, nbits,
-                               (const uint64_t*)d_qlist, (const uint32_t*)d_qcount, qcap, d_cnt, d_list,
-                               (uint32_t*)S.d_stats + 10, sst);
-            INF_CHK(hipGetLastError());
-            S.find_parts = nparts;
-            S.find_part_bits = part_words * 32;
-        } else if (nthr) {
-            // every position (the default): the compacted Kraft test (NDFL_FIND_BITSLICED=1: the
-            // bit-sliced one, A/B); windows of the stream: the bit-sliced finder
-            static const bool bitsliced = getenv("NDFL_FIND_BITSLICED") != nullptr;
-            const uint32_t fgrid = (uint32_t)((nthr + 256 * FIND_WPT - 1) / (256 * FIND_WPT));
-            if (NDFL_FIND_COMPACT && win == period && !bitsliced)
-                hipLaunchKernelGGL(ndfl_inflate_find_compact_kernel, dim3(fgrid), dim3(256), 0, s, d_w, nwords, nbits, d_qlist,
-                                   d_qcount, qcap, w_lo, scan_end);
-            else
-                hipLaunchKernelGGL(ndfl_inflate_find_kernel, dim3(fgrid), dim3(256), 0, s, d_w,
-                                   nwords, nbits, d_qlist, d_qcount, qcap, win, period, w_lo, scan_end);
-            INF_CHK(hipGetLastError());
-            hipLaunchKernelGGL(ndfl_inflate_strict_kernel, dim3(strict_grid), dim3(256), 0, s, d_w, nwords, nbits,
-                               (const uint64_t*)d_qlist, (const uint32_t*)d_qcount, qcap, d_cnt, d_list,
-                               (uint32_t*)S.d_stats + 10, sst);
-            INF_CHK(hipGetLastError());
-        }
-    }
+    INF_RC(find_headers(S, s, d_w, nwords, nbits, start_bit, end_bit, d_cnt, d_list));
     INF_CHK(hipEventRecord(S.ev[1], s));
     // the device-side path (NDFL_HOST_LINK selects the host's linking); sync probes keep the host's
     {
-        static const bool host_link = getenv("NDFL_HOST_LINK") != nullptr;
+        const bool host_link = S.knobs.host_link;
         if (!probe_sync && !host_link) {
             const int rc = inflate_devlink(S, s, d_w, nwords, nbits, nseg, d_cnt, d_list, start_bit, end_bit, out,
                                            dict_len, out_cap, out_len, consumed_bits, flags, deferred, partial, last_ms);
-            if (rc != LINK_FALLBACK) return rc;
+            if (rc == FIND_OVERFLOW && finds++ == 0) goto refind;
+            if (rc != LINK_FALLBACK && rc != FIND_OVERFLOW) return rc;
         }
     }
     std::vector<uint32_t> hcnt(nseg);
+    uint32_t hqc = 0;
     INF_CHK(hipMemcpyAsync(hcnt.data(), d_cnt, nseg * 4ull, hipMemcpyDeviceToHost, s));
+    INF_CHK(hipMemcpyAsync(&hqc, (const uint32_t*)S.d_stats + 8, 4, hipMemcpyDeviceToHost, s));
     INF_CHK(hipStreamSynchronize(s));
+    if (hqc > S.q_cap && finds++ == 0) { S.q_min = hqc + 65536; goto refind; }
     std::vector<uint64_t> hoff(nseg + 1);
     hoff[0] = 1;                                   // slot 0 is the range start
     for (uint32_t k = 0; k < nseg; k++) hoff[k + 1] = hoff[k] + std::min(hcnt[k], SEG_CAP);
@@ -1901,7 +1714,7 @@ static int inflate_run(InflateScratch& S, hipStream_t s, const uint8_t* in, uint
     const uint64_t nslot = starts.size() + std::max<uint64_t>(4096, starts.size() / 2);
     const uint64_t nrec = std::min<uint64_t>(0xFFFFFFF0ull, 2 * starts.size() + nbits / (wv::MAX_SPAN / 2) + 65536);
     // table records: at most one per block; bounded (a stream of tiny blocks parses the rest again)
-    const uint64_t nbt = std::min<uint64_t>(nrec, getenv("NDFL_NO_BT") ? 0 : (1u << 18));
+    const uint64_t nbt = std::min<uint64_t>(nrec, S.knobs.no_bt ? 0 : (1u << 18));
     const uint64_t seg_bytes = nrec * (64 * 8 + 64 * 4 + sizeof(SegMeta)) + nslot * 4 + 64 + nbt * BT_BYTES;
     INF_CHK(inf_ensure(&S.d_seg, &S.d_seg_cap, seg_bytes));
     SegPool pool;
@@ -1918,7 +1731,7 @@ static int inflate_run(InflateScratch& S, hipStream_t s, const uint8_t* in, uint
     S.pool = pool;
     INF_CHK(hipMemsetAsync(pool.head, 0xFF, nslot * 4, s));
 
-    static const bool stats_on = getenv("NDFL_STATS") != nullptr;
+    const bool stats_on = S.knobs.stats;
     std::vector<ChainRes> res;
     auto run_count = [&](const std::vector<uint64_t>& st, std::vector<ChainRes>& r) -> int {
         const uint64_t slot_base = starts.size() - (&st == &starts ? st.size() : 0);
@@ -1956,7 +1769,7 @@ static int inflate_run(InflateScratch& S, hipStream_t s, const uint8_t* in, uint
         if (!S.d_cticket) INF_CHK(hipMalloc(&S.d_cticket, 64));
         INF_CHK(hipMemsetAsync(S.d_cticket, 0, 4, s));
         if (S.count_first) INF_CHK(hipEventRecord(S.ev[2], s));
-        launch_count(s, count_w(), (uint32_t)n,
+        launch_count(s, count_w(S.knobs), (uint32_t)n,
                            d_w, nwords, nbits,
                            (const uint64_t*)S.d_starts, (const uint64_t*)S.d_stops, (uint32_t)n,
                            (const uint64_t*)S.d_cands, ncand, limit, (ChainRes*)S.d_res, stats_on ? (uint32_t*)S.d_stats : nullptr,
@@ -1990,15 +1803,7 @@ static int inflate_run(InflateScratch& S, hipStream_t s, const uint8_t* in, uint
         }
         return 0;
     }
-    if (getenv("NDFL_STATS") && !probe_sync && S.find_parts) {
-        unsigned long long sc[8];
-        INF_CHK(hipMemcpy(sc, (const uint32_t*)S.d_stats + 16, sizeof(sc), hipMemcpyDeviceToHost));
-        const uint64_t range_words = (std::min(end_bit, nbits) + 31) / 32 - (start_bit >> 5);
-        fprintf(stderr, "[ndfl] partitioned finder: %llu partitions of %llu bits, %.1f %% of the range scanned\n",
-                (unsigned long long)S.find_parts, (unsigned long long)S.find_part_bits,
-                range_words ? 100.0 * (double)sc[4] / (double)range_words : 0.0);
-    }
-    if (getenv("NDFL_STATS") && !probe_sync) {
+    if (S.knobs.stats && !probe_sync) {
         // the most expensive chains (wave time, blocks, bits, output bytes)
         std::vector<size_t> idx(res.size());
         for (size_t k = 0; k < idx.size(); k++) idx[k] = k;
@@ -2007,12 +1812,9 @@ static int inflate_run(InflateScratch& S, hipStream_t s, const uint8_t* in, uint
                           [&](size_t a, size_t b) { return (res[a].pad >> 16) > (res[b].pad >> 16); });
         for (size_t t = 0; t < top; t++) {
             const ChainRes& r = res[idx[t]];
-            const uint64_t pk = S.find_parts ? (starts[idx[t]] - (start_bit & ~31ull)) / S.find_part_bits : 0;
-            fprintf(stderr, "[ndfl] count chain %zu: %.2f ms, %u blocks, start %llu, %llu bits, %llu bytes, status %u; "
-                    "partition %llu\n",
+            fprintf(stderr, "[ndfl] count chain %zu: %.2f ms, %u blocks, start %llu, %llu bits, %llu bytes, status %u\n",
                     idx[t], (r.pad >> 16) * 0.01, r.pad & 0xFFFFu, (unsigned long long)starts[idx[t]],
-                    (unsigned long long)(r.end_bit - starts[idx[t]]), (unsigned long long)r.out_count, r.status,
-                    (unsigned long long)pk);
+                    (unsigned long long)(r.end_bit - starts[idx[t]]), (unsigned long long)r.out_count, r.status);
         }
     }
     {
@@ -2092,7 +1894,7 @@ static int inflate_run(InflateScratch& S, hipStream_t s, const uint8_t* in, uint
     }
     S.chains = chains.size();
     S.candidates = sorted_cand.size();
-    if (getenv("NDFL_STATS")) {
+    if (S.knobs.stats) {
         uint32_t st[64] = {0};
         INF_CHK(hipMemcpy(st, S.d_stats, 256, hipMemcpyDeviceToHost));
         st[4] = st[8];
@@ -2107,10 +1909,9 @@ static int inflate_run(InflateScratch& S, hipStream_t s, const uint8_t* in, uint
                 "serial %.1f record %.1f build %.1f phase-mapped %.1f\n", t64[0] * 1e-5, t64[1] * 1e-5, t64[2] * 1e-5, t64[3] * 1e-5,
                 t64[4] * 1e-5, t64[5] * 1e-5, t64[6] * 1e-5, t64[7] * 1e-5);
         const double span = (double)(t64[9] - ~t64[10]);
-        fprintf(stderr, "[ndfl] count waves %llu: busy %.1f ms x waves, span %.3f ms, occupancy %.3f, longest chain %.3f ms; "
-                "finder partitions %llu\n",
+        fprintf(stderr, "[ndfl] count waves %llu: busy %.1f ms x waves, span %.3f ms, occupancy %.3f, longest chain %.3f ms\n",
                 (unsigned long long)t64[11], t64[8] * 1e-5, span * 1e-5, t64[11] ? t64[8] / (span * t64[11]) : 0.0,
-                t64[12] * 1e-5, (unsigned long long)S.find_parts);
+                t64[12] * 1e-5);
     }
     const uint64_t total = off - dict_len;
     ht[3] = hnow();
@@ -2166,7 +1967,7 @@ static int inflate_run(InflateScratch& S, hipStream_t s, const uint8_t* in, uint
     }
     if (deferred) {
         S.pending = true;
-        S.p_out = d_out; S.p_nbytes = nbytes;
+        S.p_out = d_out; S.p_nbytes = nbytes; S.p_dict_len = dict_len;
     } else {
         uint64_t groups = 0;
         const int rr = resolve_rounds(S, s, d_out, nbytes, &groups);
@@ -2234,6 +2035,41 @@ ndfl_inflate_tail_kernel(const uint32_t* pend, const uint32_t* ref, const uint8_
         if (++steps > TAIL_STEPS) { atomicOr(fail, 1u); return; }
     }
     dst[k] = out[p];
+}
+
+// The same bytes as a map of the window: entry k = the window byte index its value comes from
+// (< dict_len), or TAIL_LITERAL | value for a byte that does not depend on the window.  Needs no
+// window content: GPU r's map composed with the maps of GPUs 0..r-1 gives its window directly.
+constexpr uint32_t TAIL_LITERAL = 0x80000000u;
+extern "C" __global__ void __launch_bounds__(256)
+ndfl_inflate_tail_map_kernel(const uint32_t* pend, const uint32_t* ref, const uint8_t* out, uint64_t t0, uint64_t n,
+                             uint64_t dict_len, uint32_t* dst, uint32_t* fail) {
+    const uint64_t k = (uint64_t)blockIdx.x * 256 + threadIdx.x;
+    if (k >= n) return;
+    uint64_t p = t0 + k;
+    uint32_t steps = 0;
+    while ((pend[p >> 5] >> (p & 31)) & 1) {
+        p -= ref[p];
+        if (++steps > TAIL_STEPS) { atomicOr(fail, 1u); return; }
+    }
+    dst[k] = p < dict_len ? (uint32_t)p : TAIL_LITERAL | out[p];
+}
+
+static int inflate_tail_map(InflateScratch& S, hipStream_t s, uint64_t n, uint32_t* dst) {
+    if (!S.pending) return -5;
+    if (n > S.p_nbytes) return -1;
+    if (n == 0) return 0;
+    if (!S.h_cnt) INF_CHK(hipHostMalloc(&S.h_cnt, 64, 0));
+    uint32_t* d_fail = (uint32_t*)S.d_stats + 14;
+    INF_CHK(hipMemsetAsync(d_fail, 0, 4, s));
+    hipLaunchKernelGGL(ndfl_inflate_tail_map_kernel, dim3((uint32_t)((n + 255) / 256)), dim3(256), 0, s,
+                       (const uint32_t*)S.d_pend, (const uint32_t*)S.d_ref, (const uint8_t*)S.p_out, S.p_nbytes - n, n,
+                       S.p_dict_len, dst, d_fail);
+    INF_CHK(hipGetLastError());
+    uint32_t* h = (uint32_t*)S.h_cnt;
+    INF_CHK(hipMemcpyAsync(h + 8, d_fail, 4, hipMemcpyDeviceToHost, s));
+    INF_CHK(hipStreamSynchronize(s));
+    return h[8] ? -6 : 0;
 }
 
 static int inflate_tail(InflateScratch& S, hipStream_t s, uint64_t n, uint8_t* dst) {

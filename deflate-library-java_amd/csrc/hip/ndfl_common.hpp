@@ -3,6 +3,44 @@
 #pragma once
 #include <hip/hip_runtime.h>
 #include <stdint.h>
+#include <stdlib.h>
+#include <string.h>
+
+// Switches of a context, read once from the environment when the context is created
+// (ndfl_ctx_create).  None is needed in production: they select the decoder's hand-over paths for
+// the tests (EMIT_FAST, NO_BT, NO_ALIAS, COUNT_W), statistics for profiling (STATS, HOST_TIMES,
+// LZ_STATS), and the few A/B alternatives still measured against the defaults.
+struct Knobs {
+    bool stats = false;          // NDFL_STATS: per-pass counters and phase clocks to stderr
+    bool host_times = false;     // NDFL_HOST_TIMES: host-side timestamps of a decode
+    bool host_link = false;      // NDFL_HOST_LINK: the host's chain linking instead of the device's
+    bool no_hdrrec = false;      // NDFL_NO_HDRREC: chain-first headers parsed by lane 0 (no records)
+    bool emit_fast = true;       // NDFL_EMIT_FAST=0: the full emit kernel alone
+    bool no_bt = false;          // NDFL_NO_BT: no table records (every Huffman chain handed over)
+    bool no_alias = false;       // NDFL_NO_ALIAS: every stored-header alias counted
+    uint32_t count_w = 0;        // NDFL_COUNT_W: waves per chain in the count pass (0: automatic)
+    bool deflate_pf = true;      // NDFL_DEFLATE_PF=0: no L2 touch of the next chunk in the encoder
+    bool deflate_profile = false;  // NDFL_DEFLATE_PROFILE: per-phase encoder clocks (one-kernel encoder)
+    bool deflate_fused = false;  // NDFL_DEFLATE_FUSED: the one-kernel encoder instead of the split passes
+    bool lz_stats = false;       // NDFL_LZ_STATS
+    bool lz_chain = false;       // NDFL_LZ_SEARCH=chain: the round-3 hash-chain LZ77 search
+    int lz_lead = -1;            // NDFL_LZ_LEAD: parse-driven search lead-in (-1: default)
+    void read() {
+        auto on = [](const char* n) { const char* e = getenv(n); return e && strcmp(e, "0") != 0; };
+        auto num = [](const char* n, int dflt) { const char* e = getenv(n); return e ? atoi(e) : dflt; };
+        stats = on("NDFL_STATS"); host_times = on("NDFL_HOST_TIMES"); host_link = on("NDFL_HOST_LINK");
+        no_hdrrec = on("NDFL_NO_HDRREC");
+        emit_fast = num("NDFL_EMIT_FAST", 1) != 0;
+        no_bt = on("NDFL_NO_BT"); no_alias = on("NDFL_NO_ALIAS");
+        count_w = (uint32_t)num("NDFL_COUNT_W", 0);
+        deflate_pf = num("NDFL_DEFLATE_PF", 1) != 0; deflate_profile = on("NDFL_DEFLATE_PROFILE");
+        deflate_fused = on("NDFL_DEFLATE_FUSED");
+        lz_stats = on("NDFL_LZ_STATS");
+        const char* se = getenv("NDFL_LZ_SEARCH");
+        lz_chain = se && !strcmp(se, "chain");
+        lz_lead = num("NDFL_LZ_LEAD", -1);
+    }
+};
 
 #define NDFL_WAVE 64
 

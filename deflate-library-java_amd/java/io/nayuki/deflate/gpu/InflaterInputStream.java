@@ -182,7 +182,10 @@ public final class InflaterInputStream extends InputStream {
 				// no block completed: read more.  The next attempt re-decodes the incomplete block from
 				// its start, so it waits for at least as much new input again (or for the source to
 				// run dry, see readMore)
-				want = (int)Math.min(Integer.MAX_VALUE - 512L - MARK_SLACK, in.limit() + Math.max((long)batch, in.limit()));
+				final long cap = Integer.MAX_VALUE - 512L - MARK_SLACK;
+				if (in.limit() >= cap)   // the buffer cannot grow: without this, fill() would retry forever
+					throw new IOException("A single DEFLATE block needs more than " + cap + " bytes of input");
+				want = (int)Math.min(cap, in.limit() + Math.max((long)batch, in.limit()));
 				continue;
 			}
 			outPos = windowLen;

@@ -348,6 +348,29 @@ class Context:
               "ndfl_inflate_sync")
         return None if v.value == NO_END else v.value
 
+    def inflate_headers_raw(self, in_addr, in_len, flags, survivors=False):
+        """ndfl_inflate_headers (diagnostics): the decoder's chain starts, sorted; with survivors=True
+        also the finder's survivors.  Returns (headers, stats[, survivors])."""
+        L = load()
+        self._order()
+        n = ctypes.c_uint64(0)
+        st = (ctypes.c_uint64 * 4)()
+        check(L.ndfl_inflate_headers(self._h, in_addr, in_len, flags, None, 0, ctypes.byref(n), None, 0, st),
+              "ndfl_inflate_headers")
+        hs = (ctypes.c_uint64 * max(1, n.value))()
+        ns = min(st[0], 2 * in_len + 65536) if survivors else 0
+        sv = (ctypes.c_uint64 * max(1, ns))()
+        check(L.ndfl_inflate_headers(self._h, in_addr, in_len, flags, hs, n.value, ctypes.byref(n),
+                                     sv if ns else None, ns, st), "ndfl_inflate_headers")
+        res = (list(hs[:n.value]), list(st))
+        return res + (list(sv[:min(ns, st[0])]),) if survivors else res
+
+    def inflate_headers(self, data, survivors=False):
+        """inflate_headers_raw over a stream in host memory."""
+        data = bytes(data)
+        src = ctypes.create_string_buffer(data, max(1, len(data)))
+        return self.inflate_headers_raw(ctypes.addressof(src), len(data), 0, survivors)
+
     def inflate_resolve(self):
         """Finish a DICT_DEFERRED range decode once the window is written; returns re-emitted chains."""
         self._order()
@@ -364,6 +387,17 @@ class Context:
         if r == _lib.E_UNSUPPORTED:
             return False
         check(r, "ndfl_inflate_tail")
+        return True
+
+    def inflate_tail_map_raw(self, tail_len, dst_addr):
+        """ndfl_inflate_tail_map: the last tail_len output bytes of the pending DICT_DEFERRED decode
+        as a map of its window (u32 per byte at dst_addr, device memory: window index, or
+        TAIL_LITERAL | value); False if a reference chain is too long (NDFL_E_UNSUPPORTED)."""
+        self._order()
+        r = load().ndfl_inflate_tail_map(self._h, tail_len, ctypes.c_void_p(dst_addr))
+        if r == _lib.E_UNSUPPORTED:
+            return False
+        check(r, "ndfl_inflate_tail_map")
         return True
 
     def bits_shift_raw(self, in_addr, nbits, shift, out_addr, out_cap):

@@ -15,6 +15,7 @@ IN_PAD_BYTES = 256
 IN_PARTIAL = 16        # NDFL_IN_PARTIAL: the input is a prefix of the stream
 NEED_INPUT = 64        # NDFL_NEED_INPUT: a partial-input decode stopped at a block boundary
 NO_END = (1 << 64) - 1
+TAIL_LITERAL = 0x80000000   # NDFL_TAIL_LITERAL: a window-map entry that holds a byte value
 
 STRATEGIES = {"LITERAL_STATIC": 0, "LITERAL_DYNAMIC": 1, "RLE_STATIC": 2, "RLE_DYNAMIC": 3,
               "FULL_STATIC": 4, "FULL_DYNAMIC": 5, "UNCOMPRESSED": 6}
@@ -38,7 +39,7 @@ EXPORTS = ["ndfl_abi_version", "ndfl_error_string", "ndfl_ctx_create", "ndfl_ctx
            "ndfl_deflate_bound",
            "ndfl_inflate", "ndfl_inflate_range", "ndfl_inflate_resolve", "ndfl_bits_shift", "ndfl_crc32", "ndfl_adler32",
            "ndfl_crc32_combine", "ndfl_decide", "ndfl_compress_to", "ndfl_decision_free", "ndfl_inflate_sync",
-           "ndfl_inflate_tail"]
+           "ndfl_inflate_tail", "ndfl_inflate_headers", "ndfl_inflate_tail_map"]
 
 KIND_LZ77, KIND_UNCOMPRESSED = 0, 1
 
@@ -94,7 +95,10 @@ def load():
                                      u32]
     L.ndfl_inflate_resolve.argtypes = [vp, ctypes.POINTER(u64)]
     L.ndfl_inflate_tail.argtypes = [vp, u64, vp]
+    L.ndfl_inflate_tail_map.argtypes = [vp, u64, vp]
     L.ndfl_inflate_sync.argtypes = [vp, vp, u64, u64, u64, ctypes.POINTER(u64), u32]
+    L.ndfl_inflate_headers.argtypes = [vp, vp, u64, u32, ctypes.POINTER(u64), u64, ctypes.POINTER(u64),
+                                       ctypes.POINTER(u64), u64, ctypes.POINTER(u64)]
     L.ndfl_bits_shift.argtypes = [vp, vp, u64, u32, vp, u64, u32]
     L.ndfl_crc32.argtypes = [vp, ctypes.POINTER(u32), vp, u64, u32]
     L.ndfl_adler32.argtypes = [vp, ctypes.POINTER(u32), vp, u64, u32]

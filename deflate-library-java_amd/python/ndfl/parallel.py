@@ -16,9 +16,11 @@ on raw input (D/DeflaterOutputStream.java:119-137).  So rank r 
               inflate_split: each rank probes for a confirmed block boundary near its share of the
               bits (ndfl_inflate_sync), the seams are proven by the range decodes themselves.
   decompress  each rank decodes its seam-delimited bit range with a deferred window
-              (ndfl_inflate_range + NDFL_DICT_DEFERRED), all ranks in parallel; then the last
-              32 KiB of output pass from rank to rank (the reference's dictionary ring,
-              D/decomp/Open.java:592-603) and each rank re-emits only the blocks that read them
+              (ndfl_inflate_range + NDFL_DICT_DEFERRED), all ranks in parallel; then one
+              all_gather of every rank's last 32 KiB as a map of its window
+              (ndfl_inflate_tail_map) gives each rank its window (the reference's dictionary ring,
+              D/decomp/Open.java:592-603, carried across all earlier shards) by composing the
+              maps before it, and each rank re-emits only the blocks that read it
               (ndfl_inflate_resolve).
 
 The protocol is codec-agnostic: `DeviceCodec` runs it on the GPU through the C ABI; the CPU tests
@@ -85,6 +87,11 @@ class DeviceCodec:
         resolve; None if a reference chain is too long to follow (resolve first)."""
         t = self.empty(n)
         return t[:n] if self.ctx.inflate_tail_raw(n, t.data_ptr()) else None
+
+    def tail_map(self, n, dst):
+        """The last n output bytes of the pending deferred decode as a map of its window, into the
+        int32 tensor dst[:n] (ndfl_inflate_tail_map); False if a reference chain is too long."""
+        return self.ctx.inflate_tail_map_raw(n, dst.data_ptr())
 
     def sync(self, src, in_len, from_bit, window_bits):
         from . import IN_DEVICE
@@ -191,22 +198,79 @@ def deflate_shard(codec, dist, torch, shard, rank, world, *, strategy="RLE_DYNAM
     return Part(out, nbits, shift, bit_offsets, byte_offsets, hist if prev_h else None)
 
 
+TAIL_LITERAL = -(1 << 31)      # NDFL_TAIL_LITERAL as an int32 map entry: a byte value, not a window index
+
+
+def _all_gather_tensor(dist, torch, t, world):
+    """all_gather of one equal-size tensor per rank (gloo: staged through the host)."""
+    staged = _staged(dist, t)
+    src = t.cpu() if staged else t
+    lst = [torch.empty_like(src) for _ in range(world)]
+    dist.all_gather(lst, src)
+    return [x.to(t.device) for x in lst] if staged else lst
+
+
+def window_from_maps(torch, maps, lens, rank):
+    """Rank `rank`'s window from the tail maps of ranks 0..rank-1 (ndfl_inflate_tail_map): rank k's
+    last lens[k] output bytes as a function of its own window, composed from rank 0 on."""
+    w = None
+    for k in range(rank):
+        m = maps[k][:lens[k]].long()
+        lit = m < 0
+        vals = m & 0xFF
+        if w is not None:
+            vals = torch.where(lit, vals, w[torch.where(lit, torch.zeros_like(m), m)])
+        w = vals
+    return w.to(torch.uint8)
+
+
 def inflate_shard(codec, dist, torch, part, out, rank, world):
     """Decode this rank's range of the stream into out[dict_len:], out[:dict_len] = the window.
     Returns (code, out_len, dict_len): code 0 or the Reason+1 of the FIRST error in stream order
-    over all ranks (every rank returns the same code)."""
+    over all ranks (every rank returns the same code).
+
+    All ranks decode at once with a deferred window.  The window chain -- rank r's window is the
+    last 32 KiB of rank r-1's output, which depends on rank r-1's own window -- is then one
+    all_gather: each rank describes its last 32 KiB as a map of its window (ndfl_inflate_tail_map:
+    per byte a window index or a value), and rank r composes the maps of ranks 0..r-1 into its
+    window itself, so no rank waits for the one before it.  Only if some rank cannot describe its
+    tail (a back-reference chain longer than the map kernel follows) does the chain run rank by
+    rank (_window_chain)."""
     dict_len = min(WINDOW, part.byte_offsets[rank])
     deferred = rank > 0 and dict_len > 0
     code, olen, _ = codec.inflate_range(part.buf, part.nbytes, part.shift, part.shift + part.nbits, out, dict_len,
                                         deferred)
     if code < 0:
         raise RuntimeError(f"inflate_range failed: {code}")
-    # window chain: rank r-1's last 32 KiB of output -> rank r.  Rank r passes its own last 32 KiB
-    # on as soon as its window is in (ndfl_inflate_tail follows those bytes' references), and
-    # resolves the rest of its range after that, so the chain's step per rank is one small kernel
-    # and one message, not a whole resolve.
     nxt = min(WINDOW, part.byte_offsets[rank + 1]) if rank + 1 < world else 0
     end = dict_len + olen
+    m = torch.full((WINDOW,), TAIL_LITERAL, dtype=torch.int32, device=codec.device)
+    ok = 1
+    if nxt and code == 0 and end >= nxt:
+        if deferred:
+            ok = int(bool(codec.tail_map(nxt, m)))
+        else:
+            m[:nxt] = out[end - nxt:end].int() | TAIL_LITERAL
+    # (an error ends the stream here: the next rank gets a window of zeros, as the chain would)
+    flags = _gather_ints(dist, torch, code * 2 + ok, world, codec.device)
+    codes = [f >> 1 for f in flags]
+    if all(f & 1 for f in flags):
+        maps = _all_gather_tensor(dist, torch, m, world)
+        if deferred:
+            lens = [min(WINDOW, part.byte_offsets[k + 1]) for k in range(world - 1)]
+            out[:dict_len] = window_from_maps(torch, maps, lens, rank)
+            if code == 0:
+                codec.resolve()
+    else:
+        _window_chain(codec, dist, torch, out, rank, world, code, dict_len, end, nxt)
+    first = next((c for c in codes if c != 0), 0)
+    return first, olen, dict_len
+
+
+def _window_chain(codec, dist, torch, out, rank, world, code, dict_len, end, nxt):
+    """The window chain rank by rank: rank r-1's last 32 KiB of output -> rank r.  Rank r passes its
+    own last 32 KiB on as soon as its window is in (ndfl_inflate_tail follows those bytes'
+    references), and resolves the rest of its range after that."""
     sent = False
     if rank > 0 and dict_len:
         _recv(dist, out[:dict_len], rank - 1)
@@ -222,10 +286,6 @@ def inflate_shard(codec, dist, torch, part, out, rank, world):
             _send(dist, out[end - nxt:end].contiguous(), rank + 1)
         else:                                    # an error ends the stream here: keep the chain moving
             _send(dist, torch.zeros(nxt, dtype=torch.uint8, device=codec.device), rank + 1)
-    # first error in stream order
-    codes = _gather_ints(dist, torch, code, world, codec.device)
-    first = next((c for c in codes if c != 0), 0)
-    return first, olen, dict_len
 
 
 SYNC_WINDOW = 8 << 20          # bits a sync probe looks ahead (1 MiB of stream)

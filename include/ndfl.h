@@ -245,6 +245,20 @@ int ndfl_inflate_range(ndfl_ctx* ctx, const uint8_t* in, uint64_t in_len, uint64
  */
 int ndfl_inflate_sync(ndfl_ctx* ctx, const uint8_t* in, uint64_t in_len, uint64_t from_bit, uint64_t window_bits,
                       uint64_t* sync_bit, uint32_t flags);
+/*
+ * Diagnostics (no reference counterpart; used by the parity tests): the decoder's chain starts in
+ * the raw DEFLATE stream `in` -- the bit positions at which the header finder and the strict stage
+ * accept a block header, by the reference's own header checks (UncompressedBlock ctor
+ * D/decomp/Open.java:232-241, HuffmanBlock(true) :336-431) restricted to headers a chain may start
+ * at (BFINAL = 0; stored with zero padding, its LEN bytes in the input and a plausible next
+ * header; dynamic with HLIT, HDIST < 30).  headers[0, min(cap, *n_headers)) = the positions in
+ * ascending order, at most 256 per 64 KiB of input (the decoder's per-segment cap); survivors
+ * (optional) = the finder's survivors before the strict stage (bit 63 set: dynamic); stats
+ * (optional, 4 entries) = survivors found, headers accepted before the cap, segments over the cap,
+ * survivors dropped past the survivor list's capacity.  flags: NDFL_IN_DEVICE / NDFL_IN_PADDED.
+ */
+int ndfl_inflate_headers(ndfl_ctx* ctx, const uint8_t* in, uint64_t in_len, uint32_t flags, uint64_t* headers,
+                         uint64_t cap, uint64_t* n_headers, uint64_t* survivors, uint64_t surv_cap, uint64_t* stats);
 /* Finish the last NDFL_DICT_DEFERRED range decode on this context (NDFL_E_STATE if none). */
 int ndfl_inflate_resolve(ndfl_ctx* ctx, uint64_t* n_reemitted);
 /*
@@ -257,6 +271,17 @@ int ndfl_inflate_resolve(ndfl_ctx* ctx, uint64_t* n_reemitted);
  * a byte's back-reference chain is too long to follow (resolve first, then take the bytes from out).
  */
 int ndfl_inflate_tail(ndfl_ctx* ctx, uint64_t tail_len, uint8_t* dst);
+/*
+ * The window chain in one step: the same last tail_len bytes of the pending
+ * NDFL_DICT_DEFERRED decode as a map of its window, before the window is written: dst[k] (device
+ * memory, u32) = the window byte index (< dict_len) byte k's value comes from, or
+ * NDFL_TAIL_LITERAL | value for a byte that does not depend on the window.  Every GPU computes its
+ * map at once; an all-gather of the maps lets GPU r compose those of GPUs 0..r-1 into its window
+ * (Open's 32 KiB dictionary, D/decomp/Open.java:592-603, carried across all earlier shards)
+ * without waiting for GPU r-1.  Errors as ndfl_inflate_tail.
+ */
+#define NDFL_TAIL_LITERAL 0x80000000u
+int ndfl_inflate_tail_map(ndfl_ctx* ctx, uint64_t tail_len, uint32_t* dst);
 
 /*
  * Multi-GPU seam step for compression: place the first `nbits` bits of `in` at bit

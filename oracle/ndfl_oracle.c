@@ -746,6 +746,53 @@ static const int8_t  DIST_EXTRA[30] = {0,0,0,0,1,1,2,2,3,3,4,4,5,5,6,6,7,7,8,8,9
 
 typedef struct { uint8_t* out; uint64_t cap, n; } ob_t;
 
+/* HuffmanBlock(true) (D/decomp/Open.java:336-431): the dynamic header after BFINAL/BTYPE, with its
+ * exact check order.  *dt = NULL for the empty distance code (:398-401). */
+static int dynamic_header(br_t* r, int16_t* litTree, int16_t* distTree, int16_t* clTree, const int16_t** dt) {
+    uint32_t hlit, hdist, hclen, v;
+    int err, tl;
+#define HCHK(x) do { err = (x); if (err) return err; } while (0)
+    HCHK(br_bits(r, 5, &hlit)); HCHK(br_bits(r, 5, &hdist)); HCHK(br_bits(r, 4, &hclen));
+    int numLit = (int)hlit + 257, numDist = (int)hdist + 1, numCl = (int)hclen + 4;
+    uint8_t clLen[19]; memset(clLen, 0, sizeof clLen);
+    for (int i = 0; i < numCl; i++) { HCHK(br_bits(r, 3, &v)); clLen[CLC_ORDER[i]] = (uint8_t)v; }
+    HCHK(code_tree(clLen, 19, clTree, &tl));
+    uint8_t lens[320];
+    int total = numLit + numDist, runVal = -1;
+    for (int i = 0; i < total;) {
+        int sym;
+        HCHK(decode_sym(r, clTree, &sym));
+        if (sym < 16) { runVal = sym; lens[i++] = (uint8_t)sym; }
+        else {
+            int runLen;
+            if (sym == 16) {
+                if (runVal == -1) HCHK(OR_NO_PREVIOUS_CODE_LENGTH_TO_COPY);
+                HCHK(br_bits(r, 2, &v)); runLen = (int)v + 3;
+            } else if (sym == 17) { runVal = 0; HCHK(br_bits(r, 3, &v)); runLen = (int)v + 3; }
+            else { runVal = 0; HCHK(br_bits(r, 7, &v)); runLen = (int)v + 11; }
+            for (; runLen > 0; runLen--, i++) {
+                if (i >= total) HCHK(OR_CODE_LENGTH_CODE_OVER_FULL);
+                lens[i] = (uint8_t)runVal;
+            }
+        }
+    }
+    if (lens[256] == 0) HCHK(OR_END_OF_BLOCK_CODE_ZERO_LENGTH);
+    HCHK(code_tree(lens, numLit, litTree, &tl));
+    uint8_t dl[32]; int nd = numDist;
+    memcpy(dl, lens + numLit, (size_t)numDist);
+    if (nd == 1 && dl[0] == 0) { *dt = NULL; return 0; }    /* empty distance code :398-401 */
+    int one = 0, other = 0;
+    for (int i = 0; i < nd; i++) { if (dl[i] == 1) one++; else if (dl[i] > 1) other++; }
+    if (one == 1 && other == 0) {                            /* :411-425 */
+        for (int i = nd; i < 32; i++) dl[i] = 0;
+        nd = 32; dl[31] = 1;
+    }
+    HCHK(code_tree(dl, nd, distTree, &tl));
+    *dt = distTree;
+    return 0;
+#undef HCHK
+}
+
 /* One raw DEFLATE stream (or a block-aligned range of one): Open.read (:83-124) run to the end.
  * Range form (multi-GPU shards): decoding starts at bit `start_bit` with `dict_len` bytes of
  * preceding output available to copies (the reference's 32 KiB ring, :592-603), and stops at the
@@ -790,48 +837,8 @@ int or_inflate_range(const uint8_t* in, uint64_t in_len, uint64_t start_bit, uin
         }
         const int16_t* lt; const int16_t* dt;
         if (bt == 1) { lt = fixLit; dt = fixDist; }
-        else {                                               /* HuffmanBlock(true) :336-431 */
-            uint32_t hlit, hdist, hclen, v;
-            CHK(br_bits(&r, 5, &hlit)); CHK(br_bits(&r, 5, &hdist)); CHK(br_bits(&r, 4, &hclen));
-            int numLit = (int)hlit + 257, numDist = (int)hdist + 1, numCl = (int)hclen + 4;
-            uint8_t clLen[19]; memset(clLen, 0, sizeof clLen);
-            for (int i = 0; i < numCl; i++) { CHK(br_bits(&r, 3, &v)); clLen[CLC_ORDER[i]] = (uint8_t)v; }
-            int tl;
-            CHK(code_tree(clLen, 19, clTree, &tl));
-            uint8_t lens[320];
-            int total = numLit + numDist, runVal = -1;
-            for (int i = 0; i < total;) {
-                int sym;
-                CHK(decode_sym(&r, clTree, &sym));
-                if (sym < 16) { runVal = sym; lens[i++] = (uint8_t)sym; }
-                else {
-                    int runLen;
-                    if (sym == 16) {
-                        if (runVal == -1) CHK(OR_NO_PREVIOUS_CODE_LENGTH_TO_COPY);
-                        CHK(br_bits(&r, 2, &v)); runLen = (int)v + 3;
-                    } else if (sym == 17) { runVal = 0; CHK(br_bits(&r, 3, &v)); runLen = (int)v + 3; }
-                    else { runVal = 0; CHK(br_bits(&r, 7, &v)); runLen = (int)v + 11; }
-                    for (; runLen > 0; runLen--, i++) {
-                        if (i >= total) CHK(OR_CODE_LENGTH_CODE_OVER_FULL);
-                        lens[i] = (uint8_t)runVal;
-                    }
-                }
-            }
-            if (lens[256] == 0) CHK(OR_END_OF_BLOCK_CODE_ZERO_LENGTH);
-            CHK(code_tree(lens, numLit, litTree, &tl));
-            uint8_t dl[32]; int nd = numDist;
-            memcpy(dl, lens + numLit, (size_t)numDist);
-            if (nd == 1 && dl[0] == 0) dt = NULL;            /* empty distance code :398-401 */
-            else {
-                int one = 0, other = 0;
-                for (int i = 0; i < nd; i++) { if (dl[i] == 1) one++; else if (dl[i] > 1) other++; }
-                if (one == 1 && other == 0) {                /* :411-425 */
-                    for (int i = nd; i < 32; i++) dl[i] = 0;
-                    nd = 32; dl[31] = 1;
-                }
-                CHK(code_tree(dl, nd, distTree, &tl));
-                dt = distTree;
-            }
+        else {
+            CHK(dynamic_header(&r, litTree, distTree, clTree, &dt));
             lt = litTree;
         }
         for (;;) {                                           /* HuffmanBlock.read :446-618 */
@@ -1044,4 +1051,72 @@ int or_zlib_decompress(const uint8_t* in, uint64_t in_len, uint8_t* out, uint64_
     uint32_t expect = (uint32_t)in[p] << 24 | (uint32_t)in[p + 1] << 16 | (uint32_t)in[p + 2] << 8 | in[p + 3];
     if (or_adler32(1, out, *out_len) != expect) return OR_DECOMPRESSED_CHECKSUM_MISMATCH;
     return 0;
+}
+
+/* ------------------------------------------------------------------------------------------ */
+/* Decoder test support: the chain starts of the GPU decoder's header finder.                  */
+/* ------------------------------------------------------------------------------------------ */
+/* 64 bits from bit p on, LSB first (zeros past the input, as the GPU's zero-padded staging). */
+static uint64_t scan_win64(const uint8_t* in, uint64_t in_len, uint64_t p) {
+    uint64_t v = 0;
+    const uint64_t b = p >> 3;
+    for (int k = 7; k >= 0; k--) v = v << 8 | (b + (uint64_t)k < in_len ? in[b + k] : 0u);
+    const uint32_t sh = (uint32_t)(p & 7);
+    if (sh) v = v >> sh | (uint64_t)(b + 8 < in_len ? in[b + 8] : 0u) << (64 - sh);
+    return v;
+}
+
+/* The header after a stored block is plausible: not BTYPE 3; stored -> LEN == ~NLEN; dynamic ->
+ * a complete code-length code; fixed -> no check (bits past the input read as zeros). */
+static int scan_next_plausible(const uint8_t* in, uint64_t in_len, uint64_t q) {
+    const uint64_t h = scan_win64(in, in_len, q);
+    const uint32_t bt = (uint32_t)(h >> 1) & 3u;
+    if (bt == 3) return 0;
+    if (bt == 0) {
+        const uint64_t x = scan_win64(in, in_len, (q + 3 + 7) & ~7ull);
+        return ((uint32_t)x & 0xFFFFu) == (((uint32_t)(x >> 16) & 0xFFFFu) ^ 0xFFFFu);
+    }
+    if (bt == 2) {
+        const uint32_t ncl = (uint32_t)(h >> 13 & 15u) + 4;
+        const uint64_t f = scan_win64(in, in_len, q + 17);
+        uint32_t kr = 0, nz = 0;
+        for (uint32_t i = 0; i < ncl; i++) { uint32_t l = (uint32_t)(f >> (3 * i)) & 7u; if (l) { kr += 128u >> l; nz++; } }
+        return kr == 128 && nz >= 2;
+    }
+    return 1;
+}
+
+int64_t or_scan_headers(const uint8_t* in, uint64_t in_len, uint64_t lo, uint64_t hi, uint64_t* out, uint64_t cap) {
+    const uint64_t nbits = in_len * 8;
+    if (hi > nbits) hi = nbits;
+    int16_t litTree[2 * 288], distTree[2 * 32], clTree[2 * 19];
+    uint64_t n = 0;
+    for (uint64_t p = lo; p + 3 <= hi; p++) {
+        const uint64_t h = scan_win64(in, in_len, p);
+        if (h & 1u) continue;                                     /* BFINAL = 1: not a chain start */
+        const uint32_t bt = (uint32_t)(h >> 1) & 3u;
+        int ok = 0;
+        if (bt == 0) {                                            /* UncompressedBlock ctor :232-241 */
+            const uint64_t al = (p + 3 + 7) & ~7ull;
+            if (al - (p + 3) && (uint32_t)(h >> 3) & ((1u << (al - (p + 3))) - 1u)) continue;   /* padding 0 */
+            const uint64_t x = scan_win64(in, in_len, al);
+            const uint32_t ln = (uint32_t)x & 0xFFFFu, nln = (uint32_t)(x >> 16) & 0xFFFFu;
+            if (ln != (nln ^ 0xFFFFu) || al + 32 + 8ull * ln > nbits) continue;
+            ok = scan_next_plausible(in, in_len, al + 32 + 8ull * ln);
+        } else if (bt == 2) {                                     /* HuffmanBlock(true) :336-431 */
+            if (((h >> 3) & 31u) >= 30 || ((h >> 8) & 31u) >= 30) continue;
+            /* complete code-length code first (a cheap necessary condition of code_tree's success) */
+            const uint32_t ncl = (uint32_t)(h >> 13 & 15u) + 4;
+            if (p + 17 + 3 * ncl > nbits) continue;
+            const uint64_t f = scan_win64(in, in_len, p + 17);
+            uint32_t kr = 0;
+            for (uint32_t i = 0; i < ncl; i++) { uint32_t l = (uint32_t)(f >> (3 * i)) & 7u; if (l) kr += 128u >> l; }
+            if (kr != 128) continue;
+            br_t r = {in, nbits, p + 3};
+            const int16_t* dt;
+            ok = dynamic_header(&r, litTree, distTree, clTree, &dt) == 0;
+        }
+        if (ok) { if (n < cap) out[n] = p; n++; }
+    }
+    return (int64_t)n;
 }

@@ -86,6 +86,15 @@ int or_inflate_range(const uint8_t* in, uint64_t in_len, uint64_t start_bit, uin
                      const uint8_t* dict, uint64_t dict_len, uint8_t* out, uint64_t out_cap,
                      uint64_t* out_len, uint64_t* consumed_bits);
 
+/* Decoder test support (not a reference interface): every bit position p in [lo, hi) at which the
+ * GPU decoder may start a chain of blocks, i.e. a block header the reference's checks accept
+ * (UncompressedBlock ctor D/decomp/Open.java:232-241, HuffmanBlock(true) :336-431) that also passes
+ * the decoder's chain-start filter: BFINAL = 0; stored: zero padding
+ * bits, the LEN bytes inside the input, and a plausible next header (BTYPE != 3; stored: LEN ==
+ * ~NLEN; dynamic: a complete code-length code); dynamic: HLIT < 30 and HDIST < 30.  Positions in
+ * ascending order; returns their number (positions past `cap` are counted, not written). */
+int64_t or_scan_headers(const uint8_t* in, uint64_t in_len, uint64_t lo, uint64_t hi, uint64_t* out, uint64_t cap);
+
 /* K iterations of DeflaterOutputStream.writeBuffer (D/DeflaterOutputStream.java:119-137) on
  * `data` with the raw bytes `hist` before it (only its last min(hist_limit, .) bytes are used),
  * starting at bit 0: the semantics of ndfl_deflate_chunks.  final_flag = 0 requires whole chunks.

@@ -7,4 +7,4 @@ bash scripts/profile_bench.sh || exit 1
 cd "$GRAFT_REPO_ROOT"
 timeout -k 10 400 python -u bench.py > gpurun_out/bench_final.log 2>&1 || { tail -20 gpurun_out/bench_final.log; exit 1; }
 tail -1 gpurun_out/bench_final.log
-bash scripts/r03_configs_final.sh
+bash scripts/r03/r03_configs_final.sh

@@ -3,4 +3,4 @@
 cd "$GRAFT_REPO_ROOT"
 mkdir -p gpurun_out
 bash scripts/gpu_tests.sh || exit 1
-bash scripts/r04_configs.sh || exit 1
+bash scripts/r04/r04_configs.sh || exit 1

@@ -9,4 +9,4 @@ NDFL_LZ_STATS=1 timeout -k 10 300 python -u scripts/bench_configs.py c3 > gpurun
 tail -3 gpurun_out/c3_parse.log
 NDFL_LZ_SEARCH=chain timeout -k 10 300 python -u scripts/bench_configs.py c3 > gpurun_out/c3_chain.log 2>&1 || { tail -20 gpurun_out/c3_chain.log; exit 1; }
 tail -1 gpurun_out/c3_chain.log
-bash scripts/r04_win.sh
+bash scripts/r04/r04_win.sh

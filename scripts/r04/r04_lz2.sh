@@ -9,4 +9,4 @@ timeout -k 10 300 python -u scripts/bench_configs.py c3 > gpurun_out/c3_parse.lo
 tail -1 gpurun_out/c3_parse.log
 NDFL_LZ_STATS=1 timeout -k 10 300 python -u scripts/bench_configs.py c3 > gpurun_out/c3_parse_stats.log 2>&1 || { tail -20 gpurun_out/c3_parse_stats.log; exit 1; }
 head -1 gpurun_out/c3_parse_stats.log
-bash scripts/r04_win.sh
+bash scripts/r04/r04_win.sh

@@ -78,6 +78,9 @@ def lib():
         L.or_inflate_range.argtypes = [u8p, ctypes.c_uint64, ctypes.c_uint64, ctypes.c_uint64, u8p, ctypes.c_uint64,
                                        u8p, ctypes.c_uint64, ctypes.POINTER(ctypes.c_uint64),
                                        ctypes.POINTER(ctypes.c_uint64)]
+        L.or_scan_headers.restype = ctypes.c_int64
+        L.or_scan_headers.argtypes = [u8p, ctypes.c_uint64, ctypes.c_uint64, ctypes.c_uint64,
+                                      ctypes.POINTER(ctypes.c_uint64), ctypes.c_uint64]
         L.or_crc32.restype = ctypes.c_uint32
         L.or_crc32.argtypes = [ctypes.c_uint32, u8p, ctypes.c_uint64]
         L.or_adler32.restype = ctypes.c_uint32
@@ -223,6 +226,17 @@ def inflate_range(data, start_bit=0, end_bit=None, dictionary=b"", out_cap=None)
         if r < 0:
             raise ValueError(f"or_inflate_range error {r}")
         return reason_name(r), out.raw[:olen.value], bits.value
+
+
+def scan_headers(data, lo=0, hi=None):
+    """The GPU decoder's chain starts in `data` (or_scan_headers): sorted bit positions."""
+    L = lib()
+    hi = len(data) * 8 if hi is None else hi
+    b, nb = _buf(data)
+    n = L.or_scan_headers(b, nb, lo, hi, None, 0)
+    arr = (ctypes.c_uint64 * max(n, 1))()
+    L.or_scan_headers(b, nb, lo, hi, arr, n)
+    return list(arr[:n])
 
 
 def crc32(data, crc=0):

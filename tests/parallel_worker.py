@@ -71,6 +71,26 @@ class OracleCodec:
         self.tails += 1
         return tmp[dict_len + olen - n:dict_len + olen].clone()
 
+    tail_maps = 0
+
+    def tail_map(self, n, dst):
+        """As ndfl_inflate_tail_map: the last n bytes of the pending decode as a map of its window.
+        The checker decodes the range with three windows -- W0[i] = i & 255, W1[i] = i >> 8,
+        W2[i] = 255 - (i & 255): a byte whose value differs between W0 and W2 comes from window
+        index W0 | W1 << 8, any other byte is a value."""
+        data, start, end, out, dict_len = self.pending
+        outs = []
+        for f in (lambda i: i & 255, lambda i: i >> 8, lambda i: 255 - (i & 255)):
+            tmp = out.clone()
+            win = bytes(f(i) for i in range(dict_len))
+            code, olen, _ = self._decode(data, start, end, tmp, dict_len, win)
+            outs.append(tmp[dict_len + olen - n:dict_len + olen].to(torch.int32))
+        o0, o1, o2 = outs
+        ref = o0 != o2
+        dst[:n] = torch.where(ref, o0 | (o1 << 8), o0 | P.TAIL_LITERAL)
+        self.tail_maps += 1
+        return True
+
     def resolve(self):
         data, start, end, out, dict_len = self.pending
         self.pending = None
@@ -196,15 +216,21 @@ def main():
     else:
         gathered = P.gather_stream(codec, dist, torch, part, rank, world)
     out = torch.zeros(P.WINDOW + sizes[rank] + 64, dtype=torch.uint8, device=codec.device)
-    tails = {"none": 0}
+    tails = {"none": 0, "map_none": 0}
     if cfg.get("count_tail_fallbacks"):
-        tail0 = codec.tail
+        tail0, map0 = codec.tail, codec.tail_map
 
         def counted_tail(n):
             t = tail0(n)
             tails["none"] += t is None
             return t
+
+        def counted_map(n, dst):
+            ok = map0(n, dst)
+            tails["map_none"] += not ok
+            return ok
         codec.tail = counted_tail
+        codec.tail_map = counted_map
     code, olen, dict_len = P.inflate_shard(codec, dist, torch, part, out, rank, world)
     if pend is not None:
         gathered = pend.wait()
@@ -217,6 +243,8 @@ def main():
     else:
         ok["gathered_equal"] = gathered is None
     ok["tail_fallbacks"] = tails["none"]
+    ok["map_fallbacks"] = tails["map_none"]
+    ok["tail_maps"] = getattr(codec, "tail_maps", None)
     ok["code"] = code
     ok["decoded_equal"] = olen == sizes[rank] and \
         bytes(out[dict_len:dict_len + olen].cpu().numpy()) == bytes(shard.cpu().numpy())

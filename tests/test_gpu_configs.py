@@ -15,6 +15,7 @@ import numpy as np
 import pytest
 
 import corpus
+import knobs
 import oracle_lib as O
 
 pytestmark = pytest.mark.gpu
@@ -93,14 +94,7 @@ def test_fused_encoder_matches_oracle(ctx):
     rng = np.random.default_rng(5)
     datas = [b"", b"\x00" * 70000, rng.integers(0, 256, 200_003, dtype=np.uint8).tobytes(),
              corpus.c4_mixed(3 << 20).numpy().tobytes()]
-    old = os.environ.get("NDFL_DEFLATE_FUSED")
-    os.environ["NDFL_DEFLATE_FUSED"] = "1"
-    try:
-        for d in datas:
-            for strategy in ["RLE_DYNAMIC", "LITERAL_STATIC"]:
-                assert ctx.deflate(d, strategy) == O.deflate(d, strategy), (len(d), strategy)
-    finally:
-        if old is None:
-            del os.environ["NDFL_DEFLATE_FUSED"]
-        else:
-            os.environ["NDFL_DEFLATE_FUSED"] = old
+    fctx = knobs.context(NDFL_DEFLATE_FUSED=1)
+    for d in datas:
+        for strategy in ["RLE_DYNAMIC", "LITERAL_STATIC"]:
+            assert fctx.deflate(d, strategy) == O.deflate(d, strategy), (len(d), strategy)

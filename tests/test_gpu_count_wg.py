@@ -1,13 +1,12 @@
 """Workgroup rounds of the count pass (inflate_wg.hpp, NDFL_COUNT_W = W waves per chain): the
 decode must equal the oracle's -- output, consumed bits, Reason of the first error -- for W = 2, 4
-and 8, with the dense header finder (rounds of 64W lane segments, waves whose lane 0 verifies from
-the previous wave's exit) and with partitions (NDFL_FIND_PART_BITS: chains of many blocks, each
-later header parsed in the kernel, a round's records written per wave and replayed by the emit
-pass from SegMeta::rs).  Streams: the config-4 mix (RLE_DYNAMIC: text, binary, random data in
+and 8 (rounds of 64W lane segments, waves whose lane 0 verifies from the previous wave's exit;
+chains of many blocks on the fixed-Huffman and small-block streams, whose later headers are parsed
+in the kernel and whose rounds' records are written per wave and replayed by the emit pass from
+SegMeta::rs).  Streams: the config-4 mix (RLE_DYNAMIC: text, binary, random data in
 phase-mapped rounds, runs), zlib -6 text (LZ77 distances), zlib Z_FIXED text (phase-locked
 fixed-Huffman literals), stored blocks, FULL_DYNAMIC, random bytes alone, the reference's 39
 known-answer tests and corrupted streams.  Reference semantics: D/decomp/Open.java:83-618."""
-import os
 import random
 import zlib
 
@@ -15,39 +14,18 @@ import numpy as np
 import pytest
 
 import corpus
+import knobs
 import oracle_lib as O
 from test_oracle_inflate import KAT
 
 pytestmark = pytest.mark.gpu
 
 
-@pytest.fixture(scope="module")
-def ctx():
-    import ndfl
-    return ndfl.Context(0)
-
-
-def _env(name, value):
-    old = os.environ.get(name)
-    if value is None:
-        os.environ.pop(name, None)
-    else:
-        os.environ[name] = str(value)
-    return old
-
-
-@pytest.fixture(params=[2, 4, 8])
-def wg(request):
-    old = _env("NDFL_COUNT_W", request.param)
-    yield request.param
-    _env("NDFL_COUNT_W", old)
-
-
-@pytest.fixture(params=[None, 524288])
-def parts(request):
-    old = _env("NDFL_FIND_PART_BITS", request.param)
-    yield request.param
-    _env("NDFL_FIND_PART_BITS", old)
+@pytest.fixture(scope="module", params=[2, 4, 8])
+def ctx(request):
+    c = knobs.context(NDFL_COUNT_W=request.param)
+    c.wg = request.param
+    return c
 
 
 def _zraw(data, level, strategy=zlib.Z_DEFAULT_STRATEGY):
@@ -87,11 +65,11 @@ def _same(ctx, comp):
 
 @pytest.mark.parametrize("name", ["rle_c4", "zlib6_text", "zlib_fixed_text", "stored_mix", "full_dynamic",
                                   "random_rle", "small_blocks"])
-def test_workgroup_rounds_match_oracle(ctx, wg, parts, name):
+def test_workgroup_rounds_match_oracle(ctx, name):
     _same(ctx, _streams()[name])
 
 
-def test_workgroup_rounds_known_answers(ctx, wg):
+def test_workgroup_rounds_known_answers(ctx):
     for kat in KAT:
         rng = random.Random(kat["line"])
         for pad in range(3):
@@ -104,9 +82,9 @@ def test_workgroup_rounds_known_answers(ctx, wg):
                 assert r is not None and r.name == kat["expect_reason"], kat["name"]
 
 
-def test_workgroup_rounds_first_error(ctx, wg, parts):
+def test_workgroup_rounds_first_error(ctx):
     comp = _streams()["rle_c4"]
-    rng = np.random.default_rng(wg)
+    rng = np.random.default_rng(ctx.wg)
     for _ in range(4):
         bad = bytearray(comp)
         k = int(rng.integers(len(bad) // 8, len(bad)))

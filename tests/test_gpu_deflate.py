@@ -120,31 +120,3 @@ def test_large_mixed_corpus_sampled(ctx):
     got = ctx.deflate(data)
     exp = O.deflate(data)
     assert len(got) == len(exp) and got == exp
-
-
-@pytest.mark.parametrize("slab", ["1", "3", "7", "0"])
-def test_slab_pipeline_matches_oracle(ctx, slab):
-    """The split encoder in slabs of `slab` chunks on two streams (NDFL_DEFLATE_SLAB; 0: one launch
-    per pass): the same bytes as the oracle and the same CRC, with chunk counts that are and are not
-    multiples of the slab, and both streams' last slabs."""
-    import os
-    old = os.environ.get("NDFL_DEFLATE_SLAB")
-    os.environ["NDFL_DEFLATE_SLAB"] = slab
-    try:
-        rng = random.Random(11)
-        for n in [65536 * 3, 65536 * 7 + 5, 65536 * 22 + 65535, 4097]:
-            buf = bytearray()
-            while len(buf) < n:
-                buf += bytes([rng.randrange(4)]) * rng.choice([1, 3, 258, 700]) + rng.randbytes(rng.randrange(40))
-            data = bytes(buf[:n])
-            for strategy in ["RLE_DYNAMIC", "LITERAL_STATIC"]:
-                comp, crc = ctx.deflate(data, strategy, with_crc=True)
-                assert comp == O.deflate(data, strategy), (slab, n, strategy)
-                assert crc == zlib.crc32(data)
-            small = ctx.deflate(data, "RLE_DYNAMIC", chunk_len=1000)
-            assert small == O.deflate(data, "RLE_DYNAMIC", 1000), (slab, n)
-    finally:
-        if old is None:
-            del os.environ["NDFL_DEFLATE_SLAB"]
-        else:
-            os.environ["NDFL_DEFLATE_SLAB"] = old

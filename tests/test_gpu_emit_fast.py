@@ -23,10 +23,6 @@ from test_oracle_inflate import KAT
 pytestmark = pytest.mark.gpu
 
 
-@pytest.fixture(scope="module")
-def ctx():
-    import ndfl
-    return ndfl.Context(0)
 
 
 def _env(name, value):
@@ -42,12 +38,18 @@ MODES = {"fast": {}, "full_only": {"NDFL_EMIT_FAST": "0"}, "hand_over": {"NDFL_N
          "no_alias": {"NDFL_NO_ALIAS": "1"}}
 
 
-@pytest.fixture(params=list(MODES))
-def mode(request):
+@pytest.fixture(scope="module", params=list(MODES))
+def ctx(request):
+    """A context per mode: the library reads its switches when a context is created."""
+    import ndfl
     olds = {k: _env(k, v) for k, v in MODES[request.param].items()}
-    yield request.param
-    for k, v in olds.items():
-        _env(k, v)
+    try:
+        c = ndfl.Context(0)
+    finally:
+        for k, v in olds.items():
+            _env(k, v)
+    c.mode = request.param
+    return c
 
 
 def _zraw(data, level, strategy=zlib.Z_DEFAULT_STRATEGY):
@@ -85,11 +87,11 @@ def _same(ctx, comp):
 
 
 @pytest.mark.parametrize("name", ["rle_c4", "zlib6_text", "zlib_fixed_text", "c2_layout", "stored"])
-def test_emit_modes_match_oracle(ctx, mode, name):
+def test_emit_modes_match_oracle(ctx, name):
     _same(ctx, _streams()[name])
 
 
-def test_emit_modes_known_answers(ctx, mode):
+def test_emit_modes_known_answers(ctx):
     for kat in KAT:
         rng = random.Random(kat["line"])
         for pad in range(3):
@@ -103,9 +105,9 @@ def test_emit_modes_known_answers(ctx, mode):
 
 
 @pytest.mark.parametrize("name", ["rle_c4", "c2_layout"])
-def test_emit_modes_first_error(ctx, mode, name):
+def test_emit_modes_first_error(ctx, name):
     comp = _streams()[name]
-    rng = np.random.default_rng(len(mode))
+    rng = np.random.default_rng(len(ctx.mode))
     for _ in range(4):
         bad = bytearray(comp)
         k = int(rng.integers(len(bad) // 8, len(bad)))

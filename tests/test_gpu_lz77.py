@@ -11,6 +11,7 @@ import zlib
 
 import pytest
 
+import knobs
 import oracle_lib as O
 
 pytestmark = pytest.mark.gpu
@@ -129,27 +130,18 @@ def test_invalid_parameters(ndfl):
 
 
 @pytest.mark.parametrize("env", [{"NDFL_LZ_SEARCH": "chain"}, {"NDFL_LZ_LEAD": "0"}])
-def test_search_modes_match_oracle(ndfl, ctx, env):
+def test_search_modes_match_oracle(ndfl, env):
     """The round-3 hash-chain search at every position (NDFL_LZ_SEARCH=chain), and the parse-driven
     search without its tile lead-in (NDFL_LZ_LEAD=0: the parse enters most tiles at positions no
     wave searched, so the encode kernel's fallback search -- lz_match_global -- supplies them):
     both give the oracle's bytes."""
-    import os
-    old = {k: os.environ.get(k) for k in env}
-    os.environ.update(env)
-    try:
-        cases = [(d, "FULL_DYNAMIC", 65536, 32768) for d in inputs(16)[::2]]
-        cases += [(_text(3 << 20, 7), "FULL_DYNAMIC", 65536, 32768), (_text(400_000, 8), "FULL_STATIC", 1000, 32768),
-                  (_text(300_000, 9), "FULL_DYNAMIC", 40000, 20000), (_text(300_000, 10), "FULL_DYNAMIC", 777, 0)]
-        for data, strategy, chunk_len, hist_limit in cases:
-            got = ctx.deflate(data, strategy, chunk_len=chunk_len, hist_limit=hist_limit)
-            assert got == O.deflate(data, strategy, chunk_len, hist_limit), (env, len(data), chunk_len)
-        strat = ndfl.Lz77Huffman(False, 5, 20, 3, 4096)
-        data = _text(500_000, 11)
-        assert ctx.deflate(data, strat) == O.deflate_lz(data, False, 5, 20, 3, 4096)
-    finally:
-        for k, v in old.items():
-            if v is None:
-                os.environ.pop(k, None)
-            else:
-                os.environ[k] = v
+    ctx = knobs.context(**env)
+    cases = [(d, "FULL_DYNAMIC", 65536, 32768) for d in inputs(16)[::2]]
+    cases += [(_text(3 << 20, 7), "FULL_DYNAMIC", 65536, 32768), (_text(400_000, 8), "FULL_STATIC", 1000, 32768),
+              (_text(300_000, 9), "FULL_DYNAMIC", 40000, 20000), (_text(300_000, 10), "FULL_DYNAMIC", 777, 0)]
+    for data, strategy, chunk_len, hist_limit in cases:
+        got = ctx.deflate(data, strategy, chunk_len=chunk_len, hist_limit=hist_limit)
+        assert got == O.deflate(data, strategy, chunk_len, hist_limit), (env, len(data), chunk_len)
+    strat = ndfl.Lz77Huffman(False, 5, 20, 3, 4096)
+    data = _text(500_000, 11)
+    assert ctx.deflate(data, strat) == O.deflate_lz(data, False, 5, 20, 3, 4096)

@@ -164,3 +164,26 @@ def test_reserved_symbols_and_quirks():
     body = "".join("1" if x == 1 else "0" for x in lens)
     reason, _, _ = O.inflate(O.bits_to_bytes(hdr2 + body + "0" * 16))
     assert reason == "END_OF_BLOCK_CODE_ZERO_LENGTH"
+
+
+@pytest.mark.parametrize("strategy,chunk_len", [("RLE_DYNAMIC", 65536), ("FULL_DYNAMIC", 4096),
+                                                ("UNCOMPRESSED", 65536), ("RLE_DYNAMIC", 300)])
+def test_scan_headers_finds_every_chain_start(strategy, chunk_len):
+    # or_scan_headers (the GPU header finder's expected accepted set, tests/test_gpu_headers.py):
+    # every interior block boundary of an encoder's stream (but the final block's) is found, in
+    # ascending order, and a decode started at a found position reads past its header
+    rng = random.Random(7)
+    data = b"".join(bytes([rng.randrange(4)]) * rng.randrange(1, 400) + rng.randbytes(rng.randrange(0, 90))
+                    for _ in range(1500))
+    comp = O.deflate(data, strategy, chunk_len=chunk_len)
+    bb = O.block_bits(data, strategy, chunk_len)
+    starts, acc = [], 0
+    for b in bb[:-1]:
+        acc += b
+        starts.append(acc)
+    found = O.scan_headers(comp)
+    assert found == sorted(found)
+    assert set(starts[:-1]) <= set(found)
+    for p in found[:40]:
+        r, out, bits = O.inflate_range(comp, start_bit=p, out_cap=4 * len(data) + 65536)
+        assert bits > p + 3

@@ -1,5 +1,6 @@
 """Multi-process (gloo, CPU) checks of the sharded one-stream protocol in ndfl.parallel
-(SURVEY §8e): world sizes 2 and 3, seams inside byte runs, a short last shard."""
+(SURVEY §8e): world sizes 2, 3 and 8 (the driver's node), seams inside byte runs, a short last
+shard, the window maps composed across all 8 ranks."""
 import json
 import os
 import socket
@@ -37,6 +38,10 @@ def run_workers(world, cfg):
     (2, dict(chunk_len=65536, chunks_per_rank=2, last_bytes=65536, seed=4, strategy="FULL_DYNAMIC", seam_run=True)),
     (3, dict(chunk_len=65536, chunks_per_rank=2, last_bytes=40000, seed=6, strategy="RLE_DYNAMIC", seam_run=True,
              async_gather=True)),
+    # the driver's 8-GPU node: 7 seams, the window composed through 7 maps, an 8-part gather
+    (8, dict(chunk_len=65536, chunks_per_rank=2, last_bytes=90001, seed=21, strategy="RLE_DYNAMIC", seam_run=True,
+             async_gather=True)),
+    (8, dict(chunk_len=32768, chunks_per_rank=1, last_bytes=5, seed=22, strategy="FULL_DYNAMIC", seam_run=True)),
 ])
 def test_sharded_stream_roundtrip(world, cfg):
     res = run_workers(world, cfg)
@@ -46,8 +51,10 @@ def test_sharded_stream_roundtrip(world, cfg):
         assert r["code"] == 0
         assert r["decoded_equal"]
     assert all(r["resolved"] == 1 for r in res[1:])
-    # the ranks between the first and the last pass their window on before resolving (inflate_tail)
-    assert all(r["tails"] == 1 for r in res[1:-1])
+    # the ranks between the first and the last describe their window's effect on their tail
+    # (ndfl_inflate_tail_map); the window chain is one all_gather, not a hop per rank
+    assert all(r["tail_maps"] == 1 for r in res[1:-1])
+    assert all(r["tails"] == 0 for r in res)
 
 
 def test_stalled_rank_times_out():
@@ -69,12 +76,13 @@ def test_stalled_rank_times_out():
     assert "timed out" in (p.stdout + p.stderr).lower() or "timeout" in (p.stdout + p.stderr).lower()
 
 
-@pytest.mark.parametrize("world,lie", [(2, False), (3, False), (2, True)])
+@pytest.mark.parametrize("world,lie", [(2, False), (3, False), (2, True), (8, False), (8, True)])
 def test_split_decode_without_seam_index(world, lie):
     """inflate_split: one oracle stream decoded across ranks from probed seams (the checker's probe
     knows the true block boundaries; `lie` moves one seam off a boundary, which the range decodes
     must catch and answer with the single-rank fallback)."""
-    res = run_workers(world, dict(mode="split", n=600_000, seed=5, stream="RLE_DYNAMIC", lie=lie))
+    n = 600_000 if world < 8 else 2_400_000       # (every rank's range must hold a 32 KiB window)
+    res = run_workers(world, dict(mode="split", n=n, seed=5, stream="RLE_DYNAMIC", lie=lie))
     assert res[0]["equal"]
     assert all(r["code"] == 0 for r in res)
     assert res[0]["split"] == (not lie)
