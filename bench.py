@@ -91,14 +91,25 @@ def main():
         per = (args.size // world) // 65536 * 65536
         off = rank * per
         n = per if rank + 1 < world else args.size - off
-        full = corpus.c4_mixed(args.size, seed=0xC4, device="cuda")
-        data = full[off:off + n].clone()
-        if rank != 0 or not gather:
-            del full                  # (rank 0 keeps it to check the gathered stream)
+        # rank 0 generates the corpus once and sends every rank its share (point to point; the
+        # ranks of a one-GPU rehearsal would otherwise all generate 4 GiB on the same card)
+        from ndfl import parallel as P
+        shares = [((args.size // world) // 65536 * 65536) * r for r in range(world)] + [args.size]
+        if rank == 0:
+            full = corpus.c4_mixed(args.size, seed=0xC4, device="cuda")
+            data = full[off:off + n].clone()
+            for r in range(1, world):
+                P._send(dist, full[shares[r]:shares[r + 1]].contiguous(), r)
+            if not gather:
+                del full              # (rank 0 keeps it to check the gathered stream)
+        else:
+            data = torch.empty(n, dtype=torch.uint8, device="cuda")
+            P._recv(dist, data, 0)
     else:
         n = args.size
         data = corpus.c4_mixed(n, seed=0xC4 + rank, device="cuda")
     torch.cuda.synchronize()
+    progress(rank, f"corpus ready ({n / 2**30:g} GiB on cuda:{local})")
     ctx = ndfl.Context(local)
     L = ndfl._lib.load()
     cap = L.ndfl_deflate_bound(n, 65536) + 64
@@ -155,6 +166,7 @@ def main():
 
     for _ in range(args.warmup):
         step()
+    progress(rank, f"{args.warmup} warmup steps done")
     if not args.no_verify:
         assert state["olen"] == n, (state["olen"], n)
         dl = state["dict_len"]
@@ -172,6 +184,7 @@ def main():
     barrier()
     t1 = time.perf_counter()
     per = (t1 - t0) / args.steps
+    progress(rank, f"{args.steps} timed steps: {per * 1e3:.3f} ms per step")
     c_total = state["cbytes"]
     if dist is not None:
         cdev = "cpu" if args.backend == "gloo" else "cuda"
@@ -196,8 +209,8 @@ def main():
     kd, ke = state["t_deflate"], state["t_emit"]
     cands = [(DEFLATE_KERNELS, kd, n + state["cbytes"]),
              ("ndfl_inflate_count_wave_kernel", state["t_count"], state["cbytes"]),
-             ("ndfl_inflate_find_kernel+ndfl_inflate_strict_kernel", state["t_find"], state["cbytes"]),
-             ("ndfl_inflate_emit_wave_kernel", ke, n + state["cbytes"])]
+             ("ndfl_inflate_find_compact_kernel+ndfl_inflate_strict_kernel", state["t_find"], state["cbytes"]),
+             ("ndfl_inflate_emit_fast_kernel+ndfl_inflate_emit_wave_kernel", ke, n + state["cbytes"])]
     dom, kms, alg = max(cands, key=lambda x: x[1])
     achieved = alg / (kms / 1e3)
     traffic, traffic_src = pmc_traffic(dom, n)
@@ -209,8 +222,10 @@ def main():
     if not args.no_cpu:
         threads = args.verify_threads or max(1, min(16, (os.cpu_count() or 1) // world))
         hist = state.get("hist")
+        progress(rank, "whole-shard oracle check")
         exact = verify_stream(data, None if hist is None else hist.cpu().numpy().tobytes(), rank == world - 1,
                               comp, state["endbits"], threads)
+        progress(rank, f"whole-shard oracle check: bit_exact {exact['bit_exact']}")
         if dist is not None:
             f = torch.tensor([1 if exact["bit_exact"] else 0], dtype=torch.int64,
                              device="cpu" if args.backend == "gloo" else "cuda")
@@ -220,12 +235,14 @@ def main():
             # the stream rank 0 actually holds after the last step's gather (parts received into a
             # reused buffer while the shards decoded) against the oracle's single-stream encoding
             # of the whole corpus: the one-GPU stream of the same bytes, bit for bit
+            progress(rank, "gathered-stream oracle check")
             g = verify_stream(full, None, True, state["stream"], state["total_bits"],
                               args.verify_threads or max(1, min(16, os.cpu_count() or 1)))
             exact["gathered"] = {k: g[k] for k in ("bit_exact", "bits_compared", "sha256", "total_s")}
             del full
     cpu = None
     if rank == 0 and not args.no_cpu:
+        progress(rank, "CPU baseline (oracle, 1 thread)")
         cpu = cpu_baseline(data, args.cpu_sample)
         cpu["bit_exact"] = (exact["all_ranks"] and exact.get("gathered", {"bit_exact": True})["bit_exact"]) \
             if world > 1 else exact["bit_exact"]
@@ -268,6 +285,14 @@ def main():
         print(json.dumps(line), flush=True)
     if dist is not None:
         dist.destroy_process_group()
+
+
+_T_START = time.perf_counter()
+
+
+def progress(rank, msg):
+    """One progress line on stderr (the JSON result stays the only stdout line)."""
+    print(f"[bench rank {rank} +{time.perf_counter() - _T_START:.1f}s] {msg}", file=sys.stderr, flush=True)
 
 
 def launch_ranks(n):

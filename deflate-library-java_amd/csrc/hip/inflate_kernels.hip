@@ -422,7 +422,7 @@ __device__ __forceinline__ void find_word_wave(const In& in, uint64_t t, uint64_
     }
     const uint64_t tw0 = t - (uint64_t)lane;                        // the wave's first word
     uint32_t rem = pm;
-    for (;;) {
+    while (__any(rem != 0)) {                                        // (uniform; no empty scan pass)
         const uint32_t cnt = min((uint32_t)__popc(rem), FIND_TAKE);
         // inclusive wave scan by DPP (row shifts, then the row totals broadcast across rows)
         uint32_t incl = cnt;
@@ -433,7 +433,6 @@ __device__ __forceinline__ void find_word_wave(const In& in, uint64_t t, uint64_
         incl += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)incl, 0x142, 0xA, 0xF, false);   // row_bcast:15
         incl += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)incl, 0x143, 0xC, 0xF, false);   // row_bcast:31
         const uint32_t total = (uint32_t)__builtin_amdgcn_readlane((int)incl, 63);
-        if (total == 0) break;                                       // (uniform)
         {
             uint32_t k = incl - cnt;
             for (uint32_t i = 0; i < cnt; i++) {
