@@ -1314,12 +1314,14 @@ static int inflate_devlink(InflateScratch& S, hipStream_t s, const uint32_t* d_w
     if ((uint32_t)hinfo[LI_QCOUNT] > S.q_cap) { S.q_min = (uint32_t)hinfo[LI_QCOUNT] + 65536; return FIND_OVERFLOW; }
     const uint64_t n = hinfo[LI_NCAND];
     // the count pass's width: one wave per chain, unless the chains to count are few against the
-    // count waves (fewer than 4 per wave), where a chain's rounds in sequence bound the pass (config
-    // 2: fixed-Huffman pieces between stored blocks: 4 waves per chain count it in 2.0 ms instead of
-    // 4.0; the bench's 66,770 chains: one wave each) -- NDFL_COUNT_W overrides
+    // count waves (fewer than 2 per wave), where a chain's rounds in sequence bound the pass (config
+    // 2: 3,286 chains, ~1.1 per wave: 4 waves per chain count it in 2.0 ms instead of 4.0; one rank's
+    // 512 MiB share of the bench at 8 GPUs: 8,191 chains, ~2.7 per wave: one wave each, 2.1 ms
+    // instead of 3.1 -- profiles/r05_shard_count_width.txt; the bench's 66,770 chains: one wave
+    // each) -- NDFL_COUNT_W overrides
     const uint64_t nrep = alias_on ? hinfo[LI_NREP] : n;
     static const uint32_t count_waves = wave_grid(ndfl_inflate_count_wave_kernel, COUNT_WAVES, "NDFL_COUNT_WPC");
-    const uint32_t W = S.knobs.count_w ? count_w(S.knobs) : (nrep < 4ull * count_waves && nbits >= (1ull << 24)) ? 4u : 1u;
+    const uint32_t W = S.knobs.count_w ? count_w(S.knobs) : (nrep < 2ull * count_waves && nbits >= (1ull << 24)) ? 4u : 1u;
     if (S.knobs.stats) fprintf(stderr, "[ndfl] count pass: %llu candidates, %llu counted, width %u\n",
                                       (unsigned long long)n, (unsigned long long)nrep, W);
     if (n == 0 || n > (1ull << 24)) return LINK_FALLBACK;
