@@ -708,10 +708,11 @@ __device__ __forceinline__ void deflate_chunk(const Args& a, uint32_t* obuf, PS&
     // any lane of the wave has a 2/3-literal piece (any2_) or a run (anyL_) in it, so the per-byte
     // work of plain literal bytes is branch-free.  A macro rather than a lambda: capturing w[] by
     // reference also demotes it to scratch.
-#define NDFL_FOR_GROUPS(...)                                                                           \
+#define NDFL_FOR_GROUPS(...) NDFL_FOR_GROUPS_X(false, __VA_ARGS__)
+#define NDFL_FOR_GROUPS_X(LIVE, ...)                                                                   \
     _Pragma("unroll 1") for (int o_ = 0; o_ < 8; o_++) {                                               \
         const uint32_t g_ = (uint32_t)(F >> (8 * o_)) & 0xFFu;                                        \
-        if (!__any(g_ != 0)) continue;                                                                 \
+        if (!__any(g_ != 0 || (LIVE))) continue;                                                       \
         const bool o1_ = o_ & 1, o2_ = o_ & 2, o4_ = o_ & 4;                                           \
         const uint32_t a0_ = o1_ ? w[2] : w[0], a1_ = o1_ ? w[6] : w[4];                               \
         const uint32_t a2_ = o1_ ? w[10] : w[8], a3_ = o1_ ? w[14] : w[12];                            \
@@ -898,25 +899,36 @@ _Pragma("unroll")
         const uint32_t d0c = d0 & 0xFFFF, d0l = d0 >> 16;
         const uint32_t m258 = (c285 & 0xFFFF) | (d0c << (c285 >> 16));
         const uint32_t m258l = (c285 >> 16) + d0l;
-        NDFL_FOR_GROUPS({
+        // A group in which no lane of the wave starts a run (wave-uniform) emits one literal code per
+        // byte of its literal pieces: a piece of 2 or 3 equal bytes is 2 or 3 literals of that value,
+        // which is the literal of each of its bytes (bit j of Lm: byte j is a literal; copies past
+        // the group's last byte carry into the next group's first two, or past the lane's last byte
+        // into the next lane's, whose value is the same).  Two codes are joined per put (<= 30 bits).
+        uint32_t carry = 0;
+        NDFL_FOR_GROUPS_X(carry != 0, {
             // codes looked up 4 bytes ahead (8 would spill: the bit buffer state, the chunk's 16
             // words and the lookups share 64 VGPRs)
             uint32_t pf[4];
 _Pragma("unroll")
             for (int j = 0; j < 4; j++) pf[j] = ps.litCode[NDFL_BYTE(j)];
             if (!anyL_) {                       // (wave-uniform: literal pieces only)
+                const uint32_t Lm = r1g_ | (r2g_ << 1) | (r3g_ << 2) | carry;
+                carry = Lm >> 8;
 _Pragma("unroll")
-                for (int j = 0; j < 8; j++) {
-                    const uint32_t lc = pf[j & 3];
-                    if (j < 4) pf[j] = ps.litCode[NDFL_BYTE(j + 4)];
-                    const bool r1 = (r1g_ >> j) & 1;
-                    bp.put(r1 ? (lc & 0xFFFF) : 0u, r1 ? (lc >> 16) : 0u);
-                    if (any2_ && ((r2g_ >> j) & 1)) {
-                        bp.put(lc & 0xFFFF, lc >> 16);
-                        if ((r3g_ >> j) & 1) bp.put(lc & 0xFFFF, lc >> 16);
-                    }
+                for (int j = 0; j < 8; j += 2) {
+                    const uint32_t e0 = pf[j & 3] & (uint32_t)((int32_t)(Lm << (31 - j)) >> 31);
+                    const uint32_t e1 = pf[(j + 1) & 3] & (uint32_t)((int32_t)(Lm << (30 - j)) >> 31);
+                    if (j < 4) { pf[j] = ps.litCode[NDFL_BYTE(j + 4)]; pf[j + 1] = ps.litCode[NDFL_BYTE(j + 5)]; }
+                    const uint32_t l0 = e0 >> 16;
+                    bp.put((e0 & 0xFFFF) | ((e1 & 0xFFFF) << l0), l0 + (e1 >> 16));
                 }
                 continue;
+            }
+            if (carry) {                        // the copies a literal piece of the previous group left
+                const uint32_t lc = pf[0];
+                bp.put(lc & 0xFFFF, lc >> 16);
+                if (carry & 2) bp.put(lc & 0xFFFF, lc >> 16);
+                carry = 0;
             }
 _Pragma("unroll")
             for (int j = 0; j < 8; j++) {
@@ -946,6 +958,11 @@ _Pragma("unroll")
                 })
             }
         })
+        if (carry) {                            // copies past the lane's last byte (same value)
+            const uint32_t lc = ps.litCode[w[15] >> 24];
+            bp.put(lc & 0xFFFF, lc >> 16);
+            if (carry & 2) bp.put(lc & 0xFFFF, lc >> 16);
+        }
         bp.flush();
     }
     __syncthreads();

@@ -506,46 +506,57 @@ ndfl_inflate_find_compact_kernel(const uint32_t* w, uint64_t nwords, uint64_t nb
 }
 
 namespace inf {
-// strict-stage reader: 64-bit buffer, the next 16-byte group always in flight
+// strict-stage reader: a 256-bit window of the input (two 16-byte groups) in registers and a 64-bit
+// bit buffer filled from it.  The window moves wave-wide: when an active lane has used its window
+// up, every lane past its first group loads the next two groups, so one memory wait serves the
+// wave.  (A per-lane rolling prefetch -- load the next group whenever a lane crosses one -- put a
+// load wait into almost every step: with ~40 lanes active some lane crosses a group nearly every
+// step, and the compiler waits for the new group where it copies it into the loop's registers.)
 struct SRd {
-    uint64_t bb, pos, qw;
-    uint32_t bn, ci;
+    uint64_t bb, pos, qw;    // bit buffer; the stream position of its bit 0; the window's first group
+    uint32_t bn, fi;         // valid bits in bb; the next window word to add to it (8: used up)
     u32x4 cur, nxt;
     __device__ __forceinline__ static uint32_t pick(const u32x4& v, uint32_t i) {
         uint32_t a = (i & 1) ? v.y : v.x, b = (i & 1) ? v.w : v.z;
         return (i & 2) ? b : a;
     }
-    __device__ __forceinline__ void adv(const In& in) {
-        if (++ci == 4) {
-            ci = 0;
-            qw++;
-            cur = nxt;
-            asm volatile("" : "+v"(cur) :: "memory");
-            nxt = in.ld4(qw + 1);
-        }
+    __device__ __forceinline__ uint32_t pick8(uint32_t i) const {
+        const uint32_t a = pick(cur, i), b = pick(nxt, i);
+        return (i & 4) ? b : a;
     }
-    __device__ __forceinline__ void fill(const In& in) {
-        if (bn <= 32) { bb |= (uint64_t)pick(cur, ci) << bn; bn += 32; adv(in); }
+    __device__ __forceinline__ void load(const In& in, uint64_t g) {
+        qw = g;
+        cur = in.ld4(g);
+        nxt = in.ld4(g + 1);
     }
-    __device__ __forceinline__ void init(const In& in, uint64_t p) {
+    // 64 bits from window bit o (o < 160)
+    __device__ __forceinline__ uint64_t bits64(uint32_t o) const {
+        const uint32_t i = o >> 5, sh = o & 31;
+        const uint64_t x = (uint64_t)pick8(i) | ((uint64_t)pick8(i + 1) << 32);
+        return sh ? (x >> sh) | ((uint64_t)pick8(i + 2) << (64 - sh)) : x;
+    }
+    __device__ __forceinline__ void fill() {
+        if (bn <= 32 && fi < 8) { bb |= (uint64_t)pick8(fi) << bn; bn += 32; fi++; }
+    }
+    // the buffer from stream bit p on (p - 128 qw < 224)
+    __device__ __forceinline__ void seek(uint64_t p) {
         pos = p;
-        qw = p >> 7;
-        cur = in.ld4(qw);
-        nxt = in.ld4(qw + 1);
-        ci = (uint32_t)(p >> 5) & 3u;
-        bb = (uint64_t)(pick(cur, ci) >> (p & 31));
-        bn = 32 - (uint32_t)(p & 31);
-        adv(in);
-        fill(in);
+        const uint32_t o = (uint32_t)(p - qw * 128);
+        fi = o >> 5;
+        bb = (uint64_t)(pick8(fi) >> (o & 31));
+        bn = 32 - (o & 31);
+        fi++;
+        fill();
+    }
+    __device__ __forceinline__ bool starved() const { return bn <= 32 && fi >= 8; }
+    // move the window to the group holding the next word to add (bb and bn stay)
+    __device__ __forceinline__ void reload(const In& in) {
+        const uint64_t wn = qw * 4 + fi;
+        load(in, wn >> 2);
+        fi = (uint32_t)wn & 3u;
     }
     __device__ __forceinline__ uint32_t peek(uint32_t n) const { return (uint32_t)bb & ((1u << n) - 1u); }
     __device__ __forceinline__ void skip(uint32_t n) { bb >>= n; bn -= n; pos += n; }
-    __device__ __forceinline__ uint32_t get(const In& in, uint32_t n) {
-        fill(in);
-        const uint32_t v = peek(n);
-        skip(n);
-        return v;
-    }
 };
 }  // namespace inf
 
@@ -585,7 +596,7 @@ ndfl_inflate_strict_kernel(const uint32_t* w, uint64_t nwords, uint64_t nbits, c
     bool active = false;
     uint64_t p = 0;
     SRd rd;
-    rd.bb = 0; rd.pos = 0; rd.qw = 0; rd.bn = 0; rd.ci = 0;
+    rd.bb = 0; rd.pos = 0; rd.qw = 0; rd.bn = 0; rd.fi = 8;
     uint32_t i = 0, total = 0, numLit = 0, numDist = 0, litK = 0, distK = 0, ones = 0, other = 0, eob = 0, d0 = 0,
              d31 = 0;
     int runVal = -1;
@@ -611,16 +622,17 @@ ndfl_inflate_strict_kernel(const uint32_t* w, uint64_t nwords, uint64_t nbits, c
                     if (!(e >> 63)) {
                         if (strict_stored(in, p)) record(p);
                     } else {
-                        rd.init(in, p + 3);
-                        const uint32_t hlit = rd.get(in, 5), hdist = rd.get(in, 5), hclen = rd.get(in, 4);
+                        // the header's fields straight from the window (p + 74 < 128 qw + 256)
+                        rd.load(in, p >> 7);
+                        const uint32_t o = (uint32_t)p & 127u;
+                        const uint32_t h = (uint32_t)rd.bits64(o + 3);
+                        const uint32_t hlit = h & 31u, hdist = (h >> 5) & 31u, hclen = (h >> 10) & 15u;
                         numLit = hlit + 257; numDist = hdist + 1; total = numLit + numDist;
                         const uint32_t numCl = hclen + 4;
                         // the numCl 3-bit code-length code lengths in stream (CLO) order as one field
                         // (two registers where a per-symbol array held 19 at the refill's peak)
-                        uint64_t F = 0;
-#pragma unroll
-                        for (int j = 0; j < 19; j++)
-                            if ((uint32_t)j < numCl) F |= (uint64_t)rd.get(in, 3) << (3 * j);
+                        const uint64_t F = rd.bits64(o + 17) & ((1ull << (3 * numCl)) - 1ull);
+                        rd.seek(p + 17 + 3 * numCl);
                         // the stage-1 test guarantees a complete code: the runs fill all 128 entries
                         // canonical (length, symbol) order without a pass per length: each length's
                         // first entry is the byte-wise exclusive prefix sum of count x run, all seven
@@ -676,10 +688,13 @@ ndfl_inflate_strict_kernel(const uint32_t* w, uint64_t nwords, uint64_t nbits, c
         const bool more = next < end || !drained;
         for (uint32_t ni = nidle;;) {
         n_steps += 64 - ni;
+        if (__any(active && rd.starved())) {            // (rare: once per ~20 steps, not per step)
+            if (active && rd.fi >= 4) rd.reload(in);
+        }
         if (active) {
             // one code-length symbol (D/decomp/Open.java's dynamic header loop, same checks)
             // one refill covers the code (<= 7 bits) and its extra bits (<= 7): no branch per symbol kind
-            rd.fill(in);
+            rd.fill();
             const uint32_t b = (uint32_t)rd.bb;
             const uint32_t te = tab[__builtin_bitreverse32(b) >> 25];
             const uint32_t sym = te & 31u, cl = te >> 5;
