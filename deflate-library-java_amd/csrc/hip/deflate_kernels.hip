@@ -694,25 +694,42 @@ __device__ __forceinline__ void deflate_chunk(const Args& a, uint32_t* obuf, PS&
     // plen comes from the next start: the lane's own starts, then nextStart as a marker bit (the
     // chunk end is one).  Only the chunk's first byte can have lead 0 (its value continues the
     // history), where plen 3 is R = 3: a run.
-    // The classes are formed per 8-byte group from F and the marker position mp (bit 31 of mpx: the
-    // chunk's first piece has lead 0), so only F and one word stay live across the loops.
+    // The classes of all 64 bytes are formed at once from F and the marker position mp (bit 31 of
+    // mpx: the chunk's first piece has lead 0): LM bit i = byte i is a literal of a literal piece (a
+    // piece of 2 or 3 equal bytes is that many literals of the same value, so its copies sit on the
+    // bytes they cover), LG bit i = a run piece starts at byte i; ce = literal copies past the lane's
+    // last byte (the next lane's first bytes, same value).
     uint32_t mpx = 0xFFFFu;
     if (vcnt > 0) {
         mpx = nextStart - t0;
         if (a.rle && tid == 0 && (F & 1) && lead_of(0, w[0] & 0xFFu) == 0) mpx |= 1u << 31;
     }
+    uint64_t LM = 0, LG = 0;
+    uint32_t ce = 0;
+    if (vcnt > 0) {
+        const uint32_t mq = mpx & 0xFFFFu;
+        const uint64_t wl = F | (mq < 64 ? 1ull << mq : 0ull);
+        const uint64_t wh = (mq >= 64 && mq < 67) ? 1ull << (mq - 64) : 0ull;      // bits 64..66
+        const uint64_t e1 = (wl >> 1) | (wh << 63), e2 = (wl >> 2) | (wh << 62), e3 = (wl >> 3) | (wh << 61);
+        uint64_t r3 = F & ~e1 & ~e2 & e3;
+        LG = F & ~(e1 | e2 | e3);
+        if ((mpx >> 31) && (r3 & 1ull)) { r3 &= ~1ull; LG |= 1ull; }
+        const uint64_t r2 = (F & ~e1 & e2) | r3;
+        const uint64_t r1 = (F & e1) | r2;
+        LM = r1 | (r2 << 1) | (r3 << 2);
+        ce = (uint32_t)(r2 >> 63) + (uint32_t)((r3 >> 62) & 1ull) + (uint32_t)(r3 >> 63);
+    }
     // visit this lane's bytes in order, 8 at a time.  Outer loop over 8-byte groups (select tree on
     // the uniform group index: a dynamic register index would put w[] in scratch memory), inner loop
     // unrolled by the caller: byte extraction is a constant shift.  BODY sees the group's bytes
-    // (gw0_, gw1_), its class masks (r1g_: >= 1 literal, r2g_: >= 2, r3g_: 3, lgg_: run) and whether
-    // any lane of the wave has a 2/3-literal piece (any2_) or a run (anyL_) in it, so the per-byte
-    // work of plain literal bytes is branch-free.  A macro rather than a lambda: capturing w[] by
-    // reference also demotes it to scratch.
-#define NDFL_FOR_GROUPS(...) NDFL_FOR_GROUPS_X(false, __VA_ARGS__)
-#define NDFL_FOR_GROUPS_X(LIVE, ...)                                                                   \
+    // (gw0_, gw1_), its literal and run-start bits (lm_, lg_) and whether any lane of the wave starts
+    // a run in it (anyL_), so the per-byte work of literal bytes is branch-free.  A macro rather than
+    // a lambda: capturing w[] by reference also demotes it to scratch.
+#define NDFL_FOR_GROUPS_L(...)                                                                         \
     _Pragma("unroll 1") for (int o_ = 0; o_ < 8; o_++) {                                               \
-        const uint32_t g_ = (uint32_t)(F >> (8 * o_)) & 0xFFu;                                        \
-        if (!__any(g_ != 0 || (LIVE))) continue;                                                       \
+        const uint32_t lm_ = (uint32_t)(LM >> (8 * o_)) & 0xFFu;                                      \
+        const uint32_t lg_ = (uint32_t)(LG >> (8 * o_)) & 0xFFu;                                      \
+        if (!__any((lm_ | lg_) != 0)) continue;                                                        \
         const bool o1_ = o_ & 1, o2_ = o_ & 2, o4_ = o_ & 4;                                           \
         const uint32_t a0_ = o1_ ? w[2] : w[0], a1_ = o1_ ? w[6] : w[4];                               \
         const uint32_t a2_ = o1_ ? w[10] : w[8], a3_ = o1_ ? w[14] : w[12];                            \
@@ -720,26 +737,15 @@ __device__ __forceinline__ void deflate_chunk(const Args& a, uint32_t* obuf, PS&
         const uint32_t b2_ = o1_ ? w[11] : w[9], b3_ = o1_ ? w[15] : w[13];                            \
         const uint32_t gw0_ = o4_ ? (o2_ ? a3_ : a2_) : (o2_ ? a1_ : a0_);                             \
         const uint32_t gw1_ = o4_ ? (o2_ ? b3_ : b2_) : (o2_ ? b1_ : b0_);                             \
-        const uint32_t mq_ = (mpx & 0xFFFFu) - 8u * (uint32_t)o_;                                      \
-        const uint32_t win_ = (uint32_t)(F >> (8 * o_)) | (mq_ < 32u ? (1u << mq_) : 0u);              \
-        const uint32_t e1_ = win_ >> 1, e2_ = win_ >> 2, e3_ = win_ >> 3;                              \
-        uint32_t r3g_ = g_ & ~e1_ & ~e2_ & e3_;                                                        \
-        uint32_t lgg_ = g_ & ~(e1_ | e2_ | e3_);                                                       \
-        if (o_ == 0 && (mpx >> 31) && (r3g_ & 1u)) { r3g_ &= ~1u; lgg_ |= 1u; }                        \
-        const uint32_t r2g_ = (g_ & ~e1_ & e2_) | r3g_;                                                \
-        const uint32_t r1g_ = (g_ & e1_) | r2g_;                                                       \
-        const bool any2_ = __any(r2g_ != 0), anyL_ = __any(lgg_ != 0);                                 \
-        (void)r1g_; (void)any2_;                                                                       \
+        const bool anyL_ = __any(lg_ != 0);                                                            \
         __VA_ARGS__                                                                                    \
     }
 #define NDFL_BYTE(j) ((((j) < 4 ? gw0_ : gw1_) >> (8 * ((j) & 3))) & 0xFFu)
-    // literal copies per group byte j: r1 + r2 + r3 (the classes nest), as a popcount of bits j,
-    // j + 8 and j + 16 of the group's packed class word
-#define NDFL_REPS() (r1g_ | (r2g_ << 8) | (r3g_ << 16))
-#define NDFL_REP(j) ((uint32_t)__builtin_popcount(R_ & (0x010101u << (j))))
+// 0 or all ones: byte j of the group is a literal
+#define NDFL_LMASK(j) ((uint32_t)((int32_t)(lm_ << (31 - (j))) >> 31))
     // a run starting at group byte j: its value v, start gpos and end pend (next start)
-#define NDFL_RUN(j, ...)                                                                               \
-    if (anyL_ && ((lgg_ >> (j)) & 1)) {                                                                \
+#define NDFL_RUN_L(j, ...)                                                                             \
+    if ((lg_ >> (j)) & 1) {                                                                            \
         const int i_ = 8 * o_ + (j);                                                                   \
         const uint32_t v = NDFL_BYTE(j);                                                               \
         const uint32_t gpos = t0 + (uint32_t)i_;                                                       \
@@ -759,22 +765,14 @@ __device__ __forceinline__ void deflate_chunk(const Args& a, uint32_t* obuf, PS&
         prefetch_next();
     }
     if (MODE != MODE_EMIT) {
-    NDFL_FOR_GROUPS({
-        const uint32_t R_ = NDFL_REPS();
-        if (!anyL_) {                           // (wave-uniform: no run starts in the group)
+    NDFL_FOR_GROUPS_L({
 _Pragma("unroll")
-            for (int j = 0; j < 8; j++) {
-                const uint32_t rep = NDFL_REP(j);
-                if (rep) atomicAdd(&hl[NDFL_BYTE(j)], rep);
-            }
-            continue;
-        }
+        for (int j = 0; j < 8; j++)
+            if ((lm_ >> j) & 1) atomicAdd(&hl[NDFL_BYTE(j)], 1u);
+        if (!anyL_) continue;                   // (wave-uniform: no run starts in the group)
 _Pragma("unroll")
         for (int j = 0; j < 8; j++) {
-            const uint32_t v = NDFL_BYTE(j);
-            const uint32_t rep = NDFL_REP(j);
-            if (rep) atomicAdd(&hl[v], rep);
-            NDFL_RUN(j, {
+            NDFL_RUN_L(j, {
                 const uint32_t lead = lead_of(gpos, v);
                 const uint32_t R = pend - gpos - lead;
                 const uint32_t n258 = R / 258, m = R % 258;
@@ -791,6 +789,7 @@ _Pragma("unroll")
             })
         }
     })
+    if (ce) atomicAdd(&hl[w[15] >> 24], ce);
     if (tid == 0) {
         atomicAdd(&hl[256], 1u);                          // end of block (:131-132)
         if (a.dynamic && len_c == 0) atomicAdd(&hl[0], 1u);  // (:146-147)
@@ -829,34 +828,34 @@ _Pragma("unroll")
     const uint32_t d0 = __builtin_amdgcn_readfirstlane(ps.distCode[0]);       // workgroup-uniform: SGPRs
     const uint32_t c285 = __builtin_amdgcn_readfirstlane(ps.litCode[285]);
     uint32_t mybits = 0;
-    NDFL_FOR_GROUPS({
+    NDFL_FOR_GROUPS_L({
         uint32_t pf[8];
 _Pragma("unroll")
         for (int j = 0; j < 8; j++) pf[j] = ps.litCode[NDFL_BYTE(j)];
-        const uint32_t R_ = NDFL_REPS();
-        if (!anyL_) {
+        uint32_t gs = 0;                        // (<= 8 x 15: the literal lengths of the group)
 _Pragma("unroll")
-            for (int j = 0; j < 8; j++) mybits += NDFL_REP(j) * (pf[j] >> 16);
-            continue;
-        }
+        for (int j = 0; j < 8; j++) gs += (pf[j] & NDFL_LMASK(j)) >> 16;
+        mybits += gs;
+        if (anyL_) {                            // (wave-uniform: some lane starts a run in the group)
 _Pragma("unroll")
-        for (int j = 0; j < 8; j++) {
-            const uint32_t lv = pf[j] >> 16;
-            mybits += NDFL_REP(j) * lv;
-            NDFL_RUN(j, {
-                const uint32_t lead = lead_of(gpos, v);
-                const uint32_t R = pend - gpos - lead;
-                const uint32_t n258 = R / 258, m = R % 258;
-                mybits += lead * lv + n258 * ((c285 >> 16) + (d0 >> 16));
-                if (m >= 3) {
-                    uint32_t sym, ne, ex; run_sym(m, sym, ne, ex);
-                    mybits += (ps.litCode[sym] >> 16) + ne + (d0 >> 16);
-                } else {
-                    mybits += m * lv;
-                }
-            })
+            for (int j = 0; j < 8; j++) {
+                NDFL_RUN_L(j, {
+                    const uint32_t lv = pf[j] >> 16;
+                    const uint32_t lead = lead_of(gpos, v);
+                    const uint32_t R = pend - gpos - lead;
+                    const uint32_t n258 = R / 258, m = R % 258;
+                    mybits += lead * lv + n258 * ((c285 >> 16) + (d0 >> 16));
+                    if (m >= 3) {
+                        uint32_t sym, ne, ex; run_sym(m, sym, ne, ex);
+                        mybits += (ps.litCode[sym] >> 16) + ne + (d0 >> 16);
+                    } else {
+                        mybits += m * lv;
+                    }
+                })
+            }
         }
     })
+    if (ce) mybits += ce * (ps.litCode[w[15] >> 24] >> 16);
     const uint64_t tp3a = wall_clock64();
     uint32_t tokTotal;
     const uint32_t myoff = block_excl_scan<uint32_t, NW>(mybits, ps.scan32, tokTotal);
@@ -899,48 +898,32 @@ _Pragma("unroll")
         const uint32_t d0c = d0 & 0xFFFF, d0l = d0 >> 16;
         const uint32_t m258 = (c285 & 0xFFFF) | (d0c << (c285 >> 16));
         const uint32_t m258l = (c285 >> 16) + d0l;
-        // A group in which no lane of the wave starts a run (wave-uniform) emits one literal code per
-        // byte of its literal pieces: a piece of 2 or 3 equal bytes is 2 or 3 literals of that value,
-        // which is the literal of each of its bytes (bit j of Lm: byte j is a literal; copies past
-        // the group's last byte carry into the next group's first two, or past the lane's last byte
-        // into the next lane's, whose value is the same).  Two codes are joined per put (<= 30 bits).
-        uint32_t carry = 0;
-        NDFL_FOR_GROUPS_X(carry != 0, {
+        // one literal code per literal byte (LM), the tokens of a run at its first byte (LG); a group
+        // in which no lane of the wave starts a run (wave-uniform) joins two codes per put (<= 30 bits)
+        NDFL_FOR_GROUPS_L({
             // codes looked up 4 bytes ahead (8 would spill: the bit buffer state, the chunk's 16
             // words and the lookups share 64 VGPRs)
             uint32_t pf[4];
 _Pragma("unroll")
             for (int j = 0; j < 4; j++) pf[j] = ps.litCode[NDFL_BYTE(j)];
-            if (!anyL_) {                       // (wave-uniform: literal pieces only)
-                const uint32_t Lm = r1g_ | (r2g_ << 1) | (r3g_ << 2) | carry;
-                carry = Lm >> 8;
+            if (!anyL_) {
 _Pragma("unroll")
                 for (int j = 0; j < 8; j += 2) {
-                    const uint32_t e0 = pf[j & 3] & (uint32_t)((int32_t)(Lm << (31 - j)) >> 31);
-                    const uint32_t e1 = pf[(j + 1) & 3] & (uint32_t)((int32_t)(Lm << (30 - j)) >> 31);
+                    const uint32_t e0 = pf[j & 3] & NDFL_LMASK(j);
+                    const uint32_t e1 = pf[(j + 1) & 3] & NDFL_LMASK(j + 1);
                     if (j < 4) { pf[j] = ps.litCode[NDFL_BYTE(j + 4)]; pf[j + 1] = ps.litCode[NDFL_BYTE(j + 5)]; }
                     const uint32_t l0 = e0 >> 16;
                     bp.put((e0 & 0xFFFF) | ((e1 & 0xFFFF) << l0), l0 + (e1 >> 16));
                 }
                 continue;
             }
-            if (carry) {                        // the copies a literal piece of the previous group left
-                const uint32_t lc = pf[0];
-                bp.put(lc & 0xFFFF, lc >> 16);
-                if (carry & 2) bp.put(lc & 0xFFFF, lc >> 16);
-                carry = 0;
-            }
 _Pragma("unroll")
             for (int j = 0; j < 8; j++) {
                 const uint32_t lc = pf[j & 3];
                 if (j < 4) pf[j] = ps.litCode[NDFL_BYTE(j + 4)];
-                const bool r1 = (r1g_ >> j) & 1;
-                bp.put(r1 ? (lc & 0xFFFF) : 0u, r1 ? (lc >> 16) : 0u);
-                if (any2_ && ((r2g_ >> j) & 1)) {
-                    bp.put(lc & 0xFFFF, lc >> 16);
-                    if ((r3g_ >> j) & 1) bp.put(lc & 0xFFFF, lc >> 16);
-                }
-                NDFL_RUN(j, {
+                const uint32_t e = lc & NDFL_LMASK(j);
+                bp.put(e & 0xFFFF, e >> 16);
+                NDFL_RUN_L(j, {
                     const uint32_t lead = lead_of(gpos, v);
                     const uint32_t R = pend - gpos - lead;
                     const uint32_t n258 = R / 258, m = R % 258;
@@ -958,10 +941,10 @@ _Pragma("unroll")
                 })
             }
         })
-        if (carry) {                            // copies past the lane's last byte (same value)
+        if (ce) {                               // copies past the lane's last byte (same value)
             const uint32_t lc = ps.litCode[w[15] >> 24];
             bp.put(lc & 0xFFFF, lc >> 16);
-            if (carry & 2) bp.put(lc & 0xFFFF, lc >> 16);
+            if (ce > 1) bp.put(lc & 0xFFFF, lc >> 16);
         }
         bp.flush();
     }
