@@ -51,39 +51,42 @@ struct WScr {
 // pm_lengths, with each lane taking every 64th item.  lens[0..n) receives the lengths.
 __device__ void wpm_lengths(const uint32_t* hist, int n, int L, uint8_t* lens, WScr& S) {
     const int lane = threadIdx.x;
-    const int npad = (n + 3) & ~3;
+    // the used symbols' keys (freq << 9 | symbol) compacted in symbol order, padded to 4 with ~0
     uint32_t nl = 0;
-    for (int base = 0; base < npad; base += 64) {            // uniform trip count
+    for (int base = 0; base < n; base += 64) {                // uniform trip count
         const int i = base + lane;
         uint32_t k = 0xFFFFFFFFu;
-        if (i < n) { const uint32_t f = hist[i]; if (f) k = f << 9 | (uint32_t)i; }
-        if (i < npad) S.key()[i] = k;
-        nl += (uint32_t)__popcll(__ballot(k != 0xFFFFFFFFu));
+        if (i < n) { const uint32_t f = hist[i]; if (f) k = f << 9 | (uint32_t)i; lens[i] = 0; }
+        const uint64_t m = __ballot(k != 0xFFFFFFFFu);
+        if (k != 0xFFFFFFFFu) S.key()[nl + (uint32_t)__popcll(m & ((1ull << lane) - 1ull))] = k;
+        nl += (uint32_t)__popcll(m);
     }
+    const uint32_t nlp = (nl + 3) & ~3u;
+    if ((uint32_t)lane < nlp - nl) S.key()[nl + lane] = 0xFFFFFFFFu;
     for (int t = lane; t < L * 20; t += 64) S.mpk[t] = 0;
     __syncthreads();
-    // leaves sorted by (freq, symbol): rank by counting, up to 5 keys per lane in registers
+    // leaves sorted by (freq, symbol): rank by counting among the used keys only (a text chunk uses
+    // ~100 of the 286 literal/length symbols), up to 5 keys per lane in registers
     {
+        const uint32_t nq = (nl + 63) >> 6;                   // uniform: key slots per lane in use
         uint32_t kk[5], r[5];
 #pragma unroll
         for (int q = 0; q < 5; q++) {
-            const int i = lane + 64 * q;
-            kk[q] = i < n ? S.key()[i] : 0xFFFFFFFFu;
+            const uint32_t i = (uint32_t)lane + 64u * q;
+            kk[q] = i < nl ? S.key()[i] : 0xFFFFFFFFu;
             r[q] = 0;
         }
-        for (int j = 0; j < npad; j += 4) {
+        for (uint32_t j = 0; j < nlp; j += 4) {
             const uint4 v = *(const uint4*)&S.key()[j];
 #pragma unroll
             for (int q = 0; q < 5; q++)
-                r[q] += (uint32_t)(v.x < kk[q]) + (uint32_t)(v.y < kk[q]) + (uint32_t)(v.z < kk[q]) + (uint32_t)(v.w < kk[q]);
+                if ((uint32_t)q < nq)
+                    r[q] += (uint32_t)(v.x < kk[q]) + (uint32_t)(v.y < kk[q]) + (uint32_t)(v.z < kk[q]) + (uint32_t)(v.w < kk[q]);
         }
 #pragma unroll
         for (int q = 0; q < 5; q++) {
-            const int i = lane + 64 * q;
-            if (i < n) {
-                if (kk[q] != 0xFFFFFFFFu) { S.lf[r[q]] = kk[q] >> 9; S.ls[r[q]] = (uint16_t)i; }
-                lens[i] = 0;
-            }
+            const uint32_t i = (uint32_t)lane + 64u * q;
+            if (i < nl) { S.lf[r[q]] = kk[q] >> 9; S.ls[r[q]] = (uint16_t)(kk[q] & 511u); }
         }
     }
     __syncthreads();
@@ -245,17 +248,20 @@ ndfl_deflate_codes_kernel(Args a) {
     } else {
         // trim litlen histogram, keep >= 257 (:148-151); single used distance code gets a dummy
         // neighbour (:155-171); empty distance code (:172-177)
-        if (lane == 0) {
-            int ln = 286;
-            while (ln > 257 && S.hlit[ln - 1] == 0) ln--;
-            S.misc[0] = (uint32_t)ln;
-            int used = 0, first = -1;
-            for (int i = 0; i < 30; i++) if (S.hdist[i]) { used++; if (first < 0) first = i; }
-            if (used == 1) { if (first < 29) S.hdist[first + 1] = 1; else S.hdist[first - 1] = 1; }
-            int dn = 30;
-            while (dn > 1 && S.hdist[dn - 1] == 0) dn--;
-            S.misc[1] = (uint32_t)dn;
-            S.misc[2] = (dn == 1 && S.hdist[0] == 0) ? 1u : 0u;
+        {
+            const uint64_t lb = __ballot(lane < 29 && S.hlit[257 + lane] != 0);
+            uint64_t db = __ballot(lane < 30 && S.hdist[lane] != 0);
+            if (__popcll(db) == 1) {
+                const int first = (int)__builtin_ctzll(db);
+                const int nb = first < 29 ? first + 1 : first - 1;
+                if (lane == 0) S.hdist[nb] = 1;
+                db |= 1ull << nb;
+            }
+            if (lane == 0) {
+                S.misc[0] = lb ? 258u + (uint32_t)(63 - __builtin_clzll(lb)) : 257u;
+                S.misc[1] = db ? 1u + (uint32_t)(63 - __builtin_clzll(db)) : 1u;
+                S.misc[2] = db ? 0u : 1u;
+            }
         }
         __syncthreads();
         const int ln = (int)S.misc[0], dn = (int)S.misc[1];
