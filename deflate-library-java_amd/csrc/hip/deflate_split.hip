@@ -401,10 +401,23 @@ ndfl_deflate_offsets_kernel(const uint64_t* sizes, uint32_t n, uint64_t base, ui
     __syncthreads();                        // (every thread has read *base_ptr before thread 0 writes total)
     const uint32_t per = (n + 1023) / 1024;
     const uint32_t b0 = min(n, threadIdx.x * per), b1 = min(n, b0 + per);
+    // (eight loads in flight per batch: a load-then-add loop waits out every load in turn)
     uint64_t sum = 0;
-    for (uint32_t i = b0; i < b1; i++) sum += sizes[i];
+    for (uint32_t i = b0; i < b1; i += 8) {
+        uint64_t x[8];
+#pragma unroll
+        for (int k = 0; k < 8; k++) x[k] = i + k < b1 ? sizes[i + k] : 0ull;
+#pragma unroll
+        for (int k = 0; k < 8; k++) sum += x[k];
+    }
     uint64_t tot;
     uint64_t run = base + block_excl_scan<uint64_t, 16>(sum, sh, tot);
-    for (uint32_t i = b0; i < b1; i++) { off[i] = run; run += sizes[i]; }
+    for (uint32_t i = b0; i < b1; i += 8) {
+        uint64_t x[8];
+#pragma unroll
+        for (int k = 0; k < 8; k++) x[k] = i + k < b1 ? sizes[i + k] : 0ull;
+#pragma unroll
+        for (int k = 0; k < 8; k++) if (i + k < b1) { off[i + k] = run; run += x[k]; }
+    }
     if (threadIdx.x == 0) total[0] = base + tot;
 }

@@ -464,7 +464,9 @@ __device__ __forceinline__ void find_word_wave(const In& in, uint64_t t, uint64_
         __builtin_amdgcn_wave_barrier();                             // (the list is rewritten next)
     }
 }
-// Kraft sums of four 3-bit lengths (index: four fields, the first in the low bits), x 1/128
+// Kraft sums of four 3-bit lengths (index: four fields, the first in the low bits), x 1/128.  (Ten
+// lookups of a 64-entry two-length table -- one entry per LDS bank, no bank conflicts -- measured
+// slower: finder phase 6.12 -> 6.50 ms, round 5.)
 __device__ __forceinline__ void kr4_fill(uint16_t* kr4) {
     for (uint32_t i = threadIdx.x; i < 4096; i += blockDim.x) {
         uint32_t s = 0;
@@ -744,21 +746,41 @@ ndfl_inflate_strict_kernel(const uint32_t* w, uint64_t nwords, uint64_t nbits, c
     }
 }
 // Sort each segment's candidates (arrival order is arbitrary) and compact them into one sorted
-// list at the offsets of an exclusive scan of the segment counts.
+// list at the offsets of an exclusive scan of the segment counts: one wave per segment, each
+// candidate placed at its rank among the segment's (positions are distinct), counted against the
+// segment's list in LDS.  (One thread per segment with an insertion sort through global memory took
+// 0.17 ms, its dense segments' quadratic chains of dependent reads.)
 extern "C" __global__ void __launch_bounds__(256)
 ndfl_inflate_compact_kernel(const uint32_t* seg_cnt, const uint64_t* seg_list, const uint64_t* seg_off,
                             uint32_t nseg, uint64_t* out) {
     using namespace inf;
-    const uint32_t seg = blockIdx.x * blockDim.x + threadIdx.x;
-    if (seg >= nseg) return;
+    __shared__ uint64_t sv[4][SEG_CAP];
+    const uint32_t wid = threadIdx.x >> 6, lane = threadIdx.x & 63u;
+    const uint32_t seg = blockIdx.x * 4 + wid;
+    if (seg >= nseg) return;                    // (no workgroup barrier below)
     const uint32_t c = min(seg_cnt[seg], SEG_CAP);
+    const uint64_t* src = seg_list + (uint64_t)seg * SEG_CAP;
     uint64_t* o = out + seg_off[seg];
-    for (uint32_t i = 0; i < c; i++) {
-        uint64_t v = seg_list[(uint64_t)seg * SEG_CAP + i];
-        uint32_t j = i;
-        while (j > 0 && o[j - 1] > v) { o[j] = o[j - 1]; j--; }
-        o[j] = v;
+    static_assert(SEG_CAP == 256, "four candidates per lane");
+    uint64_t v[4];
+#pragma unroll
+    for (int q = 0; q < 4; q++) {
+        const uint32_t i = lane + 64u * q;
+        v[q] = i < c ? src[i] : ~0ull;
+        if (i < c) sv[wid][i] = v[q];
     }
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+    uint32_t r[4] = {0, 0, 0, 0};
+    for (uint32_t j = 0; j < c; j++) {
+        const uint64_t u = sv[wid][j];
+#pragma unroll
+        for (int q = 0; q < 4; q++) r[q] += u < v[q] ? 1u : 0u;
+    }
+#pragma unroll
+    for (int q = 0; q < 4; q++)
+        if (lane + 64u * q < c) o[r[q]] = v[q];
 }
 
 struct ChainRes {
@@ -795,11 +817,24 @@ ndfl_inflate_segscan_kernel(const uint32_t* cnt, uint32_t nseg, uint64_t* segoff
     __shared__ uint64_t sh[16];
     const uint32_t per = (nseg + 1023) / 1024;
     const uint32_t b0 = min(nseg, threadIdx.x * per), b1 = min(nseg, b0 + per);
+    // (eight loads in flight per batch)
     uint64_t sum = 0;
-    for (uint32_t i = b0; i < b1; i++) sum += min(cnt[i], SEG_CAP);
+    for (uint32_t i = b0; i < b1; i += 8) {
+        uint32_t x[8];
+#pragma unroll
+        for (int k = 0; k < 8; k++) x[k] = i + k < b1 ? min(cnt[i + k], SEG_CAP) : 0u;
+#pragma unroll
+        for (int k = 0; k < 8; k++) sum += x[k];
+    }
     uint64_t tot;
     uint64_t run = 1 + block_excl_scan<uint64_t, 16>(sum, sh, tot);
-    for (uint32_t i = b0; i < b1; i++) { segoff[i] = run; run += min(cnt[i], SEG_CAP); }
+    for (uint32_t i = b0; i < b1; i += 8) {
+        uint32_t x[8];
+#pragma unroll
+        for (int k = 0; k < 8; k++) x[k] = i + k < b1 ? min(cnt[i + k], SEG_CAP) : 0u;
+#pragma unroll
+        for (int k = 0; k < 8; k++) if (i + k < b1) { segoff[i + k] = run; run += x[k]; }
+    }
     if (threadIdx.x == 0) info[LI_NCAND_ALL] = 1 + tot;
 }
 
@@ -873,21 +908,45 @@ ndfl_inflate_order_kernel(const uint64_t* cands, uint32_t n, uint64_t end_bit, u
     __shared__ uint32_t bc[NB + 1];
     if (threadIdx.x <= NB) bc[threadIdx.x] = 0;
     __syncthreads();
-    auto bucket = [&](uint32_t k) -> uint32_t {
-        const uint64_t nx = k + 1 < n ? cands[k + 1] : end_bit;
-        const uint64_t len = nx > cands[k] ? nx - cands[k] : 0;
-        return NB - 1 - (uint32_t)min<uint64_t>(NB - 1, len >> 15);
+    // (the passes take 8 items per thread at a time, their loads unconditional at clamped indices so
+    // that they are in flight together: one load wait per batch instead of one per item)
+    constexpr uint32_t NI = 8;
+    auto batch = [&](uint32_t k0, uint32_t (&bk)[NI]) {
+        uint64_t c0[NI], c1[NI];
+        uint32_t rp[NI];
+#pragma unroll
+        for (uint32_t j = 0; j < NI; j++) {
+            const uint32_t k = min(k0 + j * blockDim.x, n - 1);
+            c0[j] = cands[k];
+            c1[j] = cands[min(k + 1, n - 1)];
+            rp[j] = rep ? rep[k] : k;
+        }
+#pragma unroll
+        for (uint32_t j = 0; j < NI; j++) {
+            const uint32_t k = k0 + j * blockDim.x;
+            const uint64_t nx = k + 1 < n ? c1[j] : end_bit;
+            const uint64_t len = nx > c0[j] ? nx - c0[j] : 0;
+            bk[j] = (k < n && rp[j] == k) ? NB - 1 - (uint32_t)min<uint64_t>(NB - 1, len >> 15) : NB;
+        }
     };
-    for (uint32_t k = threadIdx.x; k < n; k += blockDim.x)
-        if (!rep || rep[k] == k) atomicAdd(&bc[bucket(k) + 1], 1u);
+    for (uint32_t k0 = threadIdx.x; k0 < n; k0 += NI * blockDim.x) {
+        uint32_t bk[NI];
+        batch(k0, bk);
+#pragma unroll
+        for (uint32_t j = 0; j < NI; j++) if (bk[j] < NB) atomicAdd(&bc[bk[j] + 1], 1u);
+    }
     __syncthreads();
     if (threadIdx.x == 0) {
         for (uint32_t b = 0; b < NB; b++) bc[b + 1] += bc[b];
         if (nord) *nord = bc[NB];
     }
     __syncthreads();
-    for (uint32_t k = threadIdx.x; k < n; k += blockDim.x)
-        if (!rep || rep[k] == k) order[atomicAdd(&bc[bucket(k)], 1u)] = k;
+    for (uint32_t k0 = threadIdx.x; k0 < n; k0 += NI * blockDim.x) {
+        uint32_t bk[NI];
+        batch(k0, bk);
+#pragma unroll
+        for (uint32_t j = 0; j < NI; j++) if (bk[j] < NB) order[atomicAdd(&bc[bk[j]], 1u)] = k0 + j * blockDim.x;
+    }
 }
 
 // The emit pass's claim order over the linked chain list (info[LI_NCH] chains): costliest first, by
@@ -906,11 +965,25 @@ ndfl_inflate_emit_order_kernel(const EmitChain* chains, const uint64_t* info, ui
         const uint64_t key = ((e.end_bit - e.start_bit) >> 15) + (e.out_count >> 14);
         return NB - 1 - (uint32_t)min<uint64_t>(NB - 1, key);
     };
-    for (uint32_t k = threadIdx.x; k < n; k += blockDim.x) atomicAdd(&bc[bucket(k) + 1], 1u);
+    constexpr uint32_t NI = 8;                  // (items per thread per batch, loads in flight together)
+    for (uint32_t k0 = threadIdx.x; k0 < n; k0 += NI * blockDim.x) {
+        uint32_t bk[NI];
+#pragma unroll
+        for (uint32_t j = 0; j < NI; j++) bk[j] = bucket(min(k0 + j * blockDim.x, n - 1));
+#pragma unroll
+        for (uint32_t j = 0; j < NI; j++) if (k0 + j * blockDim.x < n) atomicAdd(&bc[bk[j] + 1], 1u);
+    }
     __syncthreads();
     if (threadIdx.x == 0) for (uint32_t b = 0; b < NB; b++) bc[b + 1] += bc[b];
     __syncthreads();
-    for (uint32_t k = threadIdx.x; k < n; k += blockDim.x) order[atomicAdd(&bc[bucket(k)], 1u)] = k;
+    for (uint32_t k0 = threadIdx.x; k0 < n; k0 += NI * blockDim.x) {
+        uint32_t bk[NI];
+#pragma unroll
+        for (uint32_t j = 0; j < NI; j++) bk[j] = bucket(min(k0 + j * blockDim.x, n - 1));
+#pragma unroll
+        for (uint32_t j = 0; j < NI; j++)
+            if (k0 + j * blockDim.x < n) order[atomicAdd(&bc[bk[j]], 1u)] = k0 + j * blockDim.x;
+    }
 }
 
 // Linking by pointer jumping.  Chain k links to the chain starting where it stopped when it stopped
@@ -984,8 +1057,15 @@ ndfl_inflate_summary_kernel(const ChainRes* er, const EmitChain* chains, uint64_
     if (threadIdx.x == 0) first = NOLINK;
     __syncthreads();
     const uint32_t nch = (uint32_t)info[LI_NCH];
-    for (uint32_t k = threadIdx.x; k < nch; k += blockDim.x)
-        if (er[k].status == ST_ERROR) atomicMin(&first, k);
+    constexpr uint32_t NI = 8;                  // (items per thread per batch, loads in flight together)
+    for (uint32_t k0 = threadIdx.x; k0 < nch; k0 += NI * blockDim.x) {
+        uint32_t st[NI];
+#pragma unroll
+        for (uint32_t j = 0; j < NI; j++) st[j] = er[min(k0 + j * blockDim.x, nch - 1)].status;
+#pragma unroll
+        for (uint32_t j = 0; j < NI; j++)
+            if (k0 + j * blockDim.x < nch && st[j] == ST_ERROR) atomicMin(&first, k0 + j * blockDim.x);
+    }
     __syncthreads();
     if (threadIdx.x != 0) return;
     if (first == NOLINK) {
@@ -1305,7 +1385,7 @@ static int inflate_devlink(InflateScratch& S, hipStream_t s, const uint32_t* d_w
     uint64_t* d_segoff = d_sorted + cap_all;
     hipLaunchKernelGGL(ndfl_inflate_segscan_kernel, dim3(1), dim3(1024), 0, s, d_cnt, nseg, d_segoff, info);
     INF_CHK(hipGetLastError());
-    hipLaunchKernelGGL(ndfl_inflate_compact_kernel, dim3((nseg + 255) / 256), dim3(256), 0, s, d_cnt, d_list,
+    hipLaunchKernelGGL(ndfl_inflate_compact_kernel, dim3((nseg + 3) / 4), dim3(256), 0, s, d_cnt, d_list,
                        (const uint64_t*)d_segoff, nseg, d_sorted);
     INF_CHK(hipGetLastError());
     INF_CHK(inf_ensure(&S.d_cands, &S.d_cands_cap, (cap_all + 1) * 8ull));
@@ -1705,7 +1785,7 @@ refind:
     uint64_t* d_sorted = (uint64_t*)S.d_starts;
     uint64_t* d_segoff = d_sorted + ncand_all;
     INF_CHK(hipMemcpyAsync(d_segoff, hoff.data(), nseg * 8ull, hipMemcpyHostToDevice, s));
-    hipLaunchKernelGGL(ndfl_inflate_compact_kernel, dim3((nseg + 255) / 256), dim3(256), 0, s, (const uint32_t*)d_cnt,
+    hipLaunchKernelGGL(ndfl_inflate_compact_kernel, dim3((nseg + 3) / 4), dim3(256), 0, s, (const uint32_t*)d_cnt,
                        (const uint64_t*)d_list, (const uint64_t*)d_segoff, nseg, d_sorted);
     INF_CHK(hipGetLastError());
     std::vector<uint64_t> starts(ncand_all);
