@@ -298,7 +298,7 @@ int ndfl_deflate_chunks(ndfl_ctx* c, const uint8_t* hist, uint32_t hist_len, uin
     if (split) {
         HIPCHK(c->d_hist.ensure((size_t)nch * HREC * 4));
         HIPCHK(c->d_codes.ensure((size_t)nch * CREC * 4));
-        HIPCHK(c->d_off.ensure((size_t)nch * 8 + 64));
+        HIPCHK(c->d_off.ensure((size_t)nch * 8 + 64 + (size_t)((nch + SCAN_TILE - 1) / SCAN_TILE) * 8));
         a.hist_out = c->d_hist.as<uint32_t>();
         a.codes = c->d_codes.as<uint32_t>();
         a.chunk_off = c->d_off.as<uint64_t>();
@@ -311,8 +311,13 @@ int ndfl_deflate_chunks(ndfl_ctx* c, const uint8_t* hist, uint32_t hist_len, uin
         HIPCHK(hipGetLastError());
         hipLaunchKernelGGL(ndfl_deflate_codes_kernel, dim3(nch), dim3(64), 0, s, a);
         HIPCHK(hipGetLastError());
-        hipLaunchKernelGGL(ndfl_deflate_offsets_kernel, dim3(1), dim3(1024), 0, s, (const uint64_t*)a.status, nch,
-                           (uint64_t)start_bitpos, c->d_off.as<uint64_t>(), d_total, (const uint64_t*)nullptr);
+        const uint32_t ntile = (nch + SCAN_TILE - 1) / SCAN_TILE;
+        uint64_t* d_part = c->d_off.as<uint64_t>() + nch + 8;
+        hipLaunchKernelGGL(ndfl_deflate_offsets_sum_kernel, dim3(ntile), dim3(SCAN_T), 0, s, (const uint64_t*)a.status,
+                           nch, d_part);
+        HIPCHK(hipGetLastError());
+        hipLaunchKernelGGL(ndfl_deflate_offsets_kernel, dim3(ntile), dim3(SCAN_T), 0, s, (const uint64_t*)a.status, nch,
+                           (uint64_t)start_bitpos, c->d_off.as<uint64_t>(), d_total, (const uint64_t*)d_part);
         HIPCHK(hipGetLastError());
         hipLaunchKernelGGL(ndfl_deflate_emit_kernel, dim3(nch), dim3(1024), 0, s, a);
     } else {

@@ -389,35 +389,15 @@ ndfl_deflate_codes_kernel(Args a) {
     }
 }
 
-// Pass 3: chunk c's global bit offset = base + sum of the sizes before it; total[0] = end bit.
-// One workgroup; thread t scans a contiguous range of chunks.  base = *base_ptr when base_ptr is set
-// (the slab pipeline: a slab's chunks start at the end bit of the slab before it, which that slab's
-// offsets launch wrote on the device; base_ptr may equal total).
-extern "C" __global__ void __launch_bounds__(1024)
+// Pass 3: chunk c's global bit offset = base + sum of the sizes before it; total[0] = end bit.  Two
+// launches (ndfl_common.hpp scan_tile_*): the tile sums, then each tile's scan; grid = tiles.
+extern "C" __global__ void __launch_bounds__(SCAN_T)
+ndfl_deflate_offsets_sum_kernel(const uint64_t* sizes, uint32_t n, uint64_t* part) {
+    scan_tile_sum([&](uint32_t i) { return sizes[i]; }, n, part);
+}
+extern "C" __global__ void __launch_bounds__(SCAN_T)
 ndfl_deflate_offsets_kernel(const uint64_t* sizes, uint32_t n, uint64_t base, uint64_t* off, uint64_t* total,
-                            const uint64_t* base_ptr) {
-    __shared__ uint64_t sh[16];
-    if (base_ptr) base = *base_ptr;
-    __syncthreads();                        // (every thread has read *base_ptr before thread 0 writes total)
-    const uint32_t per = (n + 1023) / 1024;
-    const uint32_t b0 = min(n, threadIdx.x * per), b1 = min(n, b0 + per);
-    // (eight loads in flight per batch: a load-then-add loop waits out every load in turn)
-    uint64_t sum = 0;
-    for (uint32_t i = b0; i < b1; i += 8) {
-        uint64_t x[8];
-#pragma unroll
-        for (int k = 0; k < 8; k++) x[k] = i + k < b1 ? sizes[i + k] : 0ull;
-#pragma unroll
-        for (int k = 0; k < 8; k++) sum += x[k];
-    }
-    uint64_t tot;
-    uint64_t run = base + block_excl_scan<uint64_t, 16>(sum, sh, tot);
-    for (uint32_t i = b0; i < b1; i += 8) {
-        uint64_t x[8];
-#pragma unroll
-        for (int k = 0; k < 8; k++) x[k] = i + k < b1 ? sizes[i + k] : 0ull;
-#pragma unroll
-        for (int k = 0; k < 8; k++) if (i + k < b1) { off[i + k] = run; run += x[k]; }
-    }
-    if (threadIdx.x == 0) total[0] = base + tot;
+                            const uint64_t* part) {
+    scan_tile_apply([&](uint32_t i) { return sizes[i]; }, [&](uint32_t i, uint64_t v) { off[i] = v; }, n, part, base,
+                    total);
 }

@@ -810,36 +810,20 @@ enum : uint64_t { LF_REPAIR = 1, LF_RANGE = 2, LF_CAPACITY = 4 };
 constexpr uint32_t NOLINK = 0xFFFFFFFFu;
 
 // Exclusive scan of the finder segments' candidate counts (capped at SEG_CAP) from 1 (slot 0 is
-// the range start): the compact kernel's offsets; info[LI_NCAND_ALL] = the list length.
-extern "C" __global__ void __launch_bounds__(1024)
-ndfl_inflate_segscan_kernel(const uint32_t* cnt, uint32_t nseg, uint64_t* segoff, uint64_t* info) {
+// the range start): the compact kernel's offsets; info[LI_NCAND_ALL] = the list length.  Two
+// launches (ndfl_common.hpp scan_tile_*); grid = tiles.
+extern "C" __global__ void __launch_bounds__(SCAN_T)
+ndfl_inflate_segsum_kernel(const uint32_t* cnt, uint32_t nseg, uint64_t* part) {
     using namespace inf;
-    __shared__ uint64_t sh[16];
-    const uint32_t per = (nseg + 1023) / 1024;
-    const uint32_t b0 = min(nseg, threadIdx.x * per), b1 = min(nseg, b0 + per);
-    // (eight loads in flight per batch)
-    uint64_t sum = 0;
-    for (uint32_t i = b0; i < b1; i += 8) {
-        uint32_t x[8];
-#pragma unroll
-        for (int k = 0; k < 8; k++) x[k] = i + k < b1 ? min(cnt[i + k], SEG_CAP) : 0u;
-#pragma unroll
-        for (int k = 0; k < 8; k++) sum += x[k];
-    }
-    uint64_t tot;
-    uint64_t run = 1 + block_excl_scan<uint64_t, 16>(sum, sh, tot);
-    for (uint32_t i = b0; i < b1; i += 8) {
-        uint32_t x[8];
-#pragma unroll
-        for (int k = 0; k < 8; k++) x[k] = i + k < b1 ? min(cnt[i + k], SEG_CAP) : 0u;
-#pragma unroll
-        for (int k = 0; k < 8; k++) if (i + k < b1) { segoff[i + k] = run; run += x[k]; }
-    }
-    if (threadIdx.x == 0) info[LI_NCAND_ALL] = 1 + tot;
+    scan_tile_sum([&](uint32_t i) { return (uint64_t)min(cnt[i], SEG_CAP); }, nseg, part);
+}
+extern "C" __global__ void __launch_bounds__(SCAN_T)
+ndfl_inflate_segscan_kernel(const uint32_t* cnt, uint32_t nseg, uint64_t* segoff, uint64_t* info, const uint64_t* part) {
+    using namespace inf;
+    scan_tile_apply([&](uint32_t i) { return (uint64_t)min(cnt[i], SEG_CAP); },
+                    [&](uint32_t i, uint64_t v) { segoff[i] = v; }, nseg, part, 1, info + LI_NCAND_ALL);
 }
 
-// The chain starts: the range start, then the sorted candidates strictly inside (start, end) -- a
-// contiguous slice of the sorted list.  info[LI_NCAND] = their number.
 extern "C" __global__ void __launch_bounds__(256)
 ndfl_inflate_cand_slice_kernel(const uint64_t* sorted, uint64_t* info, uint64_t start_bit, uint64_t end_bit,
                                uint64_t* cands) {
@@ -897,93 +881,114 @@ ndfl_inflate_alias_mark_kernel(const uint64_t* cands, uint64_t* info, const uint
     }
 }
 
+// Bucket orders (the count and emit passes' claim orders) in two launches over tiles of SCAN_TILE
+// items, like the scans: the first adds each block's bucket counts into tot[OB_NB]; the second
+// places the block's items -- bucket b's slots start at the sum of tot[0..b) plus what the blocks
+// before it in arrival order took of bucket b (cursor[b]).  tot and cursor start at zero.  (One
+// workgroup over the whole list ran at one CU's bandwidth from other XCDs' data: ~80 us each.)
+constexpr uint32_t OB_NB = 24;
+constexpr uint32_t OB_WORDS = 2 * OB_NB;      // tot, cursor
+constexpr size_t CTK_BYTES = 512;             // chain ticket, nord, two bucket orders, first error
+static_assert((16 + 2 * OB_WORDS + 1) * 4 <= CTK_BYTES, "ticket buffer layout");
+template <class Bk>
+__device__ __forceinline__ void border_count(Bk bk, uint32_t n, uint32_t* ob) {
+    __shared__ uint32_t h[OB_NB];
+    const uint32_t t = threadIdx.x;
+    if (t < OB_NB) h[t] = 0;
+    __syncthreads();
+    const uint32_t i0 = blockIdx.x * SCAN_TILE + t * SCAN_PER;
+    if (i0 < n) {
+        uint32_t b[SCAN_PER];
+#pragma unroll
+        for (uint32_t k = 0; k < SCAN_PER; k++) b[k] = bk(min(i0 + k, n - 1));
+#pragma unroll
+        for (uint32_t k = 0; k < SCAN_PER; k++) if (i0 + k < n && b[k] < OB_NB) atomicAdd(&h[b[k]], 1u);
+    }
+    __syncthreads();
+    if (t < OB_NB && h[t]) atomicAdd(&ob[t], h[t]);
+}
+template <class Bk>
+__device__ __forceinline__ void border_place(Bk bk, uint32_t n, uint32_t* ob, uint32_t* order, uint32_t* ntot) {
+    __shared__ uint32_t h[OB_NB], base[OB_NB];
+    const uint32_t t = threadIdx.x;
+    if (t < OB_NB) h[t] = 0;
+    __syncthreads();
+    const uint32_t i0 = blockIdx.x * SCAN_TILE + t * SCAN_PER;
+    uint32_t b[SCAN_PER];
+#pragma unroll
+    for (uint32_t k = 0; k < SCAN_PER; k++) b[k] = OB_NB;
+    if (i0 < n) {
+#pragma unroll
+        for (uint32_t k = 0; k < SCAN_PER; k++) b[k] = bk(min(i0 + k, n - 1));
+#pragma unroll
+        for (uint32_t k = 0; k < SCAN_PER; k++) {
+            if (i0 + k >= n) b[k] = OB_NB;
+            if (b[k] < OB_NB) atomicAdd(&h[b[k]], 1u);
+        }
+    }
+    __syncthreads();
+    if (t < OB_NB) {
+        uint32_t p = 0;
+        for (uint32_t q = 0; q < t; q++) p += ob[q];
+        base[t] = p + (h[t] ? atomicAdd(&ob[OB_NB + t], h[t]) : 0u);
+        h[t] = 0;
+    }
+    __syncthreads();
+#pragma unroll
+    for (uint32_t k = 0; k < SCAN_PER; k++)
+        if (b[k] < OB_NB) order[base[b[k]] + atomicAdd(&h[b[k]], 1u)] = i0 + k;
+    if (ntot && blockIdx.x == 0 && t == 0) {
+        uint32_t p = 0;
+        for (uint32_t q = 0; q < OB_NB; q++) p += ob[q];
+        *ntot = p;
+    }
+}
+
 // Claim order of the count pass: longest first by the bits to the next start (24 buckets of 32
-// Kibit), so that no long chain is left for the end of the launch.  One workgroup.  With `rep`
+// Kibit), so that no long chain is left for the end of the launch.  With `rep`
 // (ndfl_inflate_alias_mark_kernel), stored-header aliases are left out of the order (*nord = the
-// chains to count).
-extern "C" __global__ void __launch_bounds__(1024)
+// chains to count).  grid = tiles of n.
+struct OrderBucket {
+    const uint64_t* cands; uint32_t n; uint64_t end_bit; const uint32_t* rep;
+    __device__ __forceinline__ uint32_t operator()(uint32_t k) const {
+        const uint64_t c0 = cands[k], c1 = cands[min(k + 1, n - 1)];
+        const uint32_t r = rep ? rep[k] : k;
+        const uint64_t nx = k + 1 < n ? c1 : end_bit;
+        const uint64_t len = nx > c0 ? nx - c0 : 0;
+        return r == k ? OB_NB - 1 - (uint32_t)min<uint64_t>(OB_NB - 1, len >> 15) : OB_NB;
+    }
+};
+extern "C" __global__ void __launch_bounds__(SCAN_T)
+ndfl_inflate_order_count_kernel(const uint64_t* cands, uint32_t n, uint64_t end_bit, const uint32_t* rep, uint32_t* ob) {
+    border_count(OrderBucket{cands, n, end_bit, rep}, n, ob);
+}
+extern "C" __global__ void __launch_bounds__(SCAN_T)
 ndfl_inflate_order_kernel(const uint64_t* cands, uint32_t n, uint64_t end_bit, uint32_t* order, const uint32_t* rep,
-                          uint32_t* nord) {
-    constexpr uint32_t NB = 24;
-    __shared__ uint32_t bc[NB + 1];
-    if (threadIdx.x <= NB) bc[threadIdx.x] = 0;
-    __syncthreads();
-    // (the passes take 8 items per thread at a time, their loads unconditional at clamped indices so
-    // that they are in flight together: one load wait per batch instead of one per item)
-    constexpr uint32_t NI = 8;
-    auto batch = [&](uint32_t k0, uint32_t (&bk)[NI]) {
-        uint64_t c0[NI], c1[NI];
-        uint32_t rp[NI];
-#pragma unroll
-        for (uint32_t j = 0; j < NI; j++) {
-            const uint32_t k = min(k0 + j * blockDim.x, n - 1);
-            c0[j] = cands[k];
-            c1[j] = cands[min(k + 1, n - 1)];
-            rp[j] = rep ? rep[k] : k;
-        }
-#pragma unroll
-        for (uint32_t j = 0; j < NI; j++) {
-            const uint32_t k = k0 + j * blockDim.x;
-            const uint64_t nx = k + 1 < n ? c1[j] : end_bit;
-            const uint64_t len = nx > c0[j] ? nx - c0[j] : 0;
-            bk[j] = (k < n && rp[j] == k) ? NB - 1 - (uint32_t)min<uint64_t>(NB - 1, len >> 15) : NB;
-        }
-    };
-    for (uint32_t k0 = threadIdx.x; k0 < n; k0 += NI * blockDim.x) {
-        uint32_t bk[NI];
-        batch(k0, bk);
-#pragma unroll
-        for (uint32_t j = 0; j < NI; j++) if (bk[j] < NB) atomicAdd(&bc[bk[j] + 1], 1u);
-    }
-    __syncthreads();
-    if (threadIdx.x == 0) {
-        for (uint32_t b = 0; b < NB; b++) bc[b + 1] += bc[b];
-        if (nord) *nord = bc[NB];
-    }
-    __syncthreads();
-    for (uint32_t k0 = threadIdx.x; k0 < n; k0 += NI * blockDim.x) {
-        uint32_t bk[NI];
-        batch(k0, bk);
-#pragma unroll
-        for (uint32_t j = 0; j < NI; j++) if (bk[j] < NB) order[atomicAdd(&bc[bk[j]], 1u)] = k0 + j * blockDim.x;
-    }
+                          uint32_t* nord, uint32_t* ob) {
+    border_place(OrderBucket{cands, n, end_bit, rep}, n, ob, order, nord);
 }
 
 // The emit pass's claim order over the linked chain list (info[LI_NCH] chains): costliest first, by
 // a cost key of input bits and output bytes (32 Kbit or 16 KiB per unit), so that no long chain --
-// a stream's last blocks, which share one chain -- starts at the end of the pass.  One workgroup.
-extern "C" __global__ void __launch_bounds__(1024)
-ndfl_inflate_emit_order_kernel(const EmitChain* chains, const uint64_t* info, uint32_t* order) {
-    constexpr uint32_t NB = 24;
-    __shared__ uint32_t bc[NB + 1];
-    if (info[LI_FLAGS]) return;                 // (the emit pass does not run)
-    const uint32_t n = (uint32_t)info[LI_NCH];
-    if (threadIdx.x <= NB) bc[threadIdx.x] = 0;
-    __syncthreads();
-    auto bucket = [&](uint32_t k) -> uint32_t {
+// a stream's last blocks, which share one chain -- starts at the end of the pass.  grid = tiles of
+// an upper bound of the chains (the candidates).
+struct EmitBucket {
+    const EmitChain* chains;
+    __device__ __forceinline__ uint32_t operator()(uint32_t k) const {
         const EmitChain& e = chains[k];
         const uint64_t key = ((e.end_bit - e.start_bit) >> 15) + (e.out_count >> 14);
-        return NB - 1 - (uint32_t)min<uint64_t>(NB - 1, key);
-    };
-    constexpr uint32_t NI = 8;                  // (items per thread per batch, loads in flight together)
-    for (uint32_t k0 = threadIdx.x; k0 < n; k0 += NI * blockDim.x) {
-        uint32_t bk[NI];
-#pragma unroll
-        for (uint32_t j = 0; j < NI; j++) bk[j] = bucket(min(k0 + j * blockDim.x, n - 1));
-#pragma unroll
-        for (uint32_t j = 0; j < NI; j++) if (k0 + j * blockDim.x < n) atomicAdd(&bc[bk[j] + 1], 1u);
+        return OB_NB - 1 - (uint32_t)min<uint64_t>(OB_NB - 1, key);
     }
-    __syncthreads();
-    if (threadIdx.x == 0) for (uint32_t b = 0; b < NB; b++) bc[b + 1] += bc[b];
-    __syncthreads();
-    for (uint32_t k0 = threadIdx.x; k0 < n; k0 += NI * blockDim.x) {
-        uint32_t bk[NI];
-#pragma unroll
-        for (uint32_t j = 0; j < NI; j++) bk[j] = bucket(min(k0 + j * blockDim.x, n - 1));
-#pragma unroll
-        for (uint32_t j = 0; j < NI; j++)
-            if (k0 + j * blockDim.x < n) order[atomicAdd(&bc[bk[j]], 1u)] = k0 + j * blockDim.x;
-    }
+};
+extern "C" __global__ void __launch_bounds__(SCAN_T)
+ndfl_inflate_emit_order_count_kernel(const EmitChain* chains, const uint64_t* info, uint32_t* ob) {
+    if (info[LI_FLAGS]) return;                 // (the emit pass does not run)
+    border_count(EmitBucket{chains}, (uint32_t)info[LI_NCH], ob);
+}
+extern "C" __global__ void __launch_bounds__(SCAN_T)
+ndfl_inflate_emit_order_kernel(const EmitChain* chains, const uint64_t* info, uint32_t* order, uint32_t* ob) {
+    if (info[LI_FLAGS]) return;
+    border_place(EmitBucket{chains}, (uint32_t)info[LI_NCH], ob, order, (uint32_t*)nullptr);
 }
 
 // Linking by pointer jumping.  Chain k links to the chain starting where it stopped when it stopped
@@ -1049,25 +1054,27 @@ ndfl_inflate_link_path_kernel(const uint32_t* Jall, uint32_t nlev, const uint64_
 }
 // The decode's result from the emit pass's chain results: the first error in stream order (a
 // partial-input decode that ran out of input inside a block stops at that block's start instead).
-extern "C" __global__ void __launch_bounds__(1024)
-ndfl_inflate_summary_kernel(const ChainRes* er, const EmitChain* chains, uint64_t* info, uint64_t dict_len,
-                            uint32_t partial) {
+// ndfl_inflate_first_error_kernel (grid = tiles of an upper bound of the chains) leaves the first
+// erring chain in *first (set to ~0 before); the summary kernel (one thread) writes the result.
+extern "C" __global__ void __launch_bounds__(SCAN_T)
+ndfl_inflate_first_error_kernel(const ChainRes* er, const uint64_t* info, uint32_t* first) {
     using namespace inf;
-    __shared__ uint32_t first;
-    if (threadIdx.x == 0) first = NOLINK;
-    __syncthreads();
     const uint32_t nch = (uint32_t)info[LI_NCH];
-    constexpr uint32_t NI = 8;                  // (items per thread per batch, loads in flight together)
-    for (uint32_t k0 = threadIdx.x; k0 < nch; k0 += NI * blockDim.x) {
-        uint32_t st[NI];
+    const uint32_t i0 = blockIdx.x * SCAN_TILE + threadIdx.x * SCAN_PER;
+    if (i0 >= nch) return;
+    uint32_t st[SCAN_PER];
 #pragma unroll
-        for (uint32_t j = 0; j < NI; j++) st[j] = er[min(k0 + j * blockDim.x, nch - 1)].status;
+    for (uint32_t k = 0; k < SCAN_PER; k++) st[k] = er[min(i0 + k, nch - 1)].status;
 #pragma unroll
-        for (uint32_t j = 0; j < NI; j++)
-            if (k0 + j * blockDim.x < nch && st[j] == ST_ERROR) atomicMin(&first, k0 + j * blockDim.x);
-    }
-    __syncthreads();
+    for (uint32_t k = 0; k < SCAN_PER; k++)
+        if (i0 + k < nch && st[k] == ST_ERROR) { atomicMin(first, i0 + k); break; }
+}
+extern "C" __global__ void __launch_bounds__(64)
+ndfl_inflate_summary_kernel(const ChainRes* er, const EmitChain* chains, uint64_t* info, uint64_t dict_len,
+                            uint32_t partial, const uint32_t* firstp) {
+    using namespace inf;
     if (threadIdx.x != 0) return;
+    const uint32_t first = *firstp;
     if (first == NOLINK) {
         info[LI_CODE] = 0; info[LI_OUTLEN] = info[LI_TOTAL]; info[LI_CONSUMED] = info[LI_STOP];
         return;
@@ -1380,10 +1387,15 @@ static int inflate_devlink(InflateScratch& S, hipStream_t s, const uint32_t* d_w
     volatile uint64_t* hinfo = (volatile uint64_t*)S.h_info;
     INF_CHK(hipMemsetAsync(info, 0, LI_WORDS * 8, s));
     const uint64_t cap_all = (uint64_t)nseg * SEG_CAP + 1;      // the sorted list's length at most
-    INF_CHK(inf_ensure(&S.d_starts, &S.d_starts_cap, (cap_all + nseg + 2) * 8));
+    const uint32_t ntile = (nseg + SCAN_TILE - 1) / SCAN_TILE;
+    INF_CHK(inf_ensure(&S.d_starts, &S.d_starts_cap, (cap_all + nseg + 2 + ntile) * 8));
     uint64_t* d_sorted = (uint64_t*)S.d_starts;
     uint64_t* d_segoff = d_sorted + cap_all;
-    hipLaunchKernelGGL(ndfl_inflate_segscan_kernel, dim3(1), dim3(1024), 0, s, d_cnt, nseg, d_segoff, info);
+    uint64_t* d_part = d_segoff + nseg + 2;
+    hipLaunchKernelGGL(ndfl_inflate_segsum_kernel, dim3(ntile), dim3(SCAN_T), 0, s, d_cnt, nseg, d_part);
+    INF_CHK(hipGetLastError());
+    hipLaunchKernelGGL(ndfl_inflate_segscan_kernel, dim3(ntile), dim3(SCAN_T), 0, s, d_cnt, nseg, d_segoff, info,
+                       (const uint64_t*)d_part);
     INF_CHK(hipGetLastError());
     hipLaunchKernelGGL(ndfl_inflate_compact_kernel, dim3((nseg + 3) / 4), dim3(256), 0, s, d_cnt, d_list,
                        (const uint64_t*)d_segoff, nseg, d_sorted);
@@ -1427,11 +1439,16 @@ static int inflate_devlink(InflateScratch& S, hipStream_t s, const uint32_t* d_w
     INF_CHK(inf_ensure(&S.d_stops, &S.d_stops_cap, n * 12));
     INF_CHK(inf_ensure(&S.d_res, &S.d_res_cap, n * sizeof(ChainRes)));
     uint32_t* d_order = (uint32_t*)((char*)S.d_stops + n * 8);
-    if (!S.d_cticket) INF_CHK(hipMalloc(&S.d_cticket, 64));
-    INF_CHK(hipMemsetAsync(S.d_cticket, 0, 4, s));
+    if (!S.d_cticket) INF_CHK(hipMalloc(&S.d_cticket, CTK_BYTES));
+    INF_CHK(hipMemsetAsync(S.d_cticket, 0, CTK_BYTES, s));
     uint32_t* d_nord = (uint32_t*)S.d_cticket + 8;
-    hipLaunchKernelGGL(ndfl_inflate_order_kernel, dim3(1), dim3(1024), 0, s, (const uint64_t*)S.d_cands, ncand, end_bit,
-                       d_order, (const uint32_t*)d_rep, alias_on ? d_nord : (uint32_t*)nullptr);
+    uint32_t* d_ob = (uint32_t*)S.d_cticket + 16;                      // count order: tot, cursor
+    const uint32_t otiles = (ncand + SCAN_TILE - 1) / SCAN_TILE;
+    hipLaunchKernelGGL(ndfl_inflate_order_count_kernel, dim3(otiles), dim3(SCAN_T), 0, s, (const uint64_t*)S.d_cands,
+                       ncand, end_bit, (const uint32_t*)d_rep, d_ob);
+    INF_CHK(hipGetLastError());
+    hipLaunchKernelGGL(ndfl_inflate_order_kernel, dim3(otiles), dim3(SCAN_T), 0, s, (const uint64_t*)S.d_cands, ncand,
+                       end_bit, d_order, (const uint32_t*)d_rep, alias_on ? d_nord : (uint32_t*)nullptr, d_ob);
     INF_CHK(hipGetLastError());
     if (!S.d_ph) INF_CHK(hipMalloc(&S.d_ph, (size_t)std::max(COUNT_WAVES, EMIT_WAVES) * sizeof(wv::PhArr)));
     const bool stats_on = S.knobs.stats;
@@ -1499,9 +1516,16 @@ static int inflate_devlink(InflateScratch& S, hipStream_t s, const uint32_t* d_w
                        (const uint64_t*)S.d_cands, ncand, dict_len, end_bit, out_cap, (EmitChain*)S.d_chains, info);
     INF_CHK(hipGetLastError());
     // the emit pass claims the linked chains costliest first (the count pass's order buffer is free)
-    hipLaunchKernelGGL(ndfl_inflate_emit_order_kernel, dim3(1), dim3(1024), 0, s, (const EmitChain*)S.d_chains,
-                       (const uint64_t*)info, d_order);
-    INF_CHK(hipGetLastError());
+    {
+        uint32_t* d_eob = (uint32_t*)S.d_cticket + 16 + OB_WORDS;      // emit order: tot, cursor (zeroed above)
+        const uint32_t etiles = (ncand + SCAN_TILE - 1) / SCAN_TILE;    // (chains <= candidates)
+        hipLaunchKernelGGL(ndfl_inflate_emit_order_count_kernel, dim3(etiles), dim3(SCAN_T), 0, s,
+                           (const EmitChain*)S.d_chains, (const uint64_t*)info, d_eob);
+        INF_CHK(hipGetLastError());
+        hipLaunchKernelGGL(ndfl_inflate_emit_order_kernel, dim3(etiles), dim3(SCAN_T), 0, s, (const EmitChain*)S.d_chains,
+                           (const uint64_t*)info, d_order, d_eob);
+        INF_CHK(hipGetLastError());
+    }
     // emit into the output (or a device staging buffer sized by the bound out_cap)
     uint8_t* d_out;
     const bool direct = (flags & 2u) != 0;
@@ -1557,9 +1581,16 @@ static int inflate_devlink(InflateScratch& S, hipStream_t s, const uint32_t* d_w
         INF_CHK(hipGetLastError());
     }
     INF_CHK(hipEventRecord(S.ev[5], s));
-    hipLaunchKernelGGL(ndfl_inflate_summary_kernel, dim3(1), dim3(1024), 0, s, (const ChainRes*)S.d_res,
-                       (const EmitChain*)S.d_chains, info, dict_len, partial ? 1u : 0u);
-    INF_CHK(hipGetLastError());
+    {
+        uint32_t* d_first = (uint32_t*)S.d_cticket + 16 + 2 * OB_WORDS;
+        INF_CHK(hipMemsetAsync(d_first, 0xFF, 4, s));
+        hipLaunchKernelGGL(ndfl_inflate_first_error_kernel, dim3((ncand + SCAN_TILE - 1) / SCAN_TILE), dim3(SCAN_T), 0, s,
+                           (const ChainRes*)S.d_res, (const uint64_t*)info, d_first);
+        INF_CHK(hipGetLastError());
+        hipLaunchKernelGGL(ndfl_inflate_summary_kernel, dim3(1), dim3(64), 0, s, (const ChainRes*)S.d_res,
+                           (const EmitChain*)S.d_chains, info, dict_len, partial ? 1u : 0u, (const uint32_t*)d_first);
+        INF_CHK(hipGetLastError());
+    }
     // the resolve rounds, as far as they usually go, without a host read in between
     uint32_t* left = nullptr;
     if (!deferred) {
@@ -1862,7 +1893,7 @@ refind:
         uint32_t* d_order = (uint32_t*)((char*)S.d_stops + n * 8);
         INF_CHK(hipMemcpyAsync(d_order, order.data(), n * 4, hipMemcpyHostToDevice, s));
         if (!S.d_ph) INF_CHK(hipMalloc(&S.d_ph, (size_t)std::max(COUNT_WAVES, EMIT_WAVES) * sizeof(wv::PhArr)));
-        if (!S.d_cticket) INF_CHK(hipMalloc(&S.d_cticket, 64));
+        if (!S.d_cticket) INF_CHK(hipMalloc(&S.d_cticket, CTK_BYTES));
         INF_CHK(hipMemsetAsync(S.d_cticket, 0, 4, s));
         if (S.count_first) INF_CHK(hipEventRecord(S.ev[2], s));
         launch_count(s, count_w(S.knobs), (uint32_t)n,

@@ -120,6 +120,48 @@ __device__ inline T block_excl_scan(T v, T* sh, T& total) {
     return pre;
 }
 
+// Device-wide exclusive scan in two launches over tiles of SCAN_TILE items (SCAN_T threads x
+// SCAN_PER items, loads in flight together): scan_tile_sum writes each tile's sum, scan_tile_apply
+// scans a tile from the sum of the tiles before it (each block adds those partials up itself: no
+// third launch, no block waits on another).  One workgroup over the whole list ran at the bandwidth
+// one CU draws from data other XCDs wrote (~0.1 ms for 65,536 items).  n >= 1.
+constexpr uint32_t SCAN_T = 256, SCAN_PER = 8, SCAN_TILE = SCAN_T * SCAN_PER;
+template <class Ld>
+__device__ __forceinline__ void scan_tile_sum(Ld ld, uint32_t n, uint64_t* part) {
+    __shared__ uint64_t sh[SCAN_T / 64];
+    const uint32_t i0 = blockIdx.x * SCAN_TILE + threadIdx.x * SCAN_PER;
+    uint64_t x[SCAN_PER], v = 0;
+#pragma unroll
+    for (uint32_t k = 0; k < SCAN_PER; k++) x[k] = ld(min(i0 + k, n - 1));
+#pragma unroll
+    for (uint32_t k = 0; k < SCAN_PER; k++) v += i0 + k < n ? x[k] : 0ull;
+    uint64_t tot;
+    block_excl_scan<uint64_t, SCAN_T / 64>(v, sh, tot);
+    if (threadIdx.x == 0) part[blockIdx.x] = tot;
+}
+// st(i, exclusive prefix of item i + init); *grand (if set) = init + the sum of all n items
+template <class Ld, class St>
+__device__ __forceinline__ void scan_tile_apply(Ld ld, St st, uint32_t n, const uint64_t* part, uint64_t init,
+                                                uint64_t* grand) {
+    __shared__ uint64_t sh[SCAN_T / 64], sp[SCAN_T / 64];
+    uint64_t p = 0;
+    for (uint32_t t = threadIdx.x; t < blockIdx.x; t += SCAN_T) p += part[t];
+    uint64_t before;
+    block_excl_scan<uint64_t, SCAN_T / 64>(p, sp, before);
+    const uint32_t i0 = blockIdx.x * SCAN_TILE + threadIdx.x * SCAN_PER;
+    uint64_t x[SCAN_PER], v = 0;
+#pragma unroll
+    for (uint32_t k = 0; k < SCAN_PER; k++) x[k] = ld(min(i0 + k, n - 1));
+#pragma unroll
+    for (uint32_t k = 0; k < SCAN_PER; k++) { if (i0 + k >= n) x[k] = 0; v += x[k]; }
+    uint64_t tot;
+    uint64_t run = init + before + block_excl_scan<uint64_t, SCAN_T / 64>(v, sh, tot);
+#pragma unroll
+    for (uint32_t k = 0; k < SCAN_PER; k++)
+        if (i0 + k < n) { st(i0 + k, run); run += x[k]; }
+    if (grand && blockIdx.x + 1 == gridDim.x && threadIdx.x == 0) *grand = init + before + tot;
+}
+
 // Block-wide exclusive suffix minimum: min over threads t' > t of v[t'] (or `ident`).
 template <int NWAVES>
 __device__ inline uint32_t block_excl_suffix_min(uint32_t v, uint32_t ident, uint32_t* sh) {
