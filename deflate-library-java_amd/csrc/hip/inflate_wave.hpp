@@ -431,8 +431,56 @@ struct Hdr {
     uint64_t pos, d0;
     uint32_t err, bfinal, btype, len, numlit, numdist;
 };
-__device__ __forceinline__ void parse_hdr_core(const In& in, uint64_t p, uint8_t* lens, uint16_t* cl_tab, Hdr& h) {
-    Rd rd;
+// Lane reader over a lane-private LDS window of 8 words (word i of lane j at win[i * 64 + j]: no
+// bank conflicts), refilled by two 16-byte loads in flight together: one load wait per 256 bits
+// where Rd waits one per 32 (a header of ~1,000 bits: 4 waits instead of 30).  (8 words keep the
+// header kernel at 4 workgroups per CU.)
+struct RdWin {
+    uint32_t* win;        // &lds[lane]
+    uint64_t pos, bb, wq;
+    uint32_t bn, wi;
+    __device__ __forceinline__ void load(const In& in) {
+        u32x4 g[2];
+#pragma unroll
+        for (int k = 0; k < 2; k++) g[k] = in.ld4(wq + k);
+#pragma unroll
+        for (int k = 0; k < 2; k++) {
+            win[(4 * k) * 64] = g[k].x; win[(4 * k + 1) * 64] = g[k].y;
+            win[(4 * k + 2) * 64] = g[k].z; win[(4 * k + 3) * 64] = g[k].w;
+        }
+        wq += 2;
+        wi = 0;
+    }
+    __device__ __forceinline__ void init(const In& in, uint64_t p) {
+        pos = p;
+        wq = p >> 7;
+        load(in);
+        wi = (uint32_t)(p >> 5) & 3u;
+        bb = (uint64_t)(win[wi * 64] >> (p & 31));
+        bn = 32 - (uint32_t)(p & 31);
+        wi++;
+        fill(in);
+    }
+    __device__ __forceinline__ void fill(const In& in) {
+        if (bn <= 32) {
+            if (wi == 8) load(in);
+            bb |= (uint64_t)win[wi * 64] << bn; bn += 32; wi++;
+        }
+    }
+    __device__ __forceinline__ uint32_t peek(uint32_t n) const { return (uint32_t)bb & ((1u << n) - 1u); }
+    __device__ __forceinline__ void skip(uint32_t n) { bb >>= n; bn -= n; pos += n; }
+    __device__ __forceinline__ uint32_t get(const In& in, uint32_t n) {
+        fill(in);
+        uint32_t v = n ? peek(n) : 0u;
+        skip(n);
+        return v;
+    }
+};
+template <class R = Rd>
+__device__ __forceinline__ void parse_hdr_core(const In& in, uint64_t p, uint8_t* lens, uint16_t* cl_tab, Hdr& h,
+                                               uint32_t* win = nullptr) {
+    R rd;
+    if constexpr (std::is_same<R, RdWin>::value) rd.win = win;
     rd.init(in, p);
     h.err = 0; h.len = 0; h.numlit = 0; h.numdist = 0; h.pos = 0; h.d0 = 0;
     const uint32_t bf = rd.get(in, 1), bt = rd.get(in, 2);
@@ -1414,6 +1462,7 @@ ndfl_inflate_hdr_kernel(const uint32_t* w, uint64_t nwords, uint64_t nbits, cons
     using namespace wv;
     __shared__ __attribute__((aligned(16))) uint32_t lens[64][80];
     __shared__ uint16_t clt[64][128];
+    __shared__ uint32_t win[8 * 64];
     const uint32_t lane = threadIdx.x;
     const uint32_t k = blockIdx.x * 64 + lane;
     if (k >= ncand) return;                     // (no barrier below)
@@ -1421,7 +1470,7 @@ ndfl_inflate_hdr_kernel(const uint32_t* w, uint64_t nwords, uint64_t nbits, cons
     for (uint32_t q = 0; q < 80; q++) lens[lane][q] = 0;
     const uint64_t p = cands[k];
     Hdr h;
-    parse_hdr_core(in, p, (uint8_t*)lens[lane], clt[lane], h);
+    parse_hdr_core<RdWin>(in, p, (uint8_t*)lens[lane], clt[lane], h, win + lane);
     HdrRec* r = rec + k;
     for (uint32_t q = 0; q < 80; q += 4)
         *(uint4*)&r->lens[q] = make_uint4(lens[lane][q], lens[lane][q + 1], lens[lane][q + 2], lens[lane][q + 3]);
