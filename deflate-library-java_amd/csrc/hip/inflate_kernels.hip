@@ -1606,6 +1606,12 @@ static int inflate_devlink(InflateScratch& S, hipStream_t s, const uint32_t* d_w
         const uint64_t* t64 = (const uint64_t*)(st + 32);
         fprintf(stderr, "[ndfl] device link: chains %llu of %u candidates; count pass: slow-verify lanes %u fixups %u "
                 "rounds %u\n", (unsigned long long)hinfo[LI_NCH], ncand, st[0], st[1], st[2]);
+        const unsigned long long* ss = (const unsigned long long*)(st + 16);
+        fprintf(stderr, "[ndfl] strict stage: %llu waves, %llu loop trips (%llu refills), %llu lane-symbol steps\n",
+                ss[3], ss[0], ss[1], ss[2]);
+        fprintf(stderr, "[ndfl] count wave-time (ms x waves, 100 MHz clock; -DNDFL_PHASE_CLOCK builds): header %.1f spec %.1f "
+                "verify %.1f phases %.1f serial %.1f record %.1f build %.1f phase-mapped %.1f\n", t64[0] * 1e-5,
+                t64[1] * 1e-5, t64[2] * 1e-5, t64[3] * 1e-5, t64[4] * 1e-5, t64[5] * 1e-5, t64[6] * 1e-5, t64[7] * 1e-5);
         const double span = (double)(t64[9] - ~t64[10]);
         fprintf(stderr, "[ndfl] count waves %llu: busy %.1f ms x waves, span %.3f ms, occupancy %.3f, longest chain %.3f ms\n",
                 (unsigned long long)t64[11], t64[8] * 1e-5, span * 1e-5, t64[11] ? t64[8] / (span * t64[11]) : 0.0,

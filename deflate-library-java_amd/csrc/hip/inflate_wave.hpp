@@ -683,13 +683,33 @@ __device__ int build_code(Shared& S, uint32_t base, uint32_t n, uint32_t* prim, 
         const uint32_t ent = is_lit ? lit_entry(s, l) : dist_entry(s, l);
         const uint32_t code = f + rank[q];
         if (l <= pbits) {
-            for (uint32_t k = rev_bits(code, l); k < (1u << pbits); k += (1u << l)) prim[k] = ent;
+            if (l + 4 >= pbits)                 // (<= 16 entries; shorter codes: all lanes, below)
+                for (uint32_t k = rev_bits(code, l); k < (1u << pbits); k += (1u << l)) prim[k] = ent;
         } else if (two) {
             const uint32_t pe = prim[rev_bits(code >> (l - pbits), pbits)];
             const uint32_t sb = pe >> 16, sd = (pe >> 5) & 15, r = l - pbits;
             for (uint32_t k = rev_bits(code & ((1u << r) - 1u), r); k < (1u << sd); k += (1u << r)) x[sb + k] = ent;
         }
         if (!two) x[o + rank[q]] = ent;
+    }
+    // the codes shorter than pbits - 4 (more than 16 entries each, up to 2^(pbits-1)): one symbol at a
+    // time over all lanes, where a lane filling its own would hold the wave for its longest run
+#pragma unroll
+    for (int q = 0; q < 5; q++) {
+        if ((uint32_t)q * 64 >= n) continue;    // (uniform)
+        uint64_t sm = __ballot(mylen[q] != 0 && mylen[q] + 4 < pbits);
+        while (sm) {
+            const int src = (int)__builtin_ctzll(sm);
+            sm &= sm - 1;
+            const uint32_t l = (uint32_t)__builtin_amdgcn_readlane((int)mylen[q], src);
+            const uint32_t r = (uint32_t)__builtin_amdgcn_readlane((int)rank[q], src);
+            uint32_t f = 0;
+#pragma unroll
+            for (int L = 1; L < 16; L++) if (l == (uint32_t)L) f = fst[L];
+            const uint32_t sy = (uint32_t)q * 64 + (uint32_t)src;
+            const uint32_t ent = is_lit ? lit_entry(sy, l) : dist_entry(sy, l);
+            for (uint32_t k = rev_bits(f + r, l) + ((uint32_t)lane << l); k < (1u << pbits); k += 64u << l) prim[k] = ent;
+        }
     }
     bsync<WS>();
     return 0;
