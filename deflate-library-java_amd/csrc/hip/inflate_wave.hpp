@@ -186,7 +186,9 @@ __device__ __forceinline__ void lane_seg(const Geo& g, int lane, uint32_t& s, ui
 // Stage the round's input (all lanes call).  Words past the input end read the zero padding.
 // NDFL_STAGE_CPOL: cache policy of the staging loads (2 = non-temporal: the input is read once and
 // should not push the emit pass's partly written output lines out of L2; measured: 2 is ~1 ms
-// slower and leaves the emit write traffic unchanged, 20.0 vs 21.5 GB).
+// slower and leaves the emit write traffic unchanged, 20.0 vs 21.5 GB).  Touching the next round's
+// input into L2 after each staging (one LDS-DMA dword per 128-byte line, round 5) made count and
+// emit slower too (+0.3 / +0.4 ms, profiles/r05_ab_stage_touch.txt).
 #ifndef NDFL_STAGE_CPOL
 #define NDFL_STAGE_CPOL 0
 #endif
