@@ -599,8 +599,7 @@ ndfl_inflate_strict_kernel(const uint32_t* w, uint64_t nwords, uint64_t nbits, c
     uint64_t p = 0;
     SRd rd;
     rd.bb = 0; rd.pos = 0; rd.qw = 0; rd.bn = 0; rd.fi = 8;
-    uint32_t i = 0, total = 0, numLit = 0, numDist = 0, litK = 0, distK = 0, ones = 0, other = 0, eob = 0, d0 = 0,
-             d31 = 0;
+    uint32_t i = 0, total = 0, numLit = 0, numDist = 0, litK = 0, distK = 0, nz = 0, eob = 0;
     int runVal = -1;
     uint64_t n_iter = 0, n_refill = 0, n_steps = 0;      // NDFL_STATS (sst != nullptr)
     for (;;) {
@@ -673,7 +672,7 @@ ndfl_inflate_strict_kernel(const uint32_t* w, uint64_t nwords, uint64_t nbits, c
                                 }
                             }
                         }
-                        i = 0; runVal = -1; litK = 0; distK = 0; ones = 0; other = 0; eob = 0; d0 = 0; d31 = 0;
+                        i = 0; runVal = -1; litK = 0; distK = 0; nz = 0; eob = 0;
                         active = complete;
                     }
                 }
@@ -715,19 +714,22 @@ ndfl_inflate_strict_kernel(const uint32_t* w, uint64_t nwords, uint64_t nbits, c
             litK += (min(en, numLit) - min(i, numLit)) * wt;
             const uint32_t da = max(i, numLit) - numLit, db = max(en, numLit) - numLit, cd = db - da;
             distK += cd * wt;
-            ones += v == 1 ? cd : 0u;
-            other += v > 1 ? cd : 0u;
+            nz += v ? cd : 0u;                  // distance codes of nonzero length
             eob = (i <= 256 && 256 < en) ? v : eob;
-            d0 = (cd && da == 0) ? v : d0;
-            d31 = (da <= 31 && 31 < db) ? v : d31;
             i = en;
-            const bool go = !(bad || en > total || rd.pos > in.nbits) && litK <= 32768u && distK <= 32768u;
+            // (past the input end the window reads zeros, which only end the loop: the end test
+            // below rejects such a header, as the reference's first read past the end would)
+            const bool go = !(bad || en > total) && litK <= 32768u && distK <= 32768u;
             active = go && i < total;
             if (go && i >= total) {
+                // the reference's end checks (as strict_dynamic): numDist <= 30 here (stage 1 drops
+                // HDIST >= 30), so the single distance code's dummy-31 case cannot arise; one
+                // distance code of length 1 is distK == 1/2 with one nonzero length; numDist == 1
+                // with a zero length is distK == 0
                 bool ok;
-                if (eob == 0 || litK != 32768u) ok = false;
-                else if (numDist == 1 && d0 == 0) ok = true;
-                else if (ones == 1 && other == 0) ok = !(numDist == 32 && d31 == 1);
+                if (eob == 0 || litK != 32768u || rd.pos > in.nbits) ok = false;
+                else if (numDist == 1 && distK == 0) ok = true;
+                else if (nz == 1 && distK == 16384u) ok = true;
                 else ok = distK == 32768u;
                 if (ok) record(p);
             }
