@@ -1596,7 +1596,7 @@ static int inflate_devlink(InflateScratch& S, hipStream_t s, const uint32_t* d_w
     // the resolve rounds, as far as they usually go, without a host read in between
     uint32_t* left = nullptr;
     if (!deferred) {
-        rc = resolve_rounds_dev(S, s, d_out, nbytes, 6, &left, (uint64_t*)nullptr);
+        rc = resolve_rounds_dev(S, s, d_out, nbytes, 6, &left, stats_on ? info + LI_WORDS - 3 : (uint64_t*)nullptr);
         if (rc) return rc;
         if (left) INF_CHK(hipMemcpyAsync(info + LI_WORDS - 1, left, 4, hipMemcpyDeviceToDevice, s));
     }
@@ -1611,6 +1611,8 @@ static int inflate_devlink(InflateScratch& S, hipStream_t s, const uint32_t* d_w
         const unsigned long long* ss = (const unsigned long long*)(st + 16);
         fprintf(stderr, "[ndfl] strict stage: %llu waves, %llu loop trips (%llu refills), %llu lane-symbol steps\n",
                 ss[3], ss[0], ss[1], ss[2]);
+        fprintf(stderr, "[ndfl] emit: %u pending 32-byte groups before the resolve rounds, %u after six\n",
+                (uint32_t)(hinfo[LI_WORDS - 3] & 0xFFFFFFFFu), (uint32_t)(hinfo[LI_WORDS - 1] & 0xFFFFFFFFu));
         fprintf(stderr, "[ndfl] count wave-time (ms x waves, 100 MHz clock; -DNDFL_PHASE_CLOCK builds): header %.1f spec %.1f "
                 "verify %.1f phases %.1f serial %.1f record %.1f build %.1f phase-mapped %.1f\n", t64[0] * 1e-5,
                 t64[1] * 1e-5, t64[2] * 1e-5, t64[3] * 1e-5, t64[4] * 1e-5, t64[5] * 1e-5, t64[6] * 1e-5, t64[7] * 1e-5);
