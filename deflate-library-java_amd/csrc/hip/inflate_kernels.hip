@@ -1489,6 +1489,36 @@ static int inflate_devlink(InflateScratch& S, hipStream_t s, const uint32_t* d_w
         for (int k = 0; k < 3; k++)
             fprintf(stderr, "[ndfl] count chains %s: %llu, wave time %.2f ms (max %.3f ms), blocks %llu\n", nm[k],
                     (unsigned long long)cnt[k], tsum[k] * 1e-2, tmax[k] * 1e-2, (unsigned long long)blk[k]);
+        // wave time against the chain's bits (the count order's key): per 32-Kibit bucket, and the
+        // longest chains
+        std::vector<uint64_t> cb(ncand);
+        INF_CHK(hipMemcpy(cb.data(), S.d_cands, ncand * 8, hipMemcpyDeviceToHost));
+        uint64_t bn[OB_NB] = {}, bt[OB_NB] = {}, bm[OB_NB] = {};
+        uint32_t bk[OB_NB] = {};
+        std::vector<uint32_t> top;
+        for (uint32_t k = 0; k < ncand; k++) {
+            const uint64_t nx = k + 1 < ncand ? cb[k + 1] : end_bit, len = nx > cb[k] ? nx - cb[k] : 0;
+            const uint32_t b = (uint32_t)std::min<uint64_t>(OB_NB - 1, len >> 15), t = cr[k].pad >> 16;
+            bn[b]++; bt[b] += t;
+            if (t >= bm[b]) { bm[b] = t; bk[b] = k; }
+            top.push_back(k);
+        }
+        for (uint32_t b = 0; b < OB_NB; b++)
+            if (bn[b]) fprintf(stderr, "[ndfl] count bits %2u x 32Ki: %6llu chains, mean %.3f ms, max %.3f ms "
+                               "(chain %u at bit %llu: blocks %u, status %u, out %llu)\n", b,
+                               (unsigned long long)bn[b], bt[b] * 1e-2 / bn[b], bm[b] * 1e-2, bk[b],
+                               (unsigned long long)cb[bk[b]], cr[bk[b]].pad & 0xFFFFu, cr[bk[b]].status,
+                               (unsigned long long)cr[bk[b]].out_count);
+        const size_t nt = std::min<size_t>(8, top.size());
+        std::partial_sort(top.begin(), top.begin() + nt, top.end(),
+                          [&](uint32_t a, uint32_t b) { return (cr[a].pad >> 16) > (cr[b].pad >> 16); });
+        for (size_t i = 0; i < nt; i++) {
+            const uint32_t k = top[i];
+            const uint64_t nx = k + 1 < ncand ? cb[k + 1] : end_bit;
+            fprintf(stderr, "[ndfl] count longest: chain %u at bit %llu, %llu bits, %.3f ms, blocks %u, status %u, out %llu\n",
+                    k, (unsigned long long)cb[k], (unsigned long long)(nx - cb[k]), (cr[k].pad >> 16) * 1e-2,
+                    cr[k].pad & 0xFFFFu, cr[k].status, (unsigned long long)cr[k].out_count);
+        }
     }
     // linking: J levels (u32), S and D double-buffered
     uint32_t nlev = 1;

@@ -784,7 +784,10 @@ __device__ int build_tables(Shared& S, int lane, bool& empty_dist) {
 
 // ---- segmented speculative decode of one round ------------------------------------------------
 // Lane j owns [s_j, e_j) (round-relative bits) and checkpoints C1_j = s_j + min(XCP1, len) and
-// C2_j = s_j + min(XCP2, len) (64 and 1024 bits; round 4: XCP1 128 -> 64, count 11.1 -> 10.8 ms).  A speculative run from a start records, per checkpoint, its first
+// C2_j = s_j + min(XCP2, len) (64 and 192 bits; round 4: XCP1 128 -> 64, count 11.1 -> 10.8 ms), and
+// the segment end is a third: a verify that decoded to the end is synchronised when it ends where
+// its speculation ended.  A wave's verify lasts as long as its slowest lane, and one lane missing C1
+// used to decode its whole segment.  A speculative run from a start records, per checkpoint, its first
 // token boundary at or past it (offset from s_j) and the output bytes before it, plus its end
 // state.  Two decodes that stand on the same boundary at a checkpoint agree from there on, so a
 // verify run from the TRUE start only decodes up to the first checkpoint where it meets its own
@@ -795,17 +798,23 @@ __device__ int build_tables(Shared& S, int lane, bool& empty_dist) {
 #define NDFL_XCP1 64
 #endif
 // The fallback phases 1..7 are decoded only when more than this many lanes of a round failed to
-// synchronise (a sign of phase-locked codes); fewer, isolated failures are resolved by the fix-up
-// sweeps alone.  NDFL_FIX_SERIAL=1 restores the in-order fix-up loop (A/B).
+// synchronise (a sign of phase-locked codes), or when the frontier lane of NDFL_PH_FRONTIER fix-up
+// sweeps re-ran from its exact start and still missed its speculation; fewer, isolated failures are
+// resolved by the fix-up sweeps alone (round 5: frontier trigger 1 -> 4, count 10.8 -> 10.2 ms: the
+// 4-byte-periodic binary tables miss ~20 % of their lanes, which two or three sweeps fix for less
+// than 7 phase runs cost).  NDFL_FIX_SERIAL=1 restores the in-order fix-up loop (A/B).
 #ifndef NDFL_PH_FALLBACK
 #define NDFL_PH_FALLBACK 8
+#endif
+#ifndef NDFL_PH_FRONTIER
+#define NDFL_PH_FRONTIER 4      // frontier misses (one per sweep) before the phase runs are decoded
 #endif
 #ifndef NDFL_FIX_SERIAL
 #define NDFL_FIX_SERIAL 0
 #endif
 #ifndef NDFL_XCP2
-#define NDFL_XCP2 1024
-#endif
+#define NDFL_XCP2 192           // (round 5: 1024, i.e. the segment end -> 192 with the end compared as a
+#endif                          // third checkpoint: count 10.3 -> 9.9 ms, profiles/r05_ab_count_sync.txt)
 constexpr uint32_t XCP1 = NDFL_XCP1, XCP2 = NDFL_XCP2;
 constexpr uint32_t NPH = 8;
 constexpr uint32_t NOCP = 0xFFFFFFFFu;
@@ -895,8 +904,10 @@ __device__ __forceinline__ bool verify_run(const Lv& v0, const Tabs& t, bool ed,
             }
             continue;
         }
+        // decoded to the segment end: exact either way; synchronised when it ends where the
+        // speculation ended (the next lane's verify started there)
         r.end = pos; r.cnt = c; r.kind = T_EXIT; r.reason = 0;
-        return false;
+        return pos == p0.end && p0.kind == T_EXIT;
     }
 }
 
@@ -998,6 +1009,7 @@ __device__ void round_decode(const In& in, const Tabs& t, bool ed, uint64_t rs, 
         // when it is the first inconsistent lane or its predecessor's exit held still last sweep.
         first_term = 64u;
         uint64_t chgm = 0;                      // lanes whose exit moved in the last sweep
+        uint32_t fmiss = 0;                     // sweeps whose frontier lane missed its speculation
         for (;;) {
             __syncthreads();
             const uint32_t st = lane ? (uint32_t)S.exit_[lane - 1] : r.start;
@@ -1016,7 +1028,7 @@ __device__ void round_decode(const In& in, const Tabs& t, bool ed, uint64_t rs, 
             // the frontier lane re-ran from an exact start and still missed its own speculation: a
             // phase-locked stretch (e.g. fixed-Huffman text), where every later lane would miss too
             // -- decode the phase runs now, once, so that the next re-runs meet one of them
-            if (nph == 1 && __any((uint32_t)lane == fc && !met)) { phase_runs(fc); nph = NPH; }
+            if (nph == 1 && __any((uint32_t)lane == fc && !met) && ++fmiss >= NDFL_PH_FRONTIER) { phase_runs(fc); nph = NPH; }
             chgm = __ballot(redo && r.end != old_end);
             __syncthreads();                    // every lane has read its predecessor's exit
             if (redo) S.exit_[lane] = r.end;
