@@ -1050,9 +1050,15 @@ __device__ void round_decode(const In& in, const Tabs& t, bool ed, uint64_t rs, 
 #define NDFL_PHASE_SWITCH 48   // lanes of a round that failed to synchronise before the block's next
 #endif                         // rounds are phase-mapped (measured: 4-16 much slower; 32 -> 48: config 2
                                // count 16.9 -> 9.5 ms, fixed-Huffman text resyncs through the 8-phase verify)
+#ifndef NDFL_PHASE_JUMP
+#define NDFL_PHASE_JUMP 1      // phase runs step four 8-bit literals at once where they can
+#endif
 #ifndef NDFL_PHASE_GROUP
-#define NDFL_PHASE_GROUP 8     // phase runs decoded together (1, 2, 4 or 8; measured 1: 14.6, 2: 13.9,
-#endif                         // 4: 12.9, 8: 12.8 ms count pass)
+#define NDFL_PHASE_GROUP 2     // phase runs decoded together (1, 2, 4 or 8; round 3, one token a step:
+#endif                         // 1: 14.6, 2: 13.9, 4: 12.9, 8: 12.8 ms count pass; round 5, four 8-bit
+                               // literals a step: 8 / 4 / 2: 10.35 / 9.57 / 9.46 against 10.0 ms without
+                               // the four-literal step, random-data count pass 7.5 -> 6.5 ms per GiB,
+                               // profiles/r05_ab_phase_jump.txt)
 
 // count run from st to the first token boundary at or past e (or the block end); the first step is
 // a single token whose end and bytes are returned in fb / fbc (fb = NOCP: none)
@@ -1103,6 +1109,44 @@ __device__ __forceinline__ void phase_multi(const Lv& v, const Tabs& t, bool ed,
 #pragma unroll
         for (int k = 0; k < N; k++) { f[k] = l[k] && p[k] + 48 < e; any = any || f[k]; }
         if (!any) break;
+#if NDFL_PHASE_JUMP
+        // a run's next four tokens are looked up at once, at p, p+8, p+16, p+24 (independent reads):
+        // when all four are literal entries of 8 bits (one 8-bit code, or a pair of 8 bits), the run
+        // moves 32 bits in one step -- phase-locked codes are mostly 8-bit literals (random data:
+        // ~94 % of its tokens, so ~3/4 of its steps take four)
+        uint32_t lo[N], hi[N], en[N], ex[N];
+#pragma unroll
+        for (int k = 0; k < N; k++) {
+            const uint32_t pp = f[k] ? p[k] : p[0];
+            const uint32_t* qk = v.p + ((pp >> 5) - v.rw) * 64;
+            const uint32_t a = qk[0], wb = qk[64], cw = qk[128];
+            lo[k] = __builtin_amdgcn_alignbit(wb, a, pp & 31);
+            hi[k] = __builtin_amdgcn_alignbit(cw, wb, pp & 31);
+        }
+#pragma unroll
+        for (int k = 0; k < N; k++) {
+            en[k] = t.lit[lo[k] & ((1u << LB) - 1u)];
+            const uint32_t e1 = t.lit[(lo[k] >> 8) & ((1u << LB) - 1u)];
+            const uint32_t e2 = t.lit[(lo[k] >> 16) & ((1u << LB) - 1u)];
+            const uint32_t e3 = t.lit[__builtin_amdgcn_alignbit(hi[k], lo[k], 24) & ((1u << LB) - 1u)];
+            // bit 31 | advance 8 in every entry: (x & 0x8000000F) == 0x80000008; pairs add a token each
+            const bool all8 = ((en[k] & 0x8000000Fu) == 0x80000008u) && ((e1 & 0x8000000Fu) == 0x80000008u) &&
+                              ((e2 & 0x8000000Fu) == 0x80000008u) && ((e3 & 0x8000000Fu) == 0x80000008u);
+            ex[k] = all8 ? 4u + ((en[k] >> 8) & 1u) + ((e1 >> 8) & 1u) + ((e2 >> 8) & 1u) + ((e3 >> 8) & 1u) : 0u;
+        }
+#pragma unroll
+        for (int k = 0; k < N; k++) {
+            if (f[k] && ex[k]) { p[k] += 32; c[k] += ex[k]; continue; }
+            const bool q = f[k] && (en[k] >> 31);
+            if (q) { p[k] += en[k] & 15; c[k] += 1u + ((en[k] >> 8) & 1u); }
+            if (f[k] && !q) {
+                Tok tk;
+                tok_e<false>(lo[k], hi[k], en[k], p[k], t, ed, e, nb, tk);
+                if (tk.kind > K_LEN) { l[k] = false; O[k].kr = tk.kind == K_EOB ? (T_EOB << 5) : ((T_ERR << 5) | tk.val); }
+                else c[k] += tk.n;
+            }
+        }
+#else
         // each run's window is its low word pair only; the third word (for a length/distance token's
         // distance bits) is read in the rare non-literal branch -- phase-locked codes are literals
         uint32_t lo[N], wb[N], en[N];
@@ -1129,6 +1173,7 @@ __device__ __forceinline__ void phase_multi(const Lv& v, const Tabs& t, bool ed,
                 else c[k] += tk.n;
             }
         }
+#endif
     }
 #pragma unroll
     for (int k = 0; k < N; k++) {
