@@ -1647,6 +1647,16 @@ ndfl_inflate_count_wave_kernel(const uint32_t* w, uint64_t nwords, uint64_t nbit
         if (pc) { const uint64_t x = wall_clock64(); pc->hdr += x - tb; tb = x; }
         const int te = build_tables(S, lane, ed);
         if (te) { status = ST_ERROR; reason = (uint32_t)te; endpos = d0; break; }
+        // literal/length codes mostly of one length 8 resynchronise rarely: phase-mapped rounds
+        bool phased = false;
+        {
+            uint32_t n8 = 0;
+            for (uint32_t q = 0; q < 5; q++) {
+                const uint32_t sy = q * 64 + (uint32_t)lane;
+                n8 += (uint32_t)__popcll(__ballot(sy < 288 && S.lens[sy] == 8));
+            }
+            phased = n8 >= 192;
+        }
         // the block's tables and header fields for the emit pass (a table record)
         uint32_t brec = NOREC;
         if (recording && pool.nbt) {
@@ -1665,7 +1675,7 @@ ndfl_inflate_count_wave_kernel(const uint32_t* w, uint64_t nwords, uint64_t nbit
                     uint64_t* h = (uint64_t*)(pool.bt + (uint64_t)brec * BT_BYTES + sizeof(Tabs));
                     h[0] = cur; h[1] = d0;
                     uint32_t* h32 = (uint32_t*)(h + 2);
-                    h32[0] = S.h_bfinal; h32[1] = S.h_btype; h32[2] = ed ? 1u : 0u; h32[3] = 0;
+                    h32[0] = S.h_bfinal; h32[1] = S.h_btype; h32[2] = ed ? 1u : 0u; h32[3] = phased ? 1u : 0u;
                 }
             } else {
                 brec = NOREC;
@@ -1674,16 +1684,6 @@ ndfl_inflate_count_wave_kernel(const uint32_t* w, uint64_t nwords, uint64_t nbit
         if (pc) { const uint64_t x = wall_clock64(); pc->build += x - tb; tb = x; }
         uint64_t rs = d0;
         bool block_done = false, chain_done = false;
-        // literal/length codes mostly of one length 8 resynchronise rarely: phase-mapped rounds
-        bool phased = false;
-        {
-            uint32_t n8 = 0;
-            for (uint32_t q = 0; q < 5; q++) {
-                const uint32_t sy = q * 64 + (uint32_t)lane;
-                n8 += (uint32_t)__popcll(__ballot(sy < 288 && S.lens[sy] == 8));
-            }
-            phased = n8 >= 192;
-        }
         while (!block_done) {
             uint64_t E = min(cc.after(rs, limit), rs + MAX_SPAN);
             if (E <= rs) E = rs + 1;
@@ -2054,6 +2054,9 @@ ndfl_inflate_emit_wave_kernel(const uint32_t* w, uint64_t nwords, uint64_t nbits
 #ifndef NDFL_EMITF_GX
 #define NDFL_EMITF_GX 1         // primary tables in LDS, extension areas read from the table record
 #endif
+#ifndef NDFL_EMIT_JUMP
+#define NDFL_EMIT_JUMP 1        // blocks of mostly 8-bit literal codes: four literals a step where they can
+#endif
 #ifndef NDFL_EMITF_WAVES_PER_SIMD
 #define NDFL_EMITF_WAVES_PER_SIMD 4
 #endif
@@ -2136,6 +2139,7 @@ ndfl_inflate_emit_fast_kernel(const uint32_t* w, uint64_t nwords, uint64_t nbits
         const uint64_t* h = (const uint64_t*)(btr + sizeof(Tabs));
         const uint32_t* h32 = (const uint32_t*)(h + 2);
         const bool bfinal = h32[0] != 0, ed = h32[2] != 0;
+        const bool ph8 = NDFL_EMIT_JUMP && h32[3] != 0;     // mostly 8-bit literal codes
         __syncthreads();
         bool block_done = false, chain_done = false;
         while (!block_done) {
@@ -2178,62 +2182,91 @@ ndfl_inflate_emit_fast_kernel(const uint32_t* w, uint64_t nwords, uint64_t nbits
             const uint32_t lim = min(end, nb - min(nb, 48u));
             bool fast = live && pos < lim;
             if (fast) bb_init(bb, v, pos);
-            while (live && pos < end) {
-                Tok tk;
-                if (fast) {
-                    tok_bb<true>(bb, v, T, ed, tk, end);
-                    pos = bb.pos;
-                    fast = pos < lim;
-                } else {
-                    tok<true>(v, pos, T, ed, end, nb, tk);
-                }
-                if (tk.kind == K_LIT) {
-                    wr_lit(wr, gout, tk.val, tk.n);
-                    n += tk.n;
-                    lsp = true;
-                    lastb = tk.val >> (tk.n == 2 ? 8 : 0);
-                    lastok = true;
-                    continue;
-                }
-                if (tk.kind != K_LEN) break;
-                const uint64_t dst = dst0 + n;
-                if ((uint64_t)tk.dist > dst) { kind = T_ERR; rsn = R_COPY_BEFORE; end = pos; break; }
-                const uint32_t len = tk.n, dist = tk.dist;
-                const uint64_t src = dst - dist;
-                const uint64_t src_end = src + min(len, dist);
-                bool defer = src < dst0;
-                if (!defer && src_end > dfr) {
-                    for (uint64_t q = src >> 5; q <= (src_end - 1) >> 5 && !defer; q++) {
-                        const uint64_t lo = max(src, q << 5), hi = min(src_end, (q + 1) << 5);
-                        const uint32_t mk = (uint32_t)(((1ull << (hi - lo)) - 1) << (lo & 31));
-                        defer = (__hip_atomic_load(&pend[q], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) & mk) != 0;
+            // (two instances of the token loop: blocks of mostly 8-bit literal codes try four literals a
+            // step, the others keep the plain loop's code and registers)
+            auto token_loop = [&](auto ph) {
+                using PH = decltype(ph);
+                while (live && pos < end) {
+                    Tok tk;
+                    if (PH::value && fast && bb.nb >= 34 && pos + 24 < end) {
+                        // four 8-bit literal codes at once (independent table reads at 0, 8, 16, 24 bits;
+                        // the lane's end is a token boundary, so none of the four passes it)
+                        const uint32_t lo = (uint32_t)bb.buf, hi = (uint32_t)(bb.buf >> 32);
+                        const uint32_t e0 = T.lit[lo & ((1u << LB) - 1u)], e1 = T.lit[(lo >> 8) & ((1u << LB) - 1u)];
+                        const uint32_t e2 = T.lit[(lo >> 16) & ((1u << LB) - 1u)];
+                        const uint32_t e3 = T.lit[__builtin_amdgcn_alignbit(hi, lo, 24) & ((1u << LB) - 1u)];
+                        // a single literal of 8 bits: bit 31, advance 8, first length 8, no pair
+                        if (((e0 & 0x800001FFu) == 0x80000088u) && ((e1 & 0x800001FFu) == 0x80000088u) &&
+                            ((e2 & 0x800001FFu) == 0x80000088u) && ((e3 & 0x800001FFu) == 0x80000088u)) {
+                            const uint32_t b3 = (e3 >> 9) & 0xFFu;
+                            wr_lit(wr, gout, ((e0 >> 9) & 0xFFu) | (((e1 >> 9) & 0xFFu) << 8) | (((e2 >> 9) & 0xFFu) << 16) | (b3 << 24), 4);
+                            n += 4;
+                            lsp = true;
+                            lastb = b3;
+                            lastok = true;
+                            bb_skip(bb, 32);
+                            bb_refill(bb, v);
+                            pos = bb.pos;
+                            fast = pos < lim;
+                            continue;
+                        }
                     }
-                }
-                wr_flush_word(wr, gout);
-                if (!defer && dist == 1 && !lastok) lastb = gout[dst - 1];
-                if (!defer) {
-                    wr_copy(gout, dst, len, dist, lastb);
-                    lastok = true;
-                    lsp = true;
-                } else {
-                    const uint64_t anchor = dist == 1 ? (n > 0 ? (lsp ? dst - 1 : lastsrc) : src) : 0;
-                    for (uint32_t k = 0; k < len; k++) {
-                        const uint64_t back = dst + k - anchor;
-                        ref[dst + k] = dist == 1 ? (back < (1ull << 32) ? (uint32_t)back : 1u) : dist;
+                    if (fast) {
+                        tok_bb<true>(bb, v, T, ed, tk, end);
+                        pos = bb.pos;
+                        fast = pos < lim;
+                    } else {
+                        tok<true>(v, pos, T, ed, end, nb, tk);
                     }
-                    for (uint64_t q = dst >> 5; q <= (dst + len - 1) >> 5; q++) {
-                        const uint64_t lo = max(dst, q << 5), hi = min(dst + len, (q + 1) << 5);
-                        const uint32_t mk = (uint32_t)(((1ull << (hi - lo)) - 1) << (lo & 31));
-                        atomicOr(&pend[q], mk);
+                    if (tk.kind == K_LIT) {
+                        wr_lit(wr, gout, tk.val, tk.n);
+                        n += tk.n;
+                        lsp = true;
+                        lastb = tk.val >> (tk.n == 2 ? 8 : 0);
+                        lastok = true;
+                        continue;
                     }
-                    lastsrc = anchor;
-                    lsp = dist != 1;
-                    dfr = min(dfr, dst);
-                    lastok = false;
+                    if (tk.kind != K_LEN) break;
+                    const uint64_t dst = dst0 + n;
+                    if ((uint64_t)tk.dist > dst) { kind = T_ERR; rsn = R_COPY_BEFORE; end = pos; break; }
+                    const uint32_t len = tk.n, dist = tk.dist;
+                    const uint64_t src = dst - dist;
+                    const uint64_t src_end = src + min(len, dist);
+                    bool defer = src < dst0;
+                    if (!defer && src_end > dfr) {
+                        for (uint64_t q = src >> 5; q <= (src_end - 1) >> 5 && !defer; q++) {
+                            const uint64_t lo = max(src, q << 5), hi = min(src_end, (q + 1) << 5);
+                            const uint32_t mk = (uint32_t)(((1ull << (hi - lo)) - 1) << (lo & 31));
+                            defer = (__hip_atomic_load(&pend[q], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) & mk) != 0;
+                        }
+                    }
+                    wr_flush_word(wr, gout);
+                    if (!defer && dist == 1 && !lastok) lastb = gout[dst - 1];
+                    if (!defer) {
+                        wr_copy(gout, dst, len, dist, lastb);
+                        lastok = true;
+                        lsp = true;
+                    } else {
+                        const uint64_t anchor = dist == 1 ? (n > 0 ? (lsp ? dst - 1 : lastsrc) : src) : 0;
+                        for (uint32_t k = 0; k < len; k++) {
+                            const uint64_t back = dst + k - anchor;
+                            ref[dst + k] = dist == 1 ? (back < (1ull << 32) ? (uint32_t)back : 1u) : dist;
+                        }
+                        for (uint64_t q = dst >> 5; q <= (dst + len - 1) >> 5; q++) {
+                            const uint64_t lo = max(dst, q << 5), hi = min(dst + len, (q + 1) << 5);
+                            const uint32_t mk = (uint32_t)(((1ull << (hi - lo)) - 1) << (lo & 31));
+                            atomicOr(&pend[q], mk);
+                        }
+                        lastsrc = anchor;
+                        lsp = dist != 1;
+                        dfr = min(dfr, dst);
+                        lastok = false;
+                    }
+                    n += len;
+                    wr.dst = dst0 + n;
                 }
-                n += len;
-                wr.dst = dst0 + n;
-            }
+            };
+            if (ph8) token_loop(std::true_type{}); else token_loop(std::false_type{});
             wr_flush_exact(wr, gout);
             const uint64_t em = __ballot(live && kind == T_ERR);
             if (em) {

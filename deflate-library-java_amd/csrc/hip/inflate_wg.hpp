@@ -402,6 +402,15 @@ ndfl_inflate_count_wg_kernel(const uint32_t* w, uint64_t nwords, uint64_t nbits,
         const int te = (int)X.b32[1];
         const bool ed = X.b32[2] != 0;
         if (te) { status = ST_ERROR; reason = (uint32_t)te; endpos = d0; break; }
+        bool phased;
+        {
+            uint32_t n8 = 0;                        // (every wave counts the same lengths)
+            for (uint32_t q = 0; q < 5; q++) {
+                const uint32_t sy = q * 64 + (uint32_t)lane;
+                n8 += (uint32_t)__popcll(__ballot(sy < 288 && S.lens[sy] == 8));
+            }
+            phased = n8 >= 192;
+        }
         uint32_t brec = NOREC;
         if (recording && pool.nbt) {
             if (tid == 0) {
@@ -421,7 +430,7 @@ ndfl_inflate_count_wg_kernel(const uint32_t* w, uint64_t nwords, uint64_t nbits,
                     uint64_t* h = (uint64_t*)(pool.bt + (uint64_t)brec * BT_BYTES + sizeof(Tabs));
                     h[0] = cur; h[1] = d0;
                     uint32_t* h32 = (uint32_t*)(h + 2);
-                    h32[0] = S.h_bfinal; h32[1] = S.h_btype; h32[2] = ed ? 1u : 0u; h32[3] = 0;
+                    h32[0] = S.h_bfinal; h32[1] = S.h_btype; h32[2] = ed ? 1u : 0u; h32[3] = phased ? 1u : 0u;
                 }
             } else {
                 brec = NOREC;
@@ -429,15 +438,6 @@ ndfl_inflate_count_wg_kernel(const uint32_t* w, uint64_t nwords, uint64_t nbits,
         }
         uint64_t rs = d0;
         bool block_done = false, chain_done = false;
-        bool phased;
-        {
-            uint32_t n8 = 0;                        // (every wave counts the same lengths)
-            for (uint32_t q = 0; q < 5; q++) {
-                const uint32_t sy = q * 64 + (uint32_t)lane;
-                n8 += (uint32_t)__popcll(__ballot(sy < 288 && S.lens[sy] == 8));
-            }
-            phased = n8 >= 192;
-        }
         while (!block_done) {
             uint64_t E = min(cc.after(rs, limit), rs + SPAN_W);
             if (E <= rs) E = rs + 1;
