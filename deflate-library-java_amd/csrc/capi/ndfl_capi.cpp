@@ -76,6 +76,7 @@ struct ndfl_ctx {
     InflateScratch inf;
     uint32_t* h_pinned = nullptr;   // small pinned area for results
     Knobs knobs;                    // switches read once at ndfl_ctx_create (ndfl_common.hpp)
+    int err_sym = -1;               // the last decode's reserved symbol (ndfl_ctx_error_symbol), or -1
 };
 
 #define HIPCHK(x) do { hipError_t _e = (x); if (_e != hipSuccess) return NDFL_E_DEVICE; } while (0)
@@ -144,6 +145,7 @@ int ndfl_ctx_create(ndfl_ctx** out, int device, uint32_t flags) {
     c->device = device;
     c->knobs.read();
     c->inf.knobs = c->knobs;
+    if (c->knobs.stats) c->knobs.print(stderr);
     if (hipStreamCreateWithFlags(&c->own, hipStreamDefault) != hipSuccess) { delete c; return NDFL_E_DEVICE; }
     c->stream = c->own;
     hipEventCreate(&c->ev0);
@@ -982,12 +984,31 @@ int ndfl_adler32(ndfl_ctx* c, uint32_t* adler_inout, const uint8_t* data, uint64
     return NDFL_OK;
 }
 
+// A decode's Reason as it leaves the library: the decoder reports the second reserved symbol of each
+// alphabet (length 287, distance 31) with an internal code; both become the reference's Reason, and
+// the symbol -- which the reference puts in its message, "Reserved run length symbol: " + sym
+// (D/decomp/Open.java:516, 659) and "Reserved distance symbol: " + sym (:550, 674) -- is kept for
+// ndfl_ctx_error_symbol.
+static int public_reason(ndfl_ctx* c, int r) {
+    c->err_sym = -1;
+    switch (r) {
+        case inf::R_RESERVED_LEN: c->err_sym = 286; break;
+        case inf::R_RESERVED_LEN_HI: c->err_sym = 287; r = inf::R_RESERVED_LEN; break;
+        case inf::R_RESERVED_DIST: c->err_sym = 30; break;
+        case inf::R_RESERVED_DIST_HI: c->err_sym = 31; r = inf::R_RESERVED_DIST; break;
+        default: break;
+    }
+    return r;
+}
+
+int ndfl_ctx_error_symbol(ndfl_ctx* c) { return c ? c->err_sym : -1; }
+
 int ndfl_inflate(ndfl_ctx* c, const uint8_t* in, uint64_t in_len, uint8_t* out, uint64_t out_cap,
                  uint64_t* out_len, uint64_t* consumed_bits, uint32_t flags) {
     if (!c || !out_len || !consumed_bits || (!in && in_len)) return NDFL_E_ARG;
     HIPCHK(hipSetDevice(c->device));
-    return inflate_run(c->inf, ordered_stream(c), in, in_len, 0, inf::NONE, out, 0, out_cap, out_len, consumed_bits,
-                       flags, false, &c->last_ms);
+    return public_reason(c, inflate_run(c->inf, ordered_stream(c), in, in_len, 0, inf::NONE, out, 0, out_cap, out_len,
+                                        consumed_bits, flags, false, &c->last_ms));
 }
 
 int ndfl_inflate_range(ndfl_ctx* c, const uint8_t* in, uint64_t in_len, uint64_t start_bit, uint64_t end_bit,
@@ -1000,8 +1021,8 @@ int ndfl_inflate_range(ndfl_ctx* c, const uint8_t* in, uint64_t in_len, uint64_t
     if (deferred && !(flags & NDFL_OUT_DEVICE)) return NDFL_E_ARG;
     if (partial && (deferred || end_bit != UINT64_MAX)) return NDFL_E_ARG;
     HIPCHK(hipSetDevice(c->device));
-    return inflate_run(c->inf, ordered_stream(c), in, in_len, start_bit, end_bit, out, dict_len, out_cap, out_len,
-                       consumed_bits, flags, deferred, &c->last_ms, partial);
+    return public_reason(c, inflate_run(c->inf, ordered_stream(c), in, in_len, start_bit, end_bit, out, dict_len,
+                                        out_cap, out_len, consumed_bits, flags, deferred, &c->last_ms, partial));
 }
 
 int ndfl_inflate_sync(ndfl_ctx* c, const uint8_t* in, uint64_t in_len, uint64_t from_bit, uint64_t window_bits,

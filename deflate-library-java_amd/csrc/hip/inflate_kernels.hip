@@ -45,6 +45,10 @@ enum : uint32_t { ST_BOUNDARY = 0, ST_FINAL = 1, ST_ERROR = 2 };
 constexpr int NEED_INPUT = 64;             // NDFL_NEED_INPUT (include/ndfl.h): partial-input decode stopped
 enum : int { R_UEOS = 1, R_RESERVED_BLOCK_TYPE, R_LEN_MISMATCH, R_UNDER_FULL, R_OVER_FULL, R_NO_PREV,
              R_CL_OVER_FULL, R_EOB_ZERO, R_RESERVED_LEN, R_RESERVED_DIST, R_EMPTY_DIST, R_COPY_BEFORE,
+             // internal: the second reserved symbol of each alphabet (287, distance 31); the C ABI
+             // returns R_RESERVED_LEN / R_RESERVED_DIST and keeps the symbol (ndfl_ctx_error_symbol),
+             // which the reference puts in its message (D/decomp/Open.java:516, 550)
+             R_RESERVED_LEN_HI = 20, R_RESERVED_DIST_HI = 21,
              R_INTERNAL = 100 };
 
 constexpr int CLO[19] = {16, 17, 18, 0, 8, 7, 9, 6, 10, 5, 11, 4, 12, 3, 13, 2, 14, 1, 15};
@@ -1162,6 +1166,7 @@ struct InflateScratch {
     void* d_out = nullptr; size_t d_out_cap = 0;
     Knobs knobs;                                       // the context's switches (ndfl_common.hpp)
     uint32_t q_cap = 0, q_min = 0;                    // finder survivor list: capacity of the last scan / asked minimum
+    bool q_full = false;                              //   the last scan's list could not grow (budget, allocation)
     double last_ms_find = 0, last_ms_count = 0, last_ms_emit = 0, last_ms_wall = 0;
     hipEvent_t ev[6] = {nullptr, nullptr, nullptr, nullptr, nullptr, nullptr};
     uint64_t repairs = 0, chains = 0, candidates = 0, resolved_groups = 0;
@@ -1420,7 +1425,7 @@ static int inflate_devlink(InflateScratch& S, hipStream_t s, const uint32_t* d_w
     hinfo[LI_QCOUNT] = 0;
     INF_CHK(hipMemcpyAsync((void*)(hinfo + LI_QCOUNT), (const uint32_t*)S.d_stats + 8, 4, hipMemcpyDeviceToHost, s));
     INF_CHK(hipStreamSynchronize(s));                          // (1) the number of chain starts
-    if ((uint32_t)hinfo[LI_QCOUNT] > S.q_cap) { S.q_min = (uint32_t)hinfo[LI_QCOUNT] + 65536; return FIND_OVERFLOW; }
+    if ((uint32_t)hinfo[LI_QCOUNT] > S.q_cap && !S.q_full) { S.q_min = (uint32_t)hinfo[LI_QCOUNT] + 65536; return FIND_OVERFLOW; }
     const uint64_t n = hinfo[LI_NCAND];
     // the count pass's width: one wave per chain, unless the chains to count are few against the
     // count waves (fewer than 2 per wave), where a chain's rounds in sequence bound the pass (config
@@ -1717,11 +1722,26 @@ static int find_headers(InflateScratch& S, hipStream_t s, const uint32_t* d_w, u
     const uint64_t scan_end = std::min(end_bit, nbits);
     const uint64_t w_lo = start_bit >> 5;
     const uint64_t nw32 = scan_end > w_lo * 32 ? (scan_end + 31) / 32 - w_lo : 0;
-    // (about one survivor per 1,000 positions on real streams; a longer list is scanned again
-    // with room for all of it, so no survivor is dropped: FIND_OVERFLOW)
-    const uint32_t qcap = (uint32_t)std::min<uint64_t>(0x7FFFFFFFull, std::max<uint64_t>(nbits / 256 + 65536, S.q_min));
+    // The survivor list: nbits / 256 + 64 K entries (about one survivor per 1,000 positions on real
+    // streams).  A scan whose survivors overflowed it is run again with room for all of them
+    // (FIND_OVERFLOW, q_min), up to Q_BUDGET entries (1 GiB of list): periodic stored data can pass
+    // the filters every ~32 bits, and a 4 GiB stream of it would ask for 8 GiB.  Past the budget, or
+    // when the allocation fails, the decode goes on with the list it has (q_full): a survivor past
+    // the list is a chain start not taken -- the chain before it decodes through that block -- so it
+    // costs parallelism, never a result.
+    constexpr uint64_t Q_BUDGET = (1ull << 30) / 8;
+    const uint64_t qbase = std::min<uint64_t>(0x7FFFFFFFull, nbits / 256 + 65536);
+    const uint64_t qtop = std::min<uint64_t>(0x7FFFFFFFull, std::max(qbase, Q_BUDGET));
+    uint32_t qcap = (uint32_t)std::max(qbase, std::min<uint64_t>(S.q_min, qtop));
+    S.q_full = qcap >= qtop;
+    if (inf_ensure(&S.d_q, &S.d_q_cap, (uint64_t)qcap * 8 + 64) != hipSuccess) {
+        (void)hipGetLastError();                     // (an out-of-memory result is not a sticky error)
+        qcap = (uint32_t)qbase;
+        S.q_full = true;
+        S.q_min = 0;
+        INF_CHK(inf_ensure(&S.d_q, &S.d_q_cap, (uint64_t)qcap * 8 + 64));
+    }
     S.q_cap = qcap;
-    INF_CHK(inf_ensure(&S.d_q, &S.d_q_cap, (uint64_t)qcap * 8 + 64));
     uint32_t* d_qcount = (uint32_t*)S.d_stats + 8;
     uint64_t* d_qlist = (uint64_t*)((char*)S.d_q + 64);
     static const uint32_t strict_grid = [] {
@@ -1773,7 +1793,7 @@ static int inflate_headers(InflateScratch& S, hipStream_t s, const uint8_t* in, 
         INF_RC(find_headers(S, s, d_w, nwords, nbits, 0, NONE, d_cnt, d_list));
         INF_CHK(hipMemcpyAsync(&qc, (uint32_t*)S.d_stats + 8, 4, hipMemcpyDeviceToHost, s));
         INF_CHK(hipStreamSynchronize(s));
-        if (qc <= S.q_cap) break;
+        if (qc <= S.q_cap || S.q_full) break;
         S.q_min = qc + 65536;
     }
     INF_CHK(hipMemcpyAsync(cnt.data(), d_cnt, nseg * 4ull, hipMemcpyDeviceToHost, s));
@@ -1847,7 +1867,7 @@ refind:
     INF_CHK(hipMemcpyAsync(hcnt.data(), d_cnt, nseg * 4ull, hipMemcpyDeviceToHost, s));
     INF_CHK(hipMemcpyAsync(&hqc, (const uint32_t*)S.d_stats + 8, 4, hipMemcpyDeviceToHost, s));
     INF_CHK(hipStreamSynchronize(s));
-    if (hqc > S.q_cap && finds++ == 0) { S.q_min = hqc + 65536; goto refind; }
+    if (hqc > S.q_cap && !S.q_full && finds++ == 0) { S.q_min = hqc + 65536; goto refind; }
     std::vector<uint64_t> hoff(nseg + 1);
     hoff[0] = 1;                                   // slot 0 is the range start
     for (uint32_t k = 0; k < nseg; k++) hoff[k + 1] = hoff[k] + std::min(hcnt[k], SEG_CAP);

@@ -85,7 +85,7 @@ __device__ __forceinline__ uint32_t lit_entry(uint32_t sym, uint32_t len) {
         run_base(sym - 257, base, ne);
         return len | (ne << 5) | (K_LEN << 9) | (base << 16);
     }
-    return len | (K_BAD << 9);
+    return len | (K_BAD << 9) | ((sym & 1u) << 16);     // 286 / 287 (bit 16: which, for the Reason)
 }
 __device__ __forceinline__ uint32_t dist_entry(uint32_t sym, uint32_t len) {
     if (sym <= 29) {
@@ -93,8 +93,11 @@ __device__ __forceinline__ uint32_t dist_entry(uint32_t sym, uint32_t len) {
         dist_base(sym, base, ne);
         return len | (ne << 5) | (base << 16);
     }
-    return len | (K_BAD << 9);
+    return len | (K_BAD << 9) | ((sym & 1u) << 16);     // 30 / 31
 }
+// the Reason of a reserved symbol's table entry (K_BAD): its second symbol has an internal code
+__device__ __forceinline__ uint32_t rsv_len(uint32_t e) { return (e >> 16) & 1u ? (uint32_t)R_RESERVED_LEN_HI : (uint32_t)R_RESERVED_LEN; }
+__device__ __forceinline__ uint32_t rsv_dist(uint32_t d) { return (d >> 16) & 1u ? (uint32_t)R_RESERVED_DIST_HI : (uint32_t)R_RESERVED_DIST; }
 
 // Length of a code longer than the primary: the smallest l with code < lim[l] (limits are
 // non-decreasing for a canonical code); branch-free over the five candidate lengths.
@@ -281,7 +284,7 @@ __device__ __forceinline__ void tok_e(uint32_t lo, uint32_t hi, uint32_t e, uint
         const uint32_t cl = e & 31, k = (e >> 9) & 3;
         if (k != K_LEN) {
             pos += cl;
-            kind = k; val = k == K_LIT ? e >> 16 : (uint32_t)R_RESERVED_LEN;
+            kind = k; val = k == K_LIT ? e >> 16 : rsv_len(e);
             if (CAREFUL && pos > nb) { kind = K_BAD; val = R_UEOS; }
             break;
         }
@@ -297,7 +300,7 @@ __device__ __forceinline__ void tok_e(uint32_t lo, uint32_t hi, uint32_t e, uint
         if (!(d & 31)) d = long_dist(d, dw, t);
         const uint32_t dl = d & 31, dxb = (d >> 5) & 15;
         if (CAREFUL && pos + sh + dl > nb) { pos += sh + dl; break; }
-        if (((d >> 9) & 3) == K_BAD) { pos += sh + dl; val = R_RESERVED_DIST; break; }
+        if (((d >> 9) & 3) == K_BAD) { pos += sh + dl; val = rsv_dist(d); break; }
         dist = (d >> 16) + ((dw >> dl) & ((1u << dxb) - 1u));
         pos += sh + dl + dxb;
         if (CAREFUL && pos > nb) break;
@@ -371,7 +374,7 @@ __device__ __forceinline__ void tok_bb(Bb& b, const V& v, const TT& t, bool empt
         const uint32_t cl = e & 31, k = (e >> 9) & 3;
         if (k != K_LEN) {
             bb_skip(b, cl);
-            kind = k; val = k == K_LIT ? e >> 16 : (uint32_t)R_RESERVED_LEN;
+            kind = k; val = k == K_LIT ? e >> 16 : rsv_len(e);
             break;
         }
         const uint32_t xb = (e >> 5) & 15;
@@ -383,7 +386,7 @@ __device__ __forceinline__ void tok_bb(Bb& b, const V& v, const TT& t, bool empt
         uint32_t d = t.dst[dw & ((1u << DB) - 1u)];
         if (!(d & 31)) d = long_dist(d, dw, t);
         const uint32_t dl = d & 31, dxb = (d >> 5) & 15;
-        if (((d >> 9) & 3) == K_BAD) { bb_skip(b, dl); kind = K_BAD; val = R_RESERVED_DIST; break; }
+        if (((d >> 9) & 3) == K_BAD) { bb_skip(b, dl); kind = K_BAD; val = rsv_dist(d); break; }
         dist = (d >> 16) + ((dw >> dl) & ((1u << dxb) - 1u));
         bb_skip(b, dl + dxb);
         kind = K_LEN; n = run; val = 0;

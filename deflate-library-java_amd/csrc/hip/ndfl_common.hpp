@@ -3,6 +3,7 @@
 #pragma once
 #include <hip/hip_runtime.h>
 #include <stdint.h>
+#include <stdio.h>
 #include <stdlib.h>
 #include <string.h>
 
@@ -39,6 +40,15 @@ struct Knobs {
         const char* se = getenv("NDFL_LZ_SEARCH");
         lz_chain = se && !strcmp(se, "chain");
         lz_lead = num("NDFL_LZ_LEAD", -1);
+    }
+    // the effective switches, one line (printed by ndfl_ctx_create when stats are on)
+    void print(FILE* f) const {
+        fprintf(f, "[ndfl] context knobs: stats=%d host_times=%d host_link=%d no_hdrrec=%d emit_fast=%d no_bt=%d "
+                   "no_alias=%d count_w=%u deflate_pf=%d deflate_profile=%d deflate_fused=%d lz_stats=%d "
+                   "lz_search=%s lz_lead=%d\n",
+                (int)stats, (int)host_times, (int)host_link, (int)no_hdrrec, (int)emit_fast, (int)no_bt,
+                (int)no_alias, count_w, (int)deflate_pf, (int)deflate_profile, (int)deflate_fused, (int)lz_stats,
+                lz_chain ? "chain" : "parse", lz_lead);
     }
 };
 

@@ -203,7 +203,8 @@ public final class InflaterInputStream extends InputStream {
 					input.skipNBytes(consumedBefore + used - markPos);
 				}
 			} else {
-				error = new DataFormatException(DataFormatException.Reason.values()[r - 1], "GPU decode: " + r);
+				error = new DataFormatException(DataFormatException.Reason.values()[r - 1],
+					NativeCodec.errorMessage0(codec.handle(), r));
 			}
 			return;
 		}

@@ -63,6 +63,11 @@ final class NativeCodec implements AutoCloseable {
 	static native int inflateRange0(long ctx, ByteBuffer in, long inLen, long startBit, ByteBuffer out, long dictLen,
 		boolean partial, long[] res);
 	
+	// the message of a decode's DataFormatException: ndfl_error_string(reason), with the reserved
+	// symbol appended where the reference appends it, "Reserved run length symbol: " + sym /
+	// "Reserved distance symbol: " + sym (D/decomp/Open.java:516, 550; ndfl_ctx_error_symbol)
+	static native String errorMessage0(long ctx, int reason);
+	
 	static native int crc320(long ctx, int crc, ByteBuffer data, long len);
 	static native int adler320(long ctx, int adler, ByteBuffer data, long len);
 	

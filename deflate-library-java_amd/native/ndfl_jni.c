@@ -15,6 +15,7 @@
  */
 #include <jni.h>
 #include <stdint.h>
+#include <stdio.h>
 #include <stdlib.h>
 #include "ndfl.h"
 
@@ -36,6 +37,21 @@ static int check(JNIEnv* env, int r) {
 
 static uint8_t* addr(JNIEnv* env, jobject buf) { return buf ? (uint8_t*)(*env)->GetDirectBufferAddress(env, buf) : NULL; }
 static uint64_t cap(JNIEnv* env, jobject buf) { return buf ? (uint64_t)(*env)->GetDirectBufferCapacity(env, buf) : 0; }
+
+/* DataFormatException's message for a decode's Reason r: the reference's text (ndfl_error_string),
+ * with the reserved symbol appended where the reference appends it (D/decomp/Open.java:516, 550) */
+JNIEXPORT jstring JNICALL Java_io_nayuki_deflate_gpu_NativeCodec_errorMessage0(JNIEnv* env, jclass k, jlong ctx,
+        jint reason) {
+    (void)k;
+    char msg[160];
+    const int sym = (reason == NDFL_RESERVED_LENGTH_SYMBOL || reason == NDFL_RESERVED_DISTANCE_SYMBOL)
+                    ? ndfl_ctx_error_symbol(CTX(ctx)) : -1;
+    if (sym >= 0)
+        snprintf(msg, sizeof msg, "%s: %d", ndfl_error_string(reason), sym);
+    else
+        snprintf(msg, sizeof msg, "%s", ndfl_error_string(reason));
+    return (*env)->NewStringUTF(env, msg);
+}
 
 JNIEXPORT jlong JNICALL Java_io_nayuki_deflate_gpu_NativeCodec_create(JNIEnv* env, jclass k, jint device) {
     (void)k;

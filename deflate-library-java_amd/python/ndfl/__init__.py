@@ -52,9 +52,15 @@ class DataFormatException(Exception):
     """Unchecked in the reference (extends RuntimeException, D/DataFormatException.java:15): it is
     not made sticky by InflaterInputStream and not caught by the CLIs."""
 
-    def __init__(self, reason, msg=None):
+    def __init__(self, reason, msg=None, symbol=-1):
         self.reason = reason
-        super().__init__(msg or load().ndfl_error_string(reason.value + 1).decode())
+        if msg is None:
+            msg = load().ndfl_error_string(reason.value + 1).decode()
+            # the reference names the reserved symbol: "Reserved run length symbol: " + sym,
+            # "Reserved distance symbol: " + sym (D/decomp/Open.java:516, 550, 659, 674)
+            if symbol >= 0 and reason in (Reason.RESERVED_LENGTH_SYMBOL, Reason.RESERVED_DISTANCE_SYMBOL):
+                msg += f": {symbol}"
+        super().__init__(msg)
 
     def getReason(self):
         return self.reason
@@ -329,6 +335,16 @@ class Context:
             reason = None if r == 0 else Reason(r - 1)
             return reason, out.raw[:olen], bits
 
+    def error_symbol(self):
+        """ndfl_ctx_error_symbol: the reserved symbol behind the last decode's RESERVED_LENGTH_SYMBOL /
+        RESERVED_DISTANCE_SYMBOL (286/287, 30/31), or -1."""
+        return load().ndfl_ctx_error_symbol(self._h)
+
+    def data_format_error(self, code):
+        """The DataFormatException of a decode that returned Reason+1 `code`, with the reference's
+        message (the symbol appended where D/decomp/Open.java appends it)."""
+        return DataFormatException(Reason(code - 1), symbol=self.error_symbol())
+
     def inflate_range_raw(self, in_addr, in_len, start_bit, end_bit, out_addr, dict_len, out_cap, flags):
         """ndfl_inflate_range: decode bits [start_bit, end_bit) into out_addr + dict_len, with the
         dict_len bytes at out_addr as the window.  Returns (code, out_len, consumed_bits)."""
@@ -470,9 +486,10 @@ def compress(data, strategy=Strategy.RLE_DYNAMIC):
 
 
 def decompress(data):
-    reason, out, _ = default_context().inflate(data)
+    ctx = default_context()
+    reason, out, _ = ctx.inflate(data)
     if reason is not None:
-        raise DataFormatException(reason)
+        raise ctx.data_format_error(reason.value + 1)
     return out
 
 

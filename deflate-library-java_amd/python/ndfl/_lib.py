@@ -39,7 +39,7 @@ EXPORTS = ["ndfl_abi_version", "ndfl_error_string", "ndfl_ctx_create", "ndfl_ctx
            "ndfl_deflate_bound",
            "ndfl_inflate", "ndfl_inflate_range", "ndfl_inflate_resolve", "ndfl_bits_shift", "ndfl_crc32", "ndfl_adler32",
            "ndfl_crc32_combine", "ndfl_decide", "ndfl_compress_to", "ndfl_decision_free", "ndfl_inflate_sync",
-           "ndfl_inflate_tail", "ndfl_inflate_headers", "ndfl_inflate_tail_map"]
+           "ndfl_inflate_tail", "ndfl_inflate_headers", "ndfl_inflate_tail_map", "ndfl_ctx_error_symbol"]
 
 KIND_LZ77, KIND_UNCOMPRESSED = 0, 1
 
@@ -80,6 +80,7 @@ def load():
     L.ndfl_ctx_last_kernel_ms.restype = ctypes.c_double
     L.ndfl_ctx_last_kernel_ms.argtypes = [vp]
     L.ndfl_ctx_timings.argtypes = [vp, ctypes.POINTER(ctypes.c_double), i32]
+    L.ndfl_ctx_error_symbol.argtypes = [vp]
     L.ndfl_deflate_chunks.argtypes = [vp, vp, u32, u32, vp, u64, u32, i32, i32, u32, vp, u64,
                                       ctypes.POINTER(u64), ctypes.POINTER(u32), u32]
     L.ndfl_deflate_chunks_lz77.argtypes = [vp, vp, u32, u32, vp, u64, u32, i32, i32, i32, i32, i32, i32, u32, vp,

@@ -5,7 +5,8 @@ on raw input (D/DeflaterOutputStream.java:119-137).  So rank r 
 [r*K, (r+1)*K) by itself.  The exchange steps are the only places where ranks talk to each other:
 
   compress    (1) the raw bytes preceding the shard (the encoder's history, <= 32 KiB) go from
-                  rank r-1 to rank r, point to point;
+                  rank r-1 to rank r, point to point (one all_gather of every rank's last 32 KiB when
+                  shards are shorter than that, so a history spans several earlier shards);
               (2) all_gather of every shard's bit count and byte count: the seam index;
               (3) each rank moves its bits to its global bit offset mod 8 (ndfl_bits_shift), so
                   the global stream is the concatenation of the shards with the shared boundary
@@ -170,13 +171,27 @@ def deflate_shard(codec, dist, torch, shard, rank, world, *, strategy="RLE_DYNAM
     n = shard.numel()
     if rank + 1 < world and (n == 0 or n % chunk_len):
         raise ValueError("every shard but the last must be a positive multiple of chunk_len")
-    # (1) history: the last min(hist_limit, n) raw bytes of the previous shard
+    # (1) history: the last min(hist_limit, bytes before the shard) raw bytes of the stream
     hlen = min(hist_limit, n)
     sizes = _gather_ints(dist, torch, n, world, codec.device)
-    prev_h = min(hist_limit, sizes[rank - 1]) if rank > 0 else 0
-    hist = codec.empty(prev_h)[:prev_h]
-    _exchange_prev(dist, torch, shard[n - hlen:].contiguous() if hlen else codec.empty(0)[:0], hist, rank, world)
-    if prev_h < min(hist_limit, sum(sizes[:rank])):
+    want_h = min(hist_limit, sum(sizes[:rank]))
+    if all(v >= hist_limit for v in sizes[:-1]):
+        # every shard holds a whole window: the previous rank's last bytes, point to point
+        prev_h = min(hist_limit, sizes[rank - 1]) if rank > 0 else 0
+        hist = codec.empty(prev_h)[:prev_h]
+        _exchange_prev(dist, torch, shard[n - hlen:].contiguous() if hlen else codec.empty(0)[:0], hist, rank,
+                       world)
+    else:
+        # shards shorter than the window (small inputs over many ranks): the history spans several
+        # earlier shards -- one all_gather of every rank's last <= hist_limit bytes (padded to one size)
+        tail = codec.empty(hist_limit)[:hist_limit] if hist_limit else codec.empty(1)[:1]
+        if hlen:
+            tail[hist_limit - hlen:] = shard[n - hlen:]
+        tails = _all_gather_tensor(dist, torch, tail, world)
+        pieces = [tails[k][hist_limit - min(hist_limit, sizes[k]):hist_limit] for k in range(rank)]
+        hist = torch.cat(pieces)[-want_h:] if want_h else codec.empty(0)[:0]
+        prev_h = want_h
+    if prev_h < want_h:
         raise ValueError("a shard shorter than the history window precedes this one")
     # local compress at bit 0
     cap = codec.bound(n, chunk_len)

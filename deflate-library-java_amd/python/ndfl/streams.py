@@ -364,7 +364,7 @@ class InflaterInputStream:
                     else:
                         self._in.seek(-len(rest), os.SEEK_CUR)
                 return
-            self._error = DataFormatException(Reason(r - 1))
+            self._error = self._ctx.data_format_error(r)
             return
 
     def _ensure(self):

@@ -71,7 +71,12 @@ typedef struct ndfl_ctx ndfl_ctx;
 uint32_t ndfl_abi_version(void);
 const char* ndfl_error_string(int code);
 
-/* Create a context on HIP device `device`.  Fails with NDFL_E_DEVICE if no GPU. */
+/* Create a context on HIP device `device`.  Fails with NDFL_E_DEVICE if no GPU.
+ * The NDFL_* environment switches (test hand-over paths, statistics, A/B alternatives: the Knobs of
+ * csrc/hip/ndfl_common.hpp; none is needed in production) are read ONCE, here: setting or changing
+ * one after a context exists has no effect on it -- create a new context to measure another
+ * setting.  A switch is on when set to anything but "0".  With NDFL_STATS on, the context prints its
+ * effective switches once to stderr, so a profiling run shows which path it measured. */
 int ndfl_ctx_create(ndfl_ctx** out, int device, uint32_t flags);
 int ndfl_ctx_destroy(ndfl_ctx* ctx);
 /*
@@ -91,6 +96,11 @@ double ndfl_ctx_last_kernel_ms(ndfl_ctx* ctx);
  * [2] inflate count, [3] inflate emit, [4] inflate device span, [5] linked chains, [6] repaired
  * boundaries, [7] header candidates. */
 int ndfl_ctx_timings(ndfl_ctx* ctx, double* ms, int n);
+/* The reserved symbol behind the last ndfl_inflate / ndfl_inflate_range that returned
+ * NDFL_RESERVED_LENGTH_SYMBOL (286 or 287) or NDFL_RESERVED_DISTANCE_SYMBOL (30 or 31), else -1:
+ * the reference's message names it -- "Reserved run length symbol: " + sym,
+ * "Reserved distance symbol: " + sym (D/decomp/Open.java:516, 550, 659, 674). */
+int ndfl_ctx_error_symbol(ndfl_ctx* ctx);
 
 /*
  * Compress K consecutive chunks of one DEFLATE stream.

@@ -797,6 +797,11 @@ static int dynamic_header(br_t* r, int16_t* litTree, int16_t* distTree, int16_t*
  * Range form (multi-GPU shards): decoding starts at bit `start_bit` with `dict_len` bytes of
  * preceding output available to copies (the reference's 32 KiB ring, :592-603), and stops at the
  * first block boundary == `end_bit` (UINT64_MAX: after the final block). */
+/* the reserved symbol of the calling thread's last RESERVED_*_SYMBOL error (the reference's message
+ * appends it: "Reserved run length symbol: " + sym, D/decomp/Open.java:516, 550), else -1 */
+static _Thread_local int or_err_sym = -1;
+int or_error_symbol(void) { return or_err_sym; }
+
 int or_inflate_range(const uint8_t* in, uint64_t in_len, uint64_t start_bit, uint64_t end_bit,
                      const uint8_t* dict, uint64_t dict_len, uint8_t* out, uint64_t out_cap,
                      uint64_t* out_len, uint64_t* consumed_bits) {
@@ -804,6 +809,7 @@ int or_inflate_range(const uint8_t* in, uint64_t in_len, uint64_t start_bit, uin
     uint64_t n = 0;
     if (dict_len > 32768) { dict += dict_len - 32768; dict_len = 32768; }
     int err = 0, last = 0;
+    or_err_sym = -1;
     int16_t litTree[2 * 288], distTree[2 * 32], clTree[2 * 19];
     int16_t fixLit[2 * 288], fixDist[2 * 32];
     {
@@ -850,14 +856,14 @@ int or_inflate_range(const uint8_t* in, uint64_t in_len, uint64_t start_bit, uin
                 continue;
             }
             if (sym == 256) break;
-            if (sym > 285) CHK(OR_RESERVED_LENGTH_SYMBOL);  /* :513-517, :655-660 */
+            if (sym > 285) { or_err_sym = sym; CHK(OR_RESERVED_LENGTH_SYMBOL); }  /* :513-517, :655-660 */
             uint32_t e;
             CHK(br_bits(&r, RUN_EXTRA[sym - 257], &e));
             int run = RUN_BASE[sym - 257] + (int)e;
             if (!dt) CHK(OR_LENGTH_ENCOUNTERED_WITH_EMPTY_DISTANCE_CODE);
             int dsym;
             CHK(decode_sym(&r, dt, &dsym));
-            if (dsym > 29) CHK(OR_RESERVED_DISTANCE_SYMBOL);
+            if (dsym > 29) { or_err_sym = dsym; CHK(OR_RESERVED_DISTANCE_SYMBOL); }   /* :548-551, :673-675 */
             CHK(br_bits(&r, DIST_EXTRA[dsym], &e));
             uint64_t dist = (uint64_t)DIST_BASE[dsym] + e;
             uint64_t dictLen = n + dict_len < 32768 ? n + dict_len : 32768;

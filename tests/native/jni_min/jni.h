@@ -16,6 +16,7 @@ struct _jobject;
 typedef struct _jobject* jobject;
 typedef jobject jclass;
 typedef jobject jthrowable;
+typedef jobject jstring;
 typedef jobject jarray;
 typedef jarray jbyteArray;
 typedef jarray jintArray;
@@ -38,5 +39,6 @@ struct JNINativeInterface_ {
     void (*SetLongArrayRegion)(JNIEnv*, jlongArray, jsize, jsize, const jlong*);
     void* (*GetDirectBufferAddress)(JNIEnv*, jobject);
     jlong (*GetDirectBufferCapacity)(JNIEnv*, jobject);
+    jstring (*NewStringUTF)(JNIEnv*, const char*);
 };
 #endif

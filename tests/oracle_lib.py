@@ -94,8 +94,16 @@ def lib():
         L.or_zlib_compress.argtypes = [u8p, ctypes.c_uint64, ctypes.c_int, ctypes.c_int, u8p, ctypes.c_uint64]
         L.or_zlib_decompress.restype = ctypes.c_int
         L.or_zlib_decompress.argtypes = [u8p, ctypes.c_uint64, u8p, ctypes.c_uint64, ctypes.POINTER(ctypes.c_uint64)]
+        L.or_error_symbol.restype = ctypes.c_int
+        L.or_error_symbol.argtypes = []
         _LIB = L
     return _LIB
+
+
+def error_symbol():
+    """The reserved symbol of this thread's last RESERVED_LENGTH_SYMBOL / RESERVED_DISTANCE_SYMBOL
+    decode error (the suffix of the reference's message, D/decomp/Open.java:516, 550), else -1."""
+    return lib().or_error_symbol()
 
 
 def _buf(data):

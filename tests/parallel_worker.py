@@ -83,6 +83,8 @@ class OracleCodec:
         for f in (lambda i: i & 255, lambda i: i >> 8, lambda i: 255 - (i & 255)):
             tmp = out.clone()
             win = bytes(f(i) for i in range(dict_len))
+            if dict_len:               # (a tail longer than the range's output reaches into the window)
+                tmp[:dict_len] = torch.frombuffer(bytearray(win), dtype=torch.uint8)
             code, olen, _ = self._decode(data, start, end, tmp, dict_len, win)
             outs.append(tmp[dict_len + olen - n:dict_len + olen].to(torch.int32))
         o0, o1, o2 = outs

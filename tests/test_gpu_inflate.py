@@ -11,7 +11,7 @@ import zlib
 import pytest
 
 import oracle_lib as O
-from test_oracle_inflate import KAT, quasi_log_len, lsb_bits, LSB8, MSB_LIT
+from test_oracle_inflate import KAT, quasi_log_len, lsb_bits, LSB8, MSB_LIT, reserved_symbol_streams
 
 pytestmark = pytest.mark.gpu
 
@@ -51,6 +51,25 @@ def test_known_answer(ctx, kat):
             assert (bits + 7) // 8 == len(data)
         else:
             assert reason == kat["expect_reason"]
+
+
+def test_reserved_symbol_in_the_message(ctx):
+    """The reserved symbol reaches the caller as the reference names it: "Reserved run length
+    symbol: 287", "Reserved distance symbol: 31" (D/decomp/Open.java:516, 550) -- the four fixed-Huffman
+    KATs and two dynamic blocks (287 used by a code, 31 as the padding of a single distance code),
+    symbol equal to the oracle's."""
+    import ndfl
+    for name, data, want, reason, sym in reserved_symbol_streams():
+        r, out, _ = ctx.inflate(data)
+        assert r is not None and r.name == reason, name
+        assert ctx.error_symbol() == sym == (O.inflate(data), O.error_symbol())[1], name
+        assert want is None or out == want, name
+        e = ctx.data_format_error(r.value + 1)
+        prefix = "Reserved run length symbol" if reason == "RESERVED_LENGTH_SYMBOL" else "Reserved distance symbol"
+        assert str(e) == f"{prefix}: {sym}", name
+        with pytest.raises(ndfl.DataFormatException, match=f": {sym}$"):
+            ndfl.InflaterInputStream(io.BytesIO(data), context=ctx).read()
+    assert ctx.inflate(O.deflate(b"abc"))[0] is None and ctx.error_symbol() == -1
 
 
 def test_generators(ctx):

@@ -148,6 +148,70 @@ def test_deferred_window_then_resolve(env, seed):
             ctx.inflate_resolve()                       # nothing pending any more
 
 
+@pytest.mark.parametrize("seed,a,strategy", [(3, 4, "RLE_DYNAMIC"), (4, 4, "FULL_DYNAMIC"), (5, 1, "FULL_DYNAMIC")])
+def test_tail_map_composes_to_tail_and_resolved_output(env, seed, a, strategy):
+    """ndfl_inflate_tail_map on the real device decode: a deferred range decode's last n bytes as a
+    map of its window, applied to the true window, equal ndfl_inflate_tail and the resolved output --
+    for tails inside the range's output and tails longer than it (reaching into the window: the map
+    then points those bytes back at their own window index), and a range whose output is shorter
+    than the window (a = 1: a short first shard)."""
+    torch, ndfl, ctx = env
+    rng = random.Random(seed)
+    parts = []
+    for k in range(6):
+        parts.append(mixed_bytes(30000, seed=seed * 10 + k))
+        parts.append(bytes([rng.getrandbits(8)]) * rng.randint(100, 30000))
+    data = b"".join(parts)
+    chunk = 16384 if a == 1 else 65536
+    comp, seams = _stream_and_seams(data, strategy, chunk)
+    pre = a * chunk
+    window = data[max(0, pre - 32768):pre]
+    dict_len = len(window)
+    # a range of one or two chunks: its output may be shorter than a window
+    b = min(a + (1 if a == 1 else 2), len(seams) - 1)
+    e_bit = seams[b] if b < len(seams) - 1 else None
+    r0, ref, _ = O.inflate_range(comp, seams[a], e_bit, window)
+    assert r0 is None
+    dev_in = torch.frombuffer(bytearray(comp), dtype=torch.uint8).cuda()
+    out = torch.full((dict_len + len(ref) + 64,), 0xEE, dtype=torch.uint8, device="cuda")
+    r, olen, _ = ctx.inflate_range_raw(dev_in.data_ptr(), len(comp), seams[a], e_bit, out.data_ptr(), dict_len,
+                                       len(ref) + 64, ndfl.IN_DEVICE | ndfl.OUT_DEVICE | ndfl.DICT_DEFERRED)
+    assert (r, olen) == (0, len(ref))
+    full = window + ref
+    win_t = torch.frombuffer(bytearray(window), dtype=torch.uint8).cuda().long()
+    for n in sorted({min(len(full), x) for x in (5, 4096, len(ref), len(ref) + 1000, 32768)}):
+        m = torch.zeros(n, dtype=torch.int32, device="cuda")
+        assert ctx.inflate_tail_map_raw(n, m.data_ptr())
+        mm = m.long()
+        lit = mm < 0
+        assert bool((lit | ((mm >= 0) & (mm < dict_len))).all()), n
+        got = torch.where(lit, mm & 0xFF, win_t[torch.where(lit, torch.zeros_like(mm), mm)] if dict_len else mm & 0xFF)
+        assert bytes(got.to(torch.uint8).cpu().numpy()) == full[-n:], n
+        # bytes the map takes from the window in the part before the range's output: themselves
+        k0 = max(0, n - len(ref))
+        if k0:
+            idx = torch.arange(dict_len - k0, dict_len, device="cuda")
+            assert bool((mm[:k0] == idx).all()), n
+    out[:dict_len] = torch.frombuffer(bytearray(window), dtype=torch.uint8).cuda()
+    for n in (min(len(full), 32768), 7):
+        tail = torch.zeros(n, dtype=torch.uint8, device="cuda")
+        assert ctx.inflate_tail_raw(n, tail.data_ptr())
+        assert bytes(tail.cpu().numpy()) == full[-n:]
+    ctx.inflate_resolve()
+    assert bytes(out[dict_len:dict_len + olen].cpu().numpy()) == ref
+
+
+def test_sharded_protocol_small_shards_one_gpu():
+    """4 ranks on cuda:0 with 4 KiB shards: the encoder history and the decode window each span
+    several earlier shards (composed through up to 3 tail maps whose tails reach into their own
+    windows)."""
+    from test_parallel_cpu import run_workers
+    res = run_workers(4, dict(chunk_len=4096, chunks_per_rank=1, last_bytes=2000, seed=25,
+                              strategy="FULL_DYNAMIC", seam_run=False, codec="device"))
+    assert res[0]["stream_equal"] and all(r["gathered_equal"] for r in res)
+    assert all(r["code"] == 0 and r["decoded_equal"] for r in res)
+
+
 @pytest.mark.parametrize("world", [2, 3])
 def test_sharded_protocol_ranks_one_gpu(world):
     """The whole sharded protocol with 2 and 3 ranks sharing cuda:0 over gloo; with 3, the middle

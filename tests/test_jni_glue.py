@@ -23,7 +23,7 @@ GLUE = os.path.join(PKG, "native", "ndfl_jni.c")
 SHIM = os.path.join(PKG, "java", "io", "nayuki", "deflate", "gpu", "NativeCodec.java")
 
 JNI_TYPE = {"long": "jlong", "int": "jint", "boolean": "jboolean", "void": "void", "byte": "jbyte",
-            "ByteBuffer": "jobject", "int[]": "jintArray", "long[]": "jlongArray", "byte[]": "jbyteArray"}
+            "ByteBuffer": "jobject", "String": "jstring", "int[]": "jintArray", "long[]": "jlongArray", "byte[]": "jbyteArray"}
 
 
 @pytest.mark.skipif(shutil.which("gcc") is None, reason="gcc not installed")
@@ -62,3 +62,14 @@ def test_jni_entry_points_match_the_java_natives():
     assert set(java) == set(c), (sorted(set(java) - set(c)), sorted(set(c) - set(java)))
     for name, sig in java.items():
         assert c[name] == sig, (name, sig, c[name])
+
+
+def test_shim_builds_decode_messages_from_the_c_abi():
+    """The shim's DataFormatException for a decode error carries the reference's message
+    (ndfl_error_string, with the reserved symbol appended as D/decomp/Open.java:516, 550 do), not a
+    placeholder of its own."""
+    src = open(os.path.join(PKG, "java", "io", "nayuki", "deflate", "gpu", "InflaterInputStream.java")).read()
+    assert '"GPU decode' not in src
+    assert re.search(r"new DataFormatException\([^;]*NativeCodec\.errorMessage0\(", src, re.S)
+    glue = open(GLUE).read()
+    assert "ndfl_ctx_error_symbol" in glue and "ndfl_error_string(reason)" in glue

@@ -166,6 +166,43 @@ def test_reserved_symbols_and_quirks():
     assert reason == "END_OF_BLOCK_CODE_ZERO_LENGTH"
 
 
+def reserved_symbol_streams():
+    """(name, stream, expected output or None, Reason, symbol) for each reserved symbol the reference names
+    in its message ("Reserved run length symbol: " + sym, "Reserved distance symbol: " + sym,
+    D/decomp/Open.java:516, 550, 659, 674): the four fixed-Huffman KATs of T/InflaterInputStreamTest.java
+    (the symbol is in their names) and two dynamic blocks -- a code that uses length symbol 287, and a
+    single one-bit distance code, which the reference pads with symbol 31 (:398-425) and a 1 bit then
+    decodes (lit code {65: 1, 256: 2, 287 or 257: 2}; code-length code {0: 1, 1: 2, 2: 2})."""
+    out = []
+    for k in KAT:
+        if k["expect_reason"] in ("RESERVED_LENGTH_SYMBOL", "RESERVED_DISTANCE_SYMBOL"):
+            sym = int(k["name"].rsplit("Code", 1)[1])
+            out.append((k["name"], O.bits_to_bytes(k["bits"], 0, random.Random(0)), None, k["expect_reason"], sym))
+    clc = [0] * 19
+    clc[3], clc[17], clc[15] = 1, 2, 2            # code-length symbols 0, 1, 2 (positions in CLO)
+    enc = {0: "0", 1: "10", 2: "11"}
+    for name, hlit, lsym, dist_len, data_bits, reason, sym in [
+            ("dynamicLengthSymbol287", 31, 287, 0, "0" + "11", "RESERVED_LENGTH_SYMBOL", 287),
+            ("dynamicPaddedDistanceSymbol31", 1, 257, 1, "0" + "11" + "1", "RESERVED_DISTANCE_SYMBOL", 31)]:
+        nlit = hlit + 257
+        lens = [0] * nlit + [dist_len]
+        lens[65], lens[256], lens[lsym] = 1, 2, 2
+        bits = ("1" + "01" + lsb_bits(hlit, 5) + lsb_bits(0, 5) + lsb_bits(14, 4)
+                + "".join(lsb_bits(x, 3) for x in clc[:18]) + "".join(enc[x] for x in lens) + data_bits)
+        out.append((name, O.bits_to_bytes(bits + "0" * 16), b"A", reason, sym))
+    return out
+
+
+def test_oracle_reports_the_reserved_symbol():
+    streams = reserved_symbol_streams()
+    assert len(streams) == 6
+    for name, data, want, reason, sym in streams:
+        r, out, _ = O.inflate(data)
+        assert (r, O.error_symbol()) == (reason, sym), name
+        assert want is None or out == want, name
+    assert O.inflate(O.deflate(b"abc"))[0] is None and O.error_symbol() == -1
+
+
 @pytest.mark.parametrize("strategy,chunk_len", [("RLE_DYNAMIC", 65536), ("FULL_DYNAMIC", 4096),
                                                 ("UNCOMPRESSED", 65536), ("RLE_DYNAMIC", 300)])
 def test_scan_headers_finds_every_chain_start(strategy, chunk_len):

@@ -42,6 +42,11 @@ def run_workers(world, cfg):
     (8, dict(chunk_len=65536, chunks_per_rank=2, last_bytes=90001, seed=21, strategy="RLE_DYNAMIC", seam_run=True,
              async_gather=True)),
     (8, dict(chunk_len=32768, chunks_per_rank=1, last_bytes=5, seed=22, strategy="FULL_DYNAMIC", seam_run=True)),
+    # shards far shorter than the window: a rank's encoder history spans several earlier shards, and
+    # its decode window is composed through the maps of up to 7 earlier ranks, each of whose tail maps
+    # points back into that rank's own window (its output alone is shorter than 32 KiB)
+    (8, dict(chunk_len=4096, chunks_per_rank=1, last_bytes=3001, seed=23, strategy="FULL_DYNAMIC", seam_run=False)),
+    (8, dict(chunk_len=4096, chunks_per_rank=2, last_bytes=100, seed=24, strategy="RLE_DYNAMIC", seam_run=False)),
 ])
 def test_sharded_stream_roundtrip(world, cfg):
     res = run_workers(world, cfg)

@@ -191,6 +191,9 @@ class ErrorCtx:
         ctypes.memmove(out_addr + dict_len, self.out, len(self.out))
         return O.REASONS.index(self.reason) + 1, len(self.out), self.bits
 
+    def data_format_error(self, code):
+        return ndfl.DataFormatException(ndfl.Reason(code - 1))
+
 
 def _corrupt_stream():
     rng = np.random.default_rng(4)
