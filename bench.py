@@ -275,6 +275,11 @@ def main():
                           "inflate_device_span": round(state["t_inflate_span"], 3),
                           "inflate_chains": int(state["chains"]), "inflate_repairs": int(state["repairs"]),
                           "inflate_candidates": int(state["cands"])},
+            # per direction, against the 8 TB/s peak: the encoder reads N and writes C; the decoder reads
+            # C and writes N.  north_star's decompress bar is quoted on the read side (C / span); at
+            # N >= C a decoder moving C + N bytes cannot read faster than peak * C / (C + N), so the
+            # (C + N) fraction is the one a decoder can approach ("The decompress bar")
+            "directions": directions(n, state["cbytes"], kd, state["t_inflate_span"]),
             "roofline": {"bound": "hbm", "kernel": dom, "achieved": round(achieved / 1e9, 2), "peak": HBM_PEAK / 1e9,
                          "unit": "GB/s", "frac": round(achieved / HBM_PEAK, 4), "traffic": traffic,
                          "traffic_source": traffic_src,
@@ -309,11 +314,31 @@ def launch_ranks(n):
     return subprocess.call(cmd)
 
 
+def directions(n, c, deflate_ms, inflate_span_ms):
+    """Achieved bytes per second of each direction on one rank (algorithmic bytes / device span) and
+    their fractions of the HBM peak: compress moves N + C, decompress C + N, and the decompress read
+    side alone is C / span (north_star's bar)."""
+    def rate(b, ms):
+        return b / (ms / 1e3) if ms > 0 else 0.0
+    comp = rate(n + c, deflate_ms)
+    dec = rate(c + n, inflate_span_ms)
+    rd = rate(c, inflate_span_ms)
+    return {"compress": {"bytes": n + c, "ms": round(deflate_ms, 3), "GBps": round(comp / 1e9, 1),
+                         "frac_of_peak": round(comp / HBM_PEAK, 4)},
+            "decompress": {"bytes": c + n, "ms": round(inflate_span_ms, 3), "GBps": round(dec / 1e9, 1),
+                           "frac_of_peak": round(dec / HBM_PEAK, 4), "read_GBps": round(rd / 1e9, 1),
+                           "read_frac_of_peak": round(rd / HBM_PEAK, 4),
+                           "read_frac_ceiling": round(c / (c + n), 4) if c + n else None}}
+
+
 def pmc_traffic(kernel, n):
     """HBM bytes per launch of `kernel` from the newest committed rocprofv3 --pmc summary of this same
-    bench command (profiles/rNN_traffic.json, made by scripts/profile_bench.sh + scripts/traffic_summary.py:
-    FETCH_SIZE and WRITE_SIZE passes, gfx950 corrections applied).  Counters cannot be read from inside
-    the timed run, so the value is the profiled one, quoted only for the default 4 GiB workload."""
+    bench command (profiles/rNN_traffic.json, made by scripts/profile_bench.sh + scripts/traffic_summary.py
+    from a FETCH_SIZE and a WRITE_SIZE pass).  FETCH_SIZE is corrected per kernel by the factor the
+    JSON records for it (`fetch_correction`, calibrated on known byte counts in the kernel's own load
+    shapes by scripts/r06/fetch_calib.hip; the guide's x2 for 16-B/lane and LDS-DMA loads); WRITE_SIZE
+    is taken as reported.  Counters cannot be read from inside the timed run, so the value is the
+    profiled one, quoted only for the default 4 GiB workload."""
     import glob
     found = sorted(glob.glob(os.path.join(ROOT, "profiles", "r[0-9][0-9]_traffic.json")))
     path = found[-1] if found else os.path.join(ROOT, "profiles", "r01_traffic.json")
