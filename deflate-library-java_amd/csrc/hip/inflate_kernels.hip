@@ -178,28 +178,37 @@ struct Rp {
 };
 
 // codeLengthsToCodeTree's error detection (D/decomp/Open.java:705-756) from per-length counts.
-__device__ int tree_check(const uint32_t (&cnt)[16]) {
+// Straight-line (no early exit inside the loop): fully unrolled with constant indices, so the
+// counts stay in registers -- a loop with a break left them in scratch memory (round 6).
+__device__ __forceinline__ int tree_check(const uint32_t (&cnt)[16]) {
     uint32_t num = 0, maxL = 0;
 #pragma unroll
-    for (int l = 1; l < 16; l++) { num += cnt[l]; if (cnt[l]) maxL = (uint32_t)l; }
+    for (int l = 1; l < 16; l++) { num += cnt[l]; maxL = cnt[l] ? (uint32_t)l : maxL; }
     if (num < 2) return R_UNDER_FULL;
-    const uint64_t R = 2ull * (num - 1);
-    uint64_t next = 0, end = 2;
+    // (32-bit: end stays below R + 2 <= 2 * 320, or the under-full test has fired -- 64-bit
+    // compares of wave-uniform values went through the vector unit)
+    const uint32_t R = 2u * (num - 1);
+    uint32_t next = 0, end = 2;
+    int res = 0;
 #pragma unroll
     for (uint32_t l = 1; l < 16; l++) {
-        if (l > maxL) break;
+        const bool on = l <= maxL && res == 0;
         if (l > 1) {
-            uint64_t open = end - next;
-            if (open > 0) {
-                if (end + 2 * (open - 1) >= R) return R_UNDER_FULL;
-                next = end;
-                end += 2 * open;
-            }
+            const uint32_t open = end - next;
+            const bool op = on && open > 0;
+            const bool uf = op && end + 2 * (open - 1) >= R;
+            res = uf ? (int)R_UNDER_FULL : res;
+            const bool adv = op && !uf;
+            next = adv ? end : next;
+            end = adv ? end + 2 * open : end;
         }
-        uint64_t c = cnt[l];
-        if (c > end - next) return R_OVER_FULL;
-        next += c;
+        const bool on2 = on && res == 0;
+        const uint32_t c = cnt[l];
+        const bool of = on2 && c > end - next;
+        res = of ? (int)R_OVER_FULL : res;
+        next = (on2 && !of) ? next + c : next;
     }
+    if (res) return res;
     if (end != R) return R_INTERNAL;
     if (next < end) return R_UNDER_FULL;
     return 0;

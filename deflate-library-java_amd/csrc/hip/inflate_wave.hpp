@@ -759,9 +759,272 @@ __device__ void fixed_lens(Shared& S, int lane) {
     }
 }
 
-// Tables for the block whose header S.h_* describes.  Returns a Reason (uniform) or 0.
+// ---- table build, round 6 ---------------------------------------------------------------------
+// The same tables (word for word where a decoder reads them: scripts/r06/build_bench.hip compares
+// every header of a config-4 stream), built with a fraction of the instructions.  The build above
+// runs as a call from the decode passes and took ~33 K cycles for a literal/length code at one wave
+// per SIMD: its per-length arrays (counts, first codes, rank offsets) sat in scratch memory, indexed
+// by each lane's code length; its tree check compared 64-bit values in the vector unit; 15-way
+// select chains picked a lane's per-length values; codes were written one symbol at a time; and
+// every LDS access went through a generic pointer (a null check and a conversion per access, the
+// callee not knowing its arguments were LDS).  A single wave issues about one instruction per few
+// cycles, so the instruction count -- scalar ones included -- sets the time.  Here:
+//   * LDS-typed pointers (address space 3) and the primary bits as a template parameter;
+//   * ranks bit-sliced: four ballots give each lane the mask of lanes whose length equals its own;
+//   * per-length values (rank offset O, first code F, O - F) in LDS, read by length (`scr`: 64 words
+//     of the round stage, which holds nothing while a block's tables are built);
+//   * complete codes decided by their Kraft sum in a few scalar adds (the level-wise check of the
+//     reference's error order only runs for the others: corrupt streams);
+//   * the primary table PULLED, all of a lane's entries at once: lane j computes the entries
+//     k = i * 64 + j -- the code length from the left-justified limits (codes of length <= L occupy
+//     [0, LJ[L]) of the MSB-first prefix space), the symbol from the code's rank, through the
+//     canonical entry array every symbol wrote into the extension area (x[O[l] + rank]: the slow
+//     path's array anyway);
+//   * the long codes' prefixes and second-level tables as before (the second level then overwrites
+//     that entry order in x).
+#ifndef NDFL_BUILD_V2
+#define NDFL_BUILD_V2 1
+#endif
+typedef __attribute__((address_space(3))) uint32_t lu32;
+typedef __attribute__((address_space(3))) uint16_t lu16;
+typedef __attribute__((address_space(3))) uint8_t lu8;
+typedef __attribute__((address_space(3))) u32x4 lu128;
+typedef __attribute__((address_space(3))) Shared LShared;
+#ifdef NDFL_BUILD_PROF                          // (A/B builds: per-section clocks of the build)
+__device__ unsigned long long g_bprof[8192 * 8];      // per wave (block) and section, no contention
+#define BPROF(i) do { const unsigned long long _t = clock64(); if (lane == 0) g_bprof[blockIdx.x * 8 + (i)] += _t - bp_t; bp_t = clock64(); } while (0)
+#else
+#define BPROF(i) do { } while (0)
+#endif
+// GROUP (a dynamic literal/length code): literal pairs joined into the primary entries as group_lits
+// does, from the pulled entries still in registers
+template <bool WS, uint32_t PB, bool GROUP = false>
+__device__ __forceinline__ int build_code_l(LShared* S, uint32_t base, uint32_t n, lu32* prim, lu32* x, uint32_t cap,
+                                            bool is_lit, int lane, lu32* scr) {
+#ifdef NDFL_BUILD_PROF
+    unsigned long long bp_t = clock64();
+#endif
+    constexpr uint32_t PER = (1u << PB) / 64;
+    lu32* CUM = scr;                            // [16] symbols of each length so far (then totals)
+    lu32* O = scr + 16;                         // [16] rank offset per length
+    lu32* F = scr + 32;                         // [16] first code per length
+    lu32* DD = scr + 48;                        // [16] O - F
+    uint32_t mylen[5], rank[5];
+    if (lane < 16) CUM[lane] = 0;
+#pragma unroll
+    for (int q = 0; q < 5; q++) {
+        const uint32_t s = (uint32_t)q * 64 + (uint32_t)lane;
+        const uint32_t l = (s < n) ? S->lens[base + s] : 0u;
+        mylen[q] = l;
+        uint32_t r = 0;
+        if ((uint32_t)q * 64 < n) {
+            uint64_t same = ~0ull;
+#pragma unroll
+            for (int j = 0; j < 4; j++) {
+                const uint64_t bj = __ballot((l >> j) & 1u);
+                same &= ((l >> j) & 1u) ? bj : ~bj;
+            }
+            const uint32_t before = (uint32_t)__builtin_amdgcn_mbcnt_hi((uint32_t)(same >> 32),
+                                    __builtin_amdgcn_mbcnt_lo((uint32_t)same, 0u));
+            if (l) {
+                const uint32_t cb = CUM[l];
+                r = cb + before;
+                if (before == 0) CUM[l] = cb + (uint32_t)__popcll(same);
+            }
+        }
+        rank[q] = r;
+    }
+    wsync();
+    const uint32_t cnt_l = lane < 16 && lane > 0 ? CUM[lane] : 0u;
+    uint32_t c[16];
+    c[0] = 0;
+#pragma unroll
+    for (int l = 1; l < 16; l++) c[l] = (uint32_t)__builtin_amdgcn_readlane((int)cnt_l, l);
+    BPROF(0);
+    {
+        uint32_t num = 0, kraft = 0;
+#pragma unroll
+        for (int l = 1; l < 16; l++) { num += c[l]; kraft += c[l] << (15 - l); }
+        if (!(num >= 2 && kraft == 32768u)) {   // (complete codes pass without the level-wise check)
+            const int err = tree_check(c);
+            if (err) return err;
+        }
+    }
+    // first code and rank offset of each length (lane l writes length l's), left-justified limits
+    uint32_t lj[PB + 1];
+    uint32_t maxl = 0;
+    {
+        uint32_t code = 0, o = 0, myF = 0, myO = 0;
+#pragma unroll
+        for (int l = 1; l < 16; l++) {
+            code = (code + (l > 1 ? c[l - 1] : 0)) << 1;
+            myF = lane == l ? code : myF;
+            myO = lane == l ? o : myO;
+            o += c[l];
+            if ((uint32_t)l <= PB) lj[l] = (code + c[l]) << (PB - (uint32_t)l);
+            maxl = c[l] ? (uint32_t)l : maxl;
+        }
+        if (lane < 16) { F[lane] = myF; O[lane] = myO; DD[lane] = myO - myF; }
+    }
+    wsync();
+    BPROF(1);
+    // every symbol's entry at its canonical position (the slow path's array; the pull's source)
+#pragma unroll
+    for (int q = 0; q < 5; q++) {
+        const uint32_t l = mylen[q];
+        if (l) {
+            const uint32_t s = (uint32_t)q * 64 + (uint32_t)lane;
+            x[O[l] + rank[q]] = is_lit ? lit_entry(s, l) : dist_entry(s, l);
+        }
+    }
+    BPROF(2);
+    bool two = true;
+    if (maxl > PB) {
+        // the longest code under each primary prefix of the long codes (prefix-free with the short
+        // codes, so these entries are free), then the second-level offsets (as build_code)
+#pragma unroll
+        for (uint32_t k = (uint32_t)lane * 4; k < (1u << PB); k += 256) *(lu128*)&prim[k] = u32x4{0u, 0u, 0u, 0u};
+        bsync<WS>();
+#pragma unroll
+        for (int q = 0; q < 5; q++) {
+            const uint32_t l = mylen[q];
+            if (l > PB)
+                __hip_atomic_fetch_max(&prim[rev_bits((F[l] + rank[q]) >> (l - PB), PB)], l, __ATOMIC_RELAXED,
+                                       __HIP_MEMORY_SCOPE_WORKGROUP);
+        }
+        bsync<WS>();
+        uint32_t m[PER];
+#pragma unroll
+        for (uint32_t i = 0; i < PER; i++) m[i] = prim[(uint32_t)lane * PER + i];
+        uint32_t loc = 0;
+#pragma unroll
+        for (uint32_t i = 0; i < PER; i++) loc += m[i] ? 1u << (m[i] - PB) : 0u;
+        uint32_t incl = loc;
+#pragma unroll
+        for (int o = 1; o < 64; o <<= 1) {
+            const uint32_t y = __shfl_up(incl, o, 64);
+            if (lane >= o) incl += y;
+        }
+        two = __shfl(incl, 63, 64) <= cap;
+        uint32_t o = incl - loc;
+#pragma unroll
+        for (uint32_t i = 0; i < PER; i++) {
+            if (m[i]) {
+                prim[(uint32_t)lane * PER + i] = two ? ((o << 16) | ((m[i] - PB) << 5)) : 0u;
+                o += 1u << (m[i] - PB);
+            }
+        }
+    }
+    bsync<WS>();                                // x's canonical entries, the long prefixes
+    BPROF(3);
+    // pull: every primary entry of a code of at most PB bits, all of the lane's at once
+    {
+        uint32_t cv[PER], l[PER], d[PER];
+#pragma unroll
+        for (uint32_t i = 0; i < PER; i++) {
+            cv[i] = rev_bits(i * 64 + (uint32_t)lane, PB);
+            uint32_t li = 1;
+#pragma unroll
+            for (uint32_t L = 1; L < PB; L++) li += cv[i] >= lj[L] ? 1u : 0u;
+            l[i] = li;
+        }
+#pragma unroll
+        for (uint32_t i = 0; i < PER; i++) d[i] = DD[l[i]];
+#pragma unroll
+        for (uint32_t i = 0; i < PER; i++) d[i] = x[d[i] + (cv[i] >> (PB - l[i]))];
+#pragma unroll
+        for (uint32_t i = 0; i < PER; i++)
+            if (cv[i] < lj[PB]) prim[i * 64 + (uint32_t)lane] = d[i];
+        if (GROUP) {
+            // literal pairs (group_lits): an entry whose code is a literal becomes
+            // 1 << 31 | adv | l1 << 4 | pair << 8 | b1 << 9 | b2 << 17 (see there); a long prefix's
+            // entry (length field 0) stays
+            bsync<WS>();
+            uint32_t v[PER];
+#pragma unroll
+            for (uint32_t i = 0; i < PER; i++) {
+                const uint32_t k = i * 64 + (uint32_t)lane, e1 = d[i], l1 = e1 & 31;
+                const bool lit1 = cv[i] < lj[PB] && ((e1 >> 9) & 3) == K_LIT;
+                const uint32_t e2 = lit1 ? prim[k >> l1] : 0u;
+                const uint32_t l2 = e2 & 31, b1 = (e1 >> 16) & 0xFFu;
+                const bool pair = lit1 && l1 < PB && l2 && l1 + l2 <= PB && ((e2 >> 9) & 3) == K_LIT;
+                v[i] = pair ? (1u << 31) | (l1 + l2) | (l1 << 4) | (1u << 8) | (b1 << 9) | (((e2 >> 16) & 0xFFu) << 17)
+                            : (1u << 31) | l1 | (l1 << 4) | (b1 << 9);
+                d[i] = lit1 ? 1u : 0u;
+            }
+            bsync<WS>();
+#pragma unroll
+            for (uint32_t i = 0; i < PER; i++)
+                if (d[i]) prim[i * 64 + (uint32_t)lane] = v[i];
+        }
+    }
+    BPROF(4);
+    if (!two && lane < 16) {
+        // the canonical slow path's limits and per-length first code / offset (u16)
+        lu16* first = (lu16*)(x + n + 16);
+        lu16* offv = first + 16;
+        const uint32_t f = lane ? F[lane] : 0u, o = lane ? O[lane] : 0u;
+        first[lane] = (uint16_t)f;
+        offv[lane] = (uint16_t)o;
+        x[n + lane] = lane ? ((f + cnt_l) << (15 - lane)) : 0u;
+    }
+    if (maxl > PB && two) {
+        bsync<WS>();                            // the pull has read x's canonical entries
+#pragma unroll
+        for (int q = 0; q < 5; q++) {
+            const uint32_t l = mylen[q];
+            if (l <= PB) continue;
+            const uint32_t s = (uint32_t)q * 64 + (uint32_t)lane;
+            const uint32_t ent = is_lit ? lit_entry(s, l) : dist_entry(s, l);
+            const uint32_t code = F[l] + rank[q];
+            const uint32_t pe = prim[rev_bits(code >> (l - PB), PB)];
+            const uint32_t sb = pe >> 16, sd = (pe >> 5) & 15, r = l - PB;
+            for (uint32_t k = rev_bits(code & ((1u << r) - 1u), r); k < (1u << sd); k += (1u << r)) x[sb + k] = ent;
+        }
+    }
+    bsync<WS>();
+    BPROF(5);
+    return 0;
+}
+// The whole build (one call from the decode passes): error or 0 in bits 0..7, empty distance code
+// in bit 8 -- no reference argument, which would put the caller's flag in scratch memory.
+template <bool WS>
+__device__ __noinline__ int build_tables_l(LShared* S, int lane, lu32* scr) {
+    if (S->h_btype == 1) {
+        for (uint32_t s = (uint32_t)lane; s < 320; s += 64) {
+            uint32_t l;
+            if (s < 288) l = s < 144 ? 8 : s < 256 ? 9 : s < 280 ? 7 : 8;
+            else l = 5;
+            S->lens[s] = (uint8_t)l;
+        }
+        bsync<WS>();
+        build_code_l<WS, LB>(S, 0, 288, S->t.lit, S->t.lx, LX, true, lane, scr);
+        build_code_l<WS, DB>(S, 288, 32, S->t.dst, S->t.dx, DX, false, lane, scr);
+        return 0;
+    }
+    const uint32_t numDist = S->h_numdist;
+    int e = build_code_l<WS, LB, true>(S, 0, 288, S->t.lit, S->t.lx, LX, true, lane, scr);
+    if (e) return e;
+    // distance code: empty (one zero length) or one used code padded at index 31 (:398-425)
+    const uint32_t dl = (lane < 32) ? S->lens[288 + lane] : 0u;
+    if (numDist == 1 && S->lens[288] == 0) return 0x100;
+    const uint32_t ones = (uint32_t)__popcll(__ballot(dl == 1)), other = (uint32_t)__popcll(__ballot(dl > 1));
+    bsync<WS>();
+    if (ones == 1 && other == 0 && lane == 0) S->lens[288 + 31] = 1;
+    bsync<WS>();
+    return build_code_l<WS, DB>(S, 288, 32, S->t.dst, S->t.dx, DX, false, lane, scr);
+}
+
+// Tables for the block whose header S.h_* describes.  Returns a Reason (uniform) or 0.  scr: >= 64
+// words of LDS the build may use (the round stage: nothing is staged while a block's tables are built).
 template <bool WS = false>
-__device__ int build_tables(Shared& S, int lane, bool& empty_dist) {
+__device__ __forceinline__ int build_tables(Shared& S, int lane, bool& empty_dist, uint32_t* scr) {
+#if NDFL_BUILD_V2
+    const int r = build_tables_l<WS>((LShared*)&S, lane, (lu32*)scr);
+    empty_dist = (r & 0x100) != 0;
+    return r & 0xFF;
+#else
+    (void)scr;
     empty_dist = false;
     if (S.h_btype == 1) {
         fixed_lens(S, lane);
@@ -783,6 +1046,7 @@ __device__ int build_tables(Shared& S, int lane, bool& empty_dist) {
     if (ones == 1 && other == 0 && lane == 0) S.lens[288 + 31] = 1;
     bsync<WS>();
     return build_code<WS>(S, 288, 32, S.t.dst, DB, S.t.dx, DX, false, lane);
+#endif
 }
 
 // ---- segmented speculative decode of one round ------------------------------------------------
@@ -1648,7 +1912,7 @@ ndfl_inflate_count_wave_kernel(const uint32_t* w, uint64_t nwords, uint64_t nbit
         }
         bool ed;
         if (pc) { const uint64_t x = wall_clock64(); pc->hdr += x - tb; tb = x; }
-        const int te = build_tables(S, lane, ed);
+        const int te = build_tables(S, lane, ed, stg.w);
         if (te) { status = ST_ERROR; reason = (uint32_t)te; endpos = d0; break; }
         // literal/length codes mostly of one length 8 resynchronise rarely: phase-mapped rounds
         bool phased = false;
@@ -1877,7 +2141,7 @@ ndfl_inflate_emit_wave_kernel(const uint32_t* w, uint64_t nwords, uint64_t nbits
         if (btr) {
             ed = S.h_len != 0;                  // (the loaded record's empty-distance flag)
         } else {
-            const int te = build_tables(S, lane, ed);
+            const int te = build_tables(S, lane, ed, stg.w);
             if (te) { status = ST_ERROR; reason = (uint32_t)te; endpos = d0; break; }
         }
         uint64_t rs = d0;

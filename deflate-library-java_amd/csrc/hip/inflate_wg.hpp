@@ -395,7 +395,7 @@ ndfl_inflate_count_wg_kernel(const uint32_t* w, uint64_t nwords, uint64_t nbits,
         // wave 0 builds the block's tables alone (wave synchronisation), the others wait
         if (wave == 0) {
             bool ed0;
-            const int te0 = build_tables<true>(S, lane, ed0);
+            const int te0 = build_tables<true>(S, lane, ed0, stg[0].w);
             if (lane == 0) { X.b32[1] = (uint32_t)te0; X.b32[2] = ed0 ? 1u : 0u; }
         }
         __syncthreads();

@@ -3,9 +3,10 @@
 # shards), the default bench line, and the FETCH_SIZE / WRITE_SIZE calibration on known byte counts.
 cd "$GRAFT_REPO_ROOT"
 mkdir -p gpurun_out/r06a
-PYTEST_ARGS="-k reserved_symbol_in_the_message or tail_map_composes or small_shards_one_gpu or known_answer" \
-  SKIP_BENCH=1 bash scripts/gpu_tests.sh || exit 1
-cp gpurun_out/pytest_gpu.log gpurun_out/r06a/pytest_new.log
+timeout -k 10 600 python -u -m pytest tests -m gpu -x -v --timeout 300 --timeout-method thread \
+  -k "reserved_symbol_in_the_message or tail_map_composes or small_shards_one_gpu or known_answer" \
+  > gpurun_out/r06a/pytest_new.log 2>&1 || { tail -40 gpurun_out/r06a/pytest_new.log; exit 1; }
+tail -3 gpurun_out/r06a/pytest_new.log
 timeout -k 10 400 python -u bench.py > gpurun_out/r06a/bench.log 2>&1 || { tail -30 gpurun_out/r06a/bench.log; exit 1; }
 tail -1 gpurun_out/r06a/bench.log
 cd /tmp && export TMPDIR=/tmp

@@ -1,26 +1,36 @@
 """Per-launch HBM traffic of each ndfl kernel from two rocprofv3 --pmc passes (FETCH_SIZE, WRITE_SIZE),
-corrected as /opt/skills/guides/MI355X_MICROARCH.md (HBM/rocprofv3) prescribes:
+corrected as calibrated on gfx950 (profiles/r06_fetch_calib.txt, scripts/r06/fetch_calib.hip: kernels
+that move a known 2 GiB past the Infinity Cache in one access shape each):
   * FETCH_SIZE / WRITE_SIZE are in KiB per dispatch;
-  * gfx950 FETCH_SIZE reports 1/2 of the bytes of a wide (16 B/lane) coalesced streaming read -> x2 for
-    the kernels whose input side is such a read (deflate_chunks: 16-B loads of the raw bytes);
-  * WRITE_SIZE is exact for 16-B-per-lane streaming stores; other widths are uncalibrated (noted).
+  * FETCH_SIZE reports exactly 1/2 of the bytes of a coalesced streaming read in every shape the ndfl
+    kernels use -- 4-B/lane dword loads, 16-B/lane loads and LDS-DMA dword loads (one 256-B row per
+    wave instruction) alike -> x2 for every kernel whose reads are such rows (all of the decoder's
+    full-stream passes: finder ld4 groups, round staging by LDS-DMA, record and table loads);
+  * WRITE_SIZE is exact for coalesced 4-B and 16-B stores; 16-B stores from 64 scattered lane cursors
+    (the emit pass's output) read 2.8-2.9x the bytes written (partial lines leave L2): reported as
+    measured, with that note.
 Usage: python scripts/traffic_summary.py FETCH.csv WRITE.csv OUT.json"""
 import collections
 import csv
 import json
 import sys
 
-WIDE_READ = {"ndfl_deflate_chunks_kernel": True}
+# FETCH_SIZE correction per kernel (all calibrated shapes read at 1/2)
+FETCH_CORR = collections.defaultdict(lambda: 2.0)
 NOTES = {
-    "ndfl_deflate_chunks_kernel": "16-B/lane streaming loads (x2 applied) and 16-B/lane interior stores: calibrated",
-    "ndfl_deflate_hist_kernel": "raw: the chunk arrives partly through the previous generation's L2 touch (1-B "
-                                "loads, one per 128-B line: counted in full) and partly through 16-B/lane loads "
-                                "(counted half), so no single correction applies; raw = N (0.5 + 0.5 p) gives the "
-                                "touched share p, and the actual fetch is about N; writes: 1.25 KiB per chunk",
-    "ndfl_deflate_emit_kernel": "raw, as for hist (L2 touch + 16-B/lane loads; the 4-B code-record loads add "
-                                "~1.7 KiB per chunk); 4-B/lane coalesced interior stores",
-    "ndfl_inflate_emit_wave_kernel": "reads are 16-B prefetch per chain (uncalibrated, raw); stores are 4-B per lane "
-                                     "at 64 independent chain cursors: partial lines leave L2 before they fill",
+    "ndfl_deflate_hist_kernel": "16-B/lane loads of the chunk (x2) plus the L2 touch of the next generation's "
+                                "chunk (one byte per 128-B line; those lines are then read from L2 by the next "
+                                "workgroup, so the pair counts each line about once); writes: 1.25 KiB per chunk",
+    "ndfl_deflate_emit_kernel": "as hist: 16-B/lane chunk loads (x2) + the L2 touch; 4-B code-record loads; "
+                                "coalesced 4-B interior stores (exact)",
+    "ndfl_inflate_find_compact_kernel": "16-B/lane row loads of the stream (x2)",
+    "ndfl_inflate_strict_kernel": "16-B/lane window loads of the survivors' bits (x2; gathered rows)",
+    "ndfl_inflate_count_wave_kernel": "LDS-DMA dword rows of each round (x2), header records, candidate cursor; "
+                                      "writes: segment records, table records, per-wave phase slots, scratch spills",
+    "ndfl_inflate_emit_fast_kernel": "LDS-DMA dword rows of each round (x2), segment and table records (x2); writes "
+                                     "are 16-B stores at 64 lane cursors: WRITE_SIZE 2.8-2.9x the bytes by "
+                                     "calibration (profiles/r06_fetch_calib.txt), reported as measured",
+    "ndfl_inflate_emit_wave_kernel": "as emit_fast; stores at 64 lane cursors (WRITE_SIZE above the bytes written)",
 }
 
 
@@ -44,7 +54,7 @@ def main():
         w, nw = write.get(k, (0.0, 1))
         fb = f * 1024 / max(nf, 1)
         wb = w * 1024 / max(nw, 1)
-        corr = 2.0 if WIDE_READ.get(k) else 1.0
+        corr = FETCH_CORR[k]
         out[k] = {"launches": nf, "fetch_bytes_raw": round(fb), "fetch_bytes": round(fb * corr),
                   "fetch_correction": corr, "write_bytes": round(wb), "traffic_bytes": round(fb * corr + wb),
                   "note": NOTES.get(k, "")}

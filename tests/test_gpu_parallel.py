@@ -161,7 +161,7 @@ def test_tail_map_composes_to_tail_and_resolved_output(env, seed, a, strategy):
     for k in range(6):
         parts.append(mixed_bytes(30000, seed=seed * 10 + k))
         parts.append(bytes([rng.getrandbits(8)]) * rng.randint(100, 30000))
-    data = b"".join(parts)
+    data = (b"".join(parts) * 3)[:7 * 65536]
     chunk = 16384 if a == 1 else 65536
     comp, seams = _stream_and_seams(data, strategy, chunk)
     pre = a * chunk
