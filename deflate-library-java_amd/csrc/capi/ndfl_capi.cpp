@@ -996,6 +996,7 @@ static int public_reason(ndfl_ctx* c, int r) {
         case inf::R_RESERVED_LEN_HI: c->err_sym = 287; r = inf::R_RESERVED_LEN; break;
         case inf::R_RESERVED_DIST: c->err_sym = 30; break;
         case inf::R_RESERVED_DIST_HI: c->err_sym = 31; r = inf::R_RESERVED_DIST; break;
+        case inf::R_INTERNAL: r = NDFL_E_INTERNAL; break;   // (a failed consistency check, not the data)
         default: break;
     }
     return r;

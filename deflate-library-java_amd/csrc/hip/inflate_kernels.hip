@@ -1593,6 +1593,14 @@ static int inflate_devlink(InflateScratch& S, hipStream_t s, const uint32_t* d_w
     INF_CHK(hipMemsetAsync(S.d_pend, 0, npw * 4 + 64, s));
     if (!S.d_ticket) INF_CHK(hipMalloc(&S.d_ticket, 64));
     INF_CHK(hipMemsetAsync(S.d_ticket, 0, 64, s));
+    if (S.knobs.test_segflip && S.pool.cnt) {         // (test: record 0, lane 0 counts one byte more)
+        uint32_t c0 = 0;
+        INF_CHK(hipMemcpyAsync(&c0, S.pool.cnt, 4, hipMemcpyDeviceToHost, s));
+        INF_CHK(hipStreamSynchronize(s));
+        c0++;
+        INF_CHK(hipMemcpyAsync(S.pool.cnt, &c0, 4, hipMemcpyHostToDevice, s));
+        INF_CHK(hipStreamSynchronize(s));
+    }
     INF_CHK(hipEventRecord(S.ev[4], s));
     static const uint32_t emit_grid = wave_grid(ndfl_inflate_emit_wave_kernel, EMIT_WAVES, "NDFL_EMIT_WPC");
     // the record-replay emit kernel first, the full one over what it leaves (NDFL_EMIT_FAST=0: the

@@ -2264,6 +2264,10 @@ ndfl_inflate_emit_wave_kernel(const uint32_t* w, uint64_t nwords, uint64_t nbits
                 wr.dst = dst0 + n;
             }
             wr_flush_exact(wr, gout);
+            // the segment, checked: the write pass lands on the next lane's segment
+            // start having produced exactly the bytes the count pass's record (or this round's
+            // decode) counts
+            if (live && kind != T_ERR && (n != mycnt || pos != end)) { kind = T_ERR; rsn = R_INTERNAL; }
             // the first lane (in stream order) that ended with an error decides
             const uint64_t em = __ballot(live && kind == T_ERR);
             if (em) {
@@ -2535,6 +2539,9 @@ ndfl_inflate_emit_fast_kernel(const uint32_t* w, uint64_t nwords, uint64_t nbits
             };
             if (ph8) token_loop(std::true_type{}); else token_loop(std::false_type{});
             wr_flush_exact(wr, gout);
+            // the count pass's record, checked: the lane's replay lands on the next
+            // lane's segment start having produced exactly the bytes the record counts
+            if (live && kind != T_ERR && (n != rcnt || pos != end)) { kind = T_ERR; rsn = R_INTERNAL; }
             const uint64_t em = __ballot(live && kind == T_ERR);
             if (em) {
                 const int fl = (int)__builtin_ctzll(em);

@@ -9,7 +9,7 @@
 
 // Switches of a context, read once from the environment when the context is created
 // (ndfl_ctx_create).  None is needed in production: they select the decoder's hand-over paths for
-// the tests (EMIT_FAST, NO_BT, NO_ALIAS, COUNT_W), statistics for profiling (STATS, HOST_TIMES,
+// the tests (EMIT_FAST, NO_BT, NO_ALIAS, COUNT_W, TEST_SEGFLIP), statistics for profiling (STATS, HOST_TIMES,
 // LZ_STATS), and the few A/B alternatives still measured against the defaults.
 struct Knobs {
     bool stats = false;          // NDFL_STATS: per-pass counters and phase clocks to stderr
@@ -26,6 +26,8 @@ struct Knobs {
     bool lz_stats = false;       // NDFL_LZ_STATS
     bool lz_chain = false;       // NDFL_LZ_SEARCH=chain: the round-3 hash-chain LZ77 search
     int lz_lead = -1;            // NDFL_LZ_LEAD: parse-driven search lead-in (-1: default)
+    bool test_segflip = false;   // NDFL_TEST_SEGFLIP: one count-pass record's byte count perturbed
+                                 //   before the emit pass (the emit-side check must fail the decode)
     void read() {
         auto on = [](const char* n) { const char* e = getenv(n); return e && strcmp(e, "0") != 0; };
         auto num = [](const char* n, int dflt) { const char* e = getenv(n); return e ? atoi(e) : dflt; };
@@ -40,15 +42,16 @@ struct Knobs {
         const char* se = getenv("NDFL_LZ_SEARCH");
         lz_chain = se && !strcmp(se, "chain");
         lz_lead = num("NDFL_LZ_LEAD", -1);
+        test_segflip = on("NDFL_TEST_SEGFLIP");
     }
     // the effective switches, one line (printed by ndfl_ctx_create when stats are on)
     void print(FILE* f) const {
         fprintf(f, "[ndfl] context knobs: stats=%d host_times=%d host_link=%d no_hdrrec=%d emit_fast=%d no_bt=%d "
                    "no_alias=%d count_w=%u deflate_pf=%d deflate_profile=%d deflate_fused=%d lz_stats=%d "
-                   "lz_search=%s lz_lead=%d\n",
+                   "lz_search=%s lz_lead=%d test_segflip=%d\n",
                 (int)stats, (int)host_times, (int)host_link, (int)no_hdrrec, (int)emit_fast, (int)no_bt,
                 (int)no_alias, count_w, (int)deflate_pf, (int)deflate_profile, (int)deflate_fused, (int)lz_stats,
-                lz_chain ? "chain" : "parse", lz_lead);
+                lz_chain ? "chain" : "parse", lz_lead, (int)test_segflip);
     }
 };
 

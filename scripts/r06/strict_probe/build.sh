@@ -10,6 +10,9 @@ cd "$(dirname "$0")"
 rm -rf r4 && mkdir r4
 git -C ../../.. archive a5b0dbe~1 deflate-library-java_amd/csrc deflate-library-java_amd/python include | tar x -C r4
 (cd r4 && patch -p0 -s < ../strict_probe.patch)
+# NDFL_STRICT_GRID: the strict kernel's grid (workgroups of 256), to run it at a chosen concurrency
+sed -i 's/static const uint32_t strict_grid = \[\] {/static const uint32_t strict_grid = [] { if (const char* g = getenv("NDFL_STRICT_GRID")) return (uint32_t)atoi(g);/' \
+    r4/deflate-library-java_amd/csrc/hip/inflate_kernels.hip
 cd r4/deflate-library-java_amd && mkdir -p lib
 SRC=csrc/capi/ndfl_capi.cpp
 H="/opt/rocm/bin/hipcc -O3 -std=c++17 --offload-arch=gfx950 -fPIC -w -x hip -shared"

@@ -113,3 +113,22 @@ def test_emit_modes_first_error(ctx, name):
         k = int(rng.integers(len(bad) // 8, len(bad)))
         bad[k] ^= 0x5A
         _same(ctx, bytes(bad))
+
+
+@pytest.mark.parametrize("emit_fast", ["1", "0"])
+def test_count_record_check_fails_loudly(emit_fast):
+    """both emit kernels check every lane's segment against the count pass's record
+    (the replay lands on the next segment's start having produced exactly the counted bytes).  With
+    one record's byte count perturbed (NDFL_TEST_SEGFLIP) the decode must fail with NDFL_E_INTERNAL,
+    not return wrong bytes or a data-format Reason."""
+    import ndfl
+    from ndfl import _lib
+    olds = {k: _env(k, v) for k, v in {"NDFL_TEST_SEGFLIP": "1", "NDFL_EMIT_FAST": emit_fast}.items()}
+    try:
+        c = ndfl.Context(0)
+    finally:
+        for k, v in olds.items():
+            _env(k, v)
+    with pytest.raises(_lib.NdflError) as ei:
+        c.inflate(_streams()["rle_c4"])
+    assert ei.value.code == _lib.E_INTERNAL
