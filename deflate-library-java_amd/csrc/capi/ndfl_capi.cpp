@@ -191,10 +191,11 @@ double ndfl_ctx_last_kernel_ms(ndfl_ctx* c) { return c ? c->last_ms : 0.0; }
 
 int ndfl_ctx_timings(ndfl_ctx* c, double* ms, int n) {
     if (!c || !ms) return NDFL_E_ARG;
-    double v[8] = {c->deflate_ms, c->inf.last_ms_find, c->inf.last_ms_count, c->inf.last_ms_emit,
-                   c->inf.last_ms_wall, (double)c->inf.chains, (double)c->inf.repairs, (double)c->inf.candidates};
-    for (int i = 0; i < n && i < 8; i++) ms[i] = v[i];
-    return n < 8 ? n : 8;
+    double v[9] = {c->deflate_ms, c->inf.last_ms_find, c->inf.last_ms_count, c->inf.last_ms_emit,
+                   c->inf.last_ms_wall, (double)c->inf.chains, (double)c->inf.repairs, (double)c->inf.candidates,
+                   (double)c->inf.flat_chains};
+    for (int i = 0; i < n && i < 9; i++) ms[i] = v[i];
+    return n < 9 ? n : 9;
 }
 
 uint64_t ndfl_deflate_bound(uint64_t len, uint32_t chunk_len) {

@@ -820,7 +820,7 @@ struct EmitChain {
 // ---- device-side candidate list and chain linking (one host synchronization per decode) ----------
 // Link summary (DevLink::info, u64): the decode's results the host reads once at the end.
 enum : uint32_t { LI_NCAND = 0, LI_NCH, LI_TOTAL, LI_FLAGS, LI_STOP, LI_CODE, LI_OUTLEN, LI_CONSUMED, LI_NCAND_ALL,
-                  LI_LO, LI_NREP, LI_WORDS = 16 };
+                  LI_LO, LI_NREP, LI_NFLAT, LI_WORDS = 16 };
 enum : uint64_t { LF_REPAIR = 1, LF_RANGE = 2, LF_CAPACITY = 4 };
 constexpr uint32_t NOLINK = 0xFFFFFFFFu;
 
@@ -964,23 +964,26 @@ __device__ __forceinline__ void border_place(Bk bk, uint32_t n, uint32_t* ob, ui
 // (ndfl_inflate_alias_mark_kernel), stored-header aliases are left out of the order (*nord = the
 // chains to count).  grid = tiles of n.
 struct OrderBucket {
-    const uint64_t* cands; uint32_t n; uint64_t end_bit; const uint32_t* rep;
+    const uint64_t* cands; uint32_t n; uint64_t end_bit; const uint32_t* rep; const uint32_t* flat;
     __device__ __forceinline__ uint32_t operator()(uint32_t k) const {
         const uint64_t c0 = cands[k], c1 = cands[min(k + 1, n - 1)];
         const uint32_t r = rep ? rep[k] : k;
         const uint64_t nx = k + 1 < n ? c1 : end_bit;
         const uint64_t len = nx > c0 ? nx - c0 : 0;
+        if (flat && flat[k]) return OB_NB;      // (counted in flat groups)
         return r == k ? OB_NB - 1 - (uint32_t)min<uint64_t>(OB_NB - 1, len >> 15) : OB_NB;
     }
 };
+// flat: per candidate, nonzero for a chain counted in a flat group (ndfl_inflate_hdr_kernel), or null
 extern "C" __global__ void __launch_bounds__(SCAN_T)
-ndfl_inflate_order_count_kernel(const uint64_t* cands, uint32_t n, uint64_t end_bit, const uint32_t* rep, uint32_t* ob) {
-    border_count(OrderBucket{cands, n, end_bit, rep}, n, ob);
+ndfl_inflate_order_count_kernel(const uint64_t* cands, uint32_t n, uint64_t end_bit, const uint32_t* rep, uint32_t* ob,
+                                const uint32_t* flat) {
+    border_count(OrderBucket{cands, n, end_bit, rep, flat}, n, ob);
 }
 extern "C" __global__ void __launch_bounds__(SCAN_T)
 ndfl_inflate_order_kernel(const uint64_t* cands, uint32_t n, uint64_t end_bit, uint32_t* order, const uint32_t* rep,
-                          uint32_t* nord, uint32_t* ob) {
-    border_place(OrderBucket{cands, n, end_bit, rep}, n, ob, order, nord);
+                          uint32_t* nord, uint32_t* ob, const uint32_t* flat) {
+    border_place(OrderBucket{cands, n, end_bit, rep, flat}, n, ob, order, nord);
 }
 
 // The emit pass's claim order over the linked chain list (info[LI_NCH] chains): costliest first, by
@@ -1178,7 +1181,7 @@ struct InflateScratch {
     bool q_full = false;                              //   the last scan's list could not grow (budget, allocation)
     double last_ms_find = 0, last_ms_count = 0, last_ms_emit = 0, last_ms_wall = 0;
     hipEvent_t ev[6] = {nullptr, nullptr, nullptr, nullptr, nullptr, nullptr};
-    uint64_t repairs = 0, chains = 0, candidates = 0, resolved_groups = 0;
+    uint64_t repairs = 0, chains = 0, candidates = 0, resolved_groups = 0, flat_chains = 0;
     void* h_cnt = nullptr;                            // pinned: resolve list size
     void* d_info = nullptr;                           // device-side linking: summary (LI_*)
     void* h_info = nullptr;                           //   and its pinned host copy
@@ -1458,31 +1461,44 @@ static int inflate_devlink(InflateScratch& S, hipStream_t s, const uint32_t* d_w
     if (!S.d_cticket) INF_CHK(hipMalloc(&S.d_cticket, CTK_BYTES));
     INF_CHK(hipMemsetAsync(S.d_cticket, 0, CTK_BYTES, s));
     uint32_t* d_nord = (uint32_t*)S.d_cticket + 8;
+    uint32_t* d_nflat = (uint32_t*)S.d_cticket + 4;
     uint32_t* d_ob = (uint32_t*)S.d_cticket + 16;                      // count order: tot, cursor
     const uint32_t otiles = (ncand + SCAN_TILE - 1) / SCAN_TILE;
-    hipLaunchKernelGGL(ndfl_inflate_order_count_kernel, dim3(otiles), dim3(SCAN_T), 0, s, (const uint64_t*)S.d_cands,
-                       ncand, end_bit, (const uint32_t*)d_rep, d_ob);
-    INF_CHK(hipGetLastError());
-    hipLaunchKernelGGL(ndfl_inflate_order_kernel, dim3(otiles), dim3(SCAN_T), 0, s, (const uint64_t*)S.d_cands, ncand,
-                       end_bit, d_order, (const uint32_t*)d_rep, alias_on ? d_nord : (uint32_t*)nullptr, d_ob);
-    INF_CHK(hipGetLastError());
     if (!S.d_ph) INF_CHK(hipMalloc(&S.d_ph, (size_t)std::max(COUNT_WAVES, EMIT_WAVES) * sizeof(wv::PhArr)));
     const bool stats_on = S.knobs.stats;
     const uint64_t limit = std::min(end_bit, nbits);
     INF_CHK(hipEventRecord(S.ev[2], s));
+    // header records, and the chains whose first block is counted by one lane (flat groups: the
+    // one-wave count kernel only); those leave the count order
     const bool hrec_on = !S.knobs.no_hdrrec;
+    const bool flat_on = hrec_on && W == 1 && S.knobs.flat;
+    uint32_t* d_flist = nullptr;
+    uint32_t* d_fflag = nullptr;
     if (hrec_on) {
-        INF_CHK(inf_ensure(&S.d_hrec, &S.d_hrec_cap, (size_t)ncand * sizeof(wv::HdrRec)));
+        INF_CHK(inf_ensure(&S.d_hrec, &S.d_hrec_cap, (size_t)ncand * (sizeof(wv::HdrRec) + 8) + 64));
+        d_flist = (uint32_t*)((char*)S.d_hrec + (size_t)ncand * sizeof(wv::HdrRec));
+        d_fflag = d_flist + ncand;
         hipLaunchKernelGGL(ndfl_inflate_hdr_kernel, dim3((ncand + 63) / 64), dim3(64), 0, s, d_w, nwords, nbits,
-                           (const uint64_t*)S.d_cands, ncand, (wv::HdrRec*)S.d_hrec);
+                           (const uint64_t*)S.d_cands, ncand, (wv::HdrRec*)S.d_hrec, flat_on ? d_flist : nullptr,
+                           d_nflat, flat_on ? d_fflag : nullptr);
         INF_CHK(hipGetLastError());
     }
+    hipLaunchKernelGGL(ndfl_inflate_order_count_kernel, dim3(otiles), dim3(SCAN_T), 0, s, (const uint64_t*)S.d_cands,
+                       ncand, end_bit, (const uint32_t*)d_rep, d_ob, flat_on ? (const uint32_t*)d_fflag : nullptr);
+    INF_CHK(hipGetLastError());
+    hipLaunchKernelGGL(ndfl_inflate_order_kernel, dim3(otiles), dim3(SCAN_T), 0, s, (const uint64_t*)S.d_cands, ncand,
+                       end_bit, d_order, (const uint32_t*)d_rep, (alias_on || flat_on) ? d_nord : (uint32_t*)nullptr, d_ob,
+                       flat_on ? (const uint32_t*)d_fflag : nullptr);
+    INF_CHK(hipGetLastError());
+    if (flat_on) INF_CHK(hipMemcpyAsync(info + LI_NFLAT, d_nflat, 4, hipMemcpyDeviceToDevice, s));
     launch_count(s, W, ncand,
                        d_w, nwords, nbits, (const uint64_t*)S.d_cands, (const uint64_t*)nullptr, ncand,
                        (const uint64_t*)S.d_cands, ncand, limit, (ChainRes*)S.d_res,
                        stats_on ? (uint32_t*)S.d_stats : nullptr, (uint64_t)0, S.pool, (uint32_t*)S.d_cticket,
                        (wv::PhArr*)S.d_ph, (const uint32_t*)d_order, end_bit,
-                       hrec_on ? (const wv::HdrRec*)S.d_hrec : nullptr, alias_on ? (const uint32_t*)d_nord : nullptr);
+                       hrec_on ? (const wv::HdrRec*)S.d_hrec : nullptr,
+                       (alias_on || flat_on) ? (const uint32_t*)d_nord : nullptr, flat_on ? (const uint32_t*)d_flist : nullptr,
+                       flat_on ? (const uint32_t*)d_nflat : nullptr);
     INF_CHK(hipGetLastError());
     if (alias_on) {
         hipLaunchKernelGGL(ndfl_inflate_alias_copy_kernel, dim3(std::min<uint32_t>(1024, (ncand + 255) / 256)), dim3(256), 0, s,
@@ -1498,6 +1514,19 @@ static int inflate_devlink(InflateScratch& S, hipStream_t s, const uint32_t* d_w
         for (uint32_t k = 0; k < ncand; k++) {
             const uint32_t st = std::min<uint32_t>(cr[k].status, 2u), t = cr[k].pad >> 16;
             cnt[st]++; tsum[st] += t; tmax[st] = std::max<uint64_t>(tmax[st], t); blk[st] += cr[k].pad & 0xFFFFu;
+        }
+        if (flat_on) {
+            uint32_t fw[4] = {0, 0, 0, 0};
+            INF_CHK(hipMemcpy(fw, (uint32_t*)S.d_cticket + 4, 16, hipMemcpyDeviceToHost));
+            const unsigned long long gt = (unsigned long long)fw[2] | ((unsigned long long)fw[3] << 32);
+            fprintf(stderr, "[ndfl] count flat groups: %u chains in %u groups, %u sent back to the wave decode, "
+                    "group wave time %.3f ms mean\n", fw[0], (fw[0] + 63) / 64, fw[1], fw[0] ? gt * 1e-5 / ((fw[0] + 63) / 64) : 0.0);
+#ifdef NDFL_FLAT_PROF
+            unsigned long long fpv[4] = {0, 0, 0, 0}, z[4] = {0, 0, 0, 0};
+            INF_CHK(hipMemcpyFromSymbol(fpv, HIP_SYMBOL(wv::g_flat_prof), 32));
+            INF_CHK(hipMemcpyToSymbol(HIP_SYMBOL(wv::g_flat_prof), z, 32));
+            fprintf(stderr, "[ndfl] flat decode loops (lane 0, clock64): %llu cycles, %llu at %llu phase points\n", fpv[0], fpv[1], fpv[2]);
+#endif
         }
         const char* nm[3] = {"boundary", "final", "error"};
         for (int k = 0; k < 3; k++)
@@ -1678,6 +1707,7 @@ static int inflate_devlink(InflateScratch& S, hipStream_t s, const uint32_t* d_w
     if (lflags & LF_RANGE) return -1;                          // the range end is no block boundary
     S.chains = hinfo[LI_NCH];
     S.candidates = ncand;
+    S.flat_chains = hinfo[LI_NFLAT];
     S.repairs = 0;
     if (lflags & LF_CAPACITY) { *out_len = hinfo[LI_TOTAL]; return -3; }
     const uint32_t pending_left = (uint32_t)(hinfo[LI_WORDS - 1] & 0xFFFFFFFFu);
@@ -1978,7 +2008,8 @@ refind:
                            (const uint64_t*)S.d_starts, (const uint64_t*)S.d_stops, (uint32_t)n,
                            (const uint64_t*)S.d_cands, ncand, limit, (ChainRes*)S.d_res, stats_on ? (uint32_t*)S.d_stats : nullptr,
                            slot_base, pool, (uint32_t*)S.d_cticket, (wv::PhArr*)S.d_ph, (const uint32_t*)d_order,
-                           end_bit, (const wv::HdrRec*)nullptr, (const uint32_t*)nullptr);
+                           end_bit, (const wv::HdrRec*)nullptr, (const uint32_t*)nullptr, (const uint32_t*)nullptr,
+                           (const uint32_t*)nullptr);
         INF_CHK(hipGetLastError());
         if (S.count_first) { INF_CHK(hipEventRecord(S.ev[3], s)); S.count_first = false; }
         r.resize(n);
@@ -2097,6 +2128,7 @@ refind:
         S.repairs++;
     }
     S.chains = chains.size();
+    S.flat_chains = 0;
     S.candidates = sorted_cand.size();
     if (S.knobs.stats) {
         uint32_t st[64] = {0};

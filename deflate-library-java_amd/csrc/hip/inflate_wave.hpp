@@ -574,6 +574,8 @@ struct HdrRec {
     uint32_t lens[80];                       // S.lens as words
     Hdr h;
     uint64_t at;                             // the candidate's bit position
+    uint32_t flat;                           // escape-prefix literal code (count_flat_group): k + 1, else 0
+    uint32_t pad;
 };
 
 // Synchronisation of the table build: the whole workgroup (WS = false: the one-wave kernels), or
@@ -990,6 +992,8 @@ __device__ __forceinline__ int build_code_l(LShared* S, uint32_t base, uint32_t 
 // in bit 8 -- no reference argument, which would put the caller's flag in scratch memory.
 template <bool WS>
 __device__ __noinline__ int build_tables_l(LShared* S, int lane, lu32* scr) {
+    // (one literal/length build for both block types: fixed codes of 7..9 bits form no pairs in a
+    // 10-bit primary, and the function's code stays one build long)
     if (S->h_btype == 1) {
         for (uint32_t s = (uint32_t)lane; s < 320; s += 64) {
             uint32_t l;
@@ -998,16 +1002,14 @@ __device__ __noinline__ int build_tables_l(LShared* S, int lane, lu32* scr) {
             S->lens[s] = (uint8_t)l;
         }
         bsync<WS>();
-        build_code_l<WS, LB>(S, 0, 288, S->t.lit, S->t.lx, LX, true, lane, scr);
-        build_code_l<WS, DB>(S, 288, 32, S->t.dst, S->t.dx, DX, false, lane, scr);
-        return 0;
     }
-    const uint32_t numDist = S->h_numdist;
-    int e = build_code_l<WS, LB, true>(S, 0, 288, S->t.lit, S->t.lx, LX, true, lane, scr);
+    const int e = build_code_l<WS, LB, true>(S, 0, 288, S->t.lit, S->t.lx, LX, true, lane, scr);
     if (e) return e;
-    // distance code: empty (one zero length) or one used code padded at index 31 (:398-425)
+    // distance code: empty (one zero length) or one used code padded at index 31 (:398-425); fixed
+    // blocks' 32 lengths of 5 take neither branch
+    const uint32_t numDist = S->h_numdist;
     const uint32_t dl = (lane < 32) ? S->lens[288 + lane] : 0u;
-    if (numDist == 1 && S->lens[288] == 0) return 0x100;
+    if (S->h_btype != 1 && numDist == 1 && S->lens[288] == 0) return 0x100;
     const uint32_t ones = (uint32_t)__popcll(__ballot(dl == 1)), other = (uint32_t)__popcll(__ballot(dl > 1));
     bsync<WS>();
     if (ones == 1 && other == 0 && lane == 0) S->lens[288 + 31] = 1;
@@ -1320,6 +1322,9 @@ __device__ void round_decode(const In& in, const Tabs& t, bool ed, uint64_t rs, 
 #ifndef NDFL_PHASE_JUMP
 #define NDFL_PHASE_JUMP 1      // phase runs step four 8-bit literals at once where they can
 #endif
+#ifndef NDFL_PHASE_ESC
+#define NDFL_PHASE_ESC 1       // escape-prefix literal blocks: phase runs step to the next escape byte
+#endif
 #ifndef NDFL_PHASE_GROUP
 #define NDFL_PHASE_GROUP 2     // phase runs decoded together (1, 2, 4 or 8; round 3, one token a step:
 #endif                         // 1: 14.6, 2: 13.9, 4: 12.9, 8: 12.8 ms count pass; round 5, four 8-bit
@@ -1450,6 +1455,73 @@ __device__ __forceinline__ void phase_multi(const Lv& v, const Tabs& t, bool ed,
     }
 }
 
+// Escape-prefix literal blocks (what encoders make of incompressible data: 255 literals of 8 bits --
+// or 254, 252 -- with every longer code under the remaining all-ones (8 - k)-bit prefix): a run
+// steps up to 8 tokens at once, to the first byte at its alignment that starts with the prefix
+// (a byte-wise zero test on the 64-bit window), and decodes that one through the full token decoder.
+// Same results as phase_run.  esc4: the prefix mask repeated in the 4 bytes (flat8_mask).
+__device__ __forceinline__ uint32_t esc_index(uint32_t lo, uint32_t hi, uint32_t esc4) {
+    const uint32_t tl = (lo & esc4) ^ esc4, th = (hi & esc4) ^ esc4;
+    const uint32_t zl = (tl - 0x01010101u) & ~tl & 0x80808080u, zh = (th - 0x01010101u) & ~th & 0x80808080u;
+    return zl ? (uint32_t)__builtin_ctz(zl) >> 3 : zh ? 4u + ((uint32_t)__builtin_ctz(zh) >> 3) : 8u;
+}
+template <int N>
+__device__ __forceinline__ void phase_multi_esc(const Lv& v, const Tabs& t, bool ed, uint32_t nb, uint32_t s0, uint32_t e,
+                                                uint32_t esc4, PhOut (&O)[N]) {
+    uint32_t p[N], c[N];
+    bool l[N];
+#pragma unroll
+    for (int k = 0; k < N; k++) phase_first(v, t, ed, nb, s0 + k, e, p[k], c[k], O[k], l[k]);
+    for (;;) {
+        bool f[N], any = false;
+#pragma unroll
+        for (int k = 0; k < N; k++) { f[k] = l[k] && p[k] < e; any = any || f[k]; }
+        if (!any) break;
+        uint32_t lo[N], hi[N];
+#pragma unroll
+        for (int k = 0; k < N; k++) {
+            const uint32_t pp = f[k] ? p[k] : p[0];
+            const uint32_t* qk = v.p + ((pp >> 5) - v.rw) * 64;
+            const uint32_t a = qk[0], wb = qk[64], cw = qk[128];
+            lo[k] = __builtin_amdgcn_alignbit(wb, a, pp & 31);
+            hi[k] = __builtin_amdgcn_alignbit(cw, wb, pp & 31);
+        }
+#pragma unroll
+        for (int k = 0; k < N; k++) {
+            if (!f[k]) continue;
+            // the literals before the first escape byte, the stop (tokens starting before e) and
+            // the input's end
+            const uint32_t q = (e - p[k] + 7) >> 3, qi = (nb - min(nb, p[k])) >> 3;
+            const uint32_t tt = min(min(esc_index(lo[k], hi[k], esc4), q), qi);
+            if (tt) { p[k] += 8 * tt; c[k] += tt; continue; }
+            Tok tk;
+            tok_e<true>(lo[k], hi[k], t.lit[lo[k] & ((1u << LB) - 1u)], p[k], t, ed, e, nb, tk);
+            if (tk.kind > K_LEN) { l[k] = false; O[k].kr = tk.kind == K_EOB ? (T_EOB << 5) : ((T_ERR << 5) | tk.val); }
+            else c[k] += tk.n;
+        }
+    }
+#pragma unroll
+    for (int k = 0; k < N; k++) { O[k].end = p[k]; O[k].cnt = c[k]; }
+}
+// The prefix mask of an escape-prefix literal block, repeated in the 4 bytes, or 0: every stream
+// byte x with (x & M) != M (M = 2^(8-k) - 1, k <= 2) is a single 8-bit literal's primary entry and
+// no other byte is.  All lanes call (the tables in LDS, built).
+__device__ __forceinline__ uint32_t flat8_mask(const Tabs& t, int lane) {
+    uint64_t L[4];
+#pragma unroll
+    for (uint32_t i = 0; i < 4; i++) L[i] = __ballot((t.lit[(uint32_t)lane + 64 * i] & 0x800001FFu) == 0x80000088u);
+    uint32_t m4 = 0;
+#pragma unroll
+    for (uint32_t kk = 0; kk < 3; kk++) {
+        const uint32_t M = (1u << (8 - kk)) - 1u;
+        bool same = true;
+#pragma unroll
+        for (uint32_t i = 0; i < 4; i++) same = same && __ballot((((uint32_t)lane + 64 * i) & M) != M) == L[i];
+        if (same && !m4) m4 = M * 0x01010101u;
+    }
+    return m4;
+}
+
 __device__ __forceinline__ uint32_t sel8(const uint32_t (&v)[8], uint32_t i) {
     uint32_t r = v[0];
 #pragma unroll
@@ -1481,7 +1553,7 @@ __device__ __forceinline__ uint32_t map_compose(uint32_t A, uint32_t B) {
 
 __device__ __noinline__ void round_decode_phased(const In& in, const Tabs& t, bool ed, uint64_t rs, uint64_t E,
                                                  Shared& S, Stage& stg, int lane, Seg& out, uint32_t& first_term,
-                                                 uint32_t& nfix, Geo& g) {
+                                                 uint32_t& nfix, Geo& g, uint32_t esc4) {
     g = make_geo(in, rs, E);
     stage_round(in, g, stg, lane);
     const Lv v = make_lv(stg, g, lane);
@@ -1493,17 +1565,23 @@ __device__ __noinline__ void round_decode_phased(const In& in, const Tabs& t, bo
     uint32_t fbl = 0, fbh = 0;
 #if NDFL_PHASE_GROUP > 1
     constexpr uint32_t G = NDFL_PHASE_GROUP >= 8 ? 8 : NDFL_PHASE_GROUP >= 4 ? 4 : 2;
-#pragma unroll
+    // (one copy of each run group's code, its results selected into place: the loop unrolled made the
+    // function 74 KB, more than the instruction cache, with the pass's other code competing)
+#pragma unroll 1
     for (uint32_t f = 0; f < 8; f += G) {
         PhOut P[G];
-        phase_multi<G>(v, t, ed, nb, s + f, e, P);       // (past e: empty, ends at s + f)
+        if (esc4) phase_multi_esc<G>(v, t, ed, nb, s + f, e, esc4, P);
+        else phase_multi<G>(v, t, ed, nb, s + f, e, P);  // (past e: empty, ends at s + f)
 #pragma unroll
         for (uint32_t h = 0; h < G; h++) {
             const uint32_t g = f + h;
-            endv[g] = P[h].end;
-            cntv[g] = P[h].cnt;
-            fbcv[g] = P[h].fbc;
-            krv[g] = P[h].kr;
+#pragma unroll
+            for (uint32_t k = 0; k < 8; k++) {
+                endv[k] = k == g ? P[h].end : endv[k];
+                cntv[k] = k == g ? P[h].cnt : cntv[k];
+                fbcv[k] = k == g ? P[h].fbc : fbcv[k];
+                krv[k] = k == g ? P[h].kr : krv[k];
+            }
             const uint32_t fo = (P[h].fb != NOCP && P[h].fb - s < 255u) ? P[h].fb - s : 255u;
             if (g < 4) fbl |= fo << (8 * g); else fbh |= fo << (8 * (g - 4));
         }
@@ -1569,7 +1647,13 @@ __device__ __noinline__ void round_decode_phased(const In& in, const Tabs& t, bo
             if ((uint32_t)lane == j) {
                 const uint32_t st = j ? (uint32_t)S.exit_[j - 1] : s;
                 uint32_t en, cn, kr, fb, fbc;
-                phase_run(v, t, ed, nb, st, e, en, cn, kr, fb, fbc);
+                if (esc4) {
+                    PhOut P1[1];
+                    phase_multi_esc<1>(v, t, ed, nb, st, e, esc4, P1);
+                    en = P1[0].end; cn = P1[0].cnt; kr = P1[0].kr;
+                } else {
+                    phase_run(v, t, ed, nb, st, e, en, cn, kr, fb, fbc);
+                }
                 r.start = st; r.end = en; r.cnt = cn; r.kind = kr >> 5; r.reason = kr & 31u;
                 S.exit_[lane] = en;
                 S.kind_[lane] = r.kind;
@@ -1804,7 +1888,7 @@ __device__ __forceinline__ void wr_copy(gu8* out, uint64_t dst, uint32_t len, ui
 // leaves 63 lanes idle through a chain of dependent loads, becomes a load of 336 bytes).
 extern "C" __global__ void __launch_bounds__(64)
 ndfl_inflate_hdr_kernel(const uint32_t* w, uint64_t nwords, uint64_t nbits, const uint64_t* cands, uint32_t ncand,
-                        wv::HdrRec* rec) {
+                        wv::HdrRec* rec, uint32_t* flat_list, uint32_t* nflat, uint32_t* flat_flag) {
     using namespace wv;
     __shared__ __attribute__((aligned(16))) uint32_t lens[64][80];
     __shared__ uint16_t clt[64][128];
@@ -1822,6 +1906,31 @@ ndfl_inflate_hdr_kernel(const uint32_t* w, uint64_t nwords, uint64_t nbits, cons
         *(uint4*)&r->lens[q] = make_uint4(lens[lane][q], lens[lane][q + 1], lens[lane][q + 2], lens[lane][q + 3]);
     r->h = h;
     r->at = p;
+    // escape-prefix literal code (count_flat_group): no code shorter than 8 bits, every 8-bit code a
+    // literal, 256 - 2^k of them (k <= 2) -- the other 2^k prefixes lead to the longer codes
+    uint32_t c8 = 0;
+    bool bad = false;
+    for (uint32_t q = 0; q < 72; q++) {
+        const uint32_t v = lens[lane][q];
+#pragma unroll
+        for (uint32_t b = 0; b < 4; b++) {
+            const uint32_t l = (v >> (8 * b)) & 0xFFu;
+            c8 += l == 8 ? 1u : 0u;
+            bad = bad || (l - 1u < 7u) || (l == 8 && q >= 64);
+        }
+    }
+    const uint32_t esc = 256u - min(c8, 256u);
+    const uint32_t kk = esc == 1 ? 1u : esc == 2 ? 2u : esc == 4 ? 3u : 0u;
+    r->flat = (flat_list && h.err == 0 && h.btype == 2 && !bad) ? kk : 0u;
+    r->pad = 0;
+    if (flat_flag) flat_flag[k] = r->flat;
+    if (flat_list) {                            // (wave-aggregated append)
+        const uint64_t m = __ballot(r->flat != 0);
+        uint32_t b = 0;
+        if (lane == 0 && m) b = atomicAdd(nflat, (uint32_t)__popcll(m));
+        b = __shfl(b, 0, 64);
+        if (r->flat) flat_list[b + (uint32_t)__popcll(m & ((1ull << lane) - 1ull))] = k;
+    }
 }
 
 // Count pass: persistent waves, each claiming candidate chains through `ticket`; the phase-fallback
@@ -1836,17 +1945,344 @@ ndfl_inflate_hdr_kernel(const uint32_t* w, uint64_t nwords, uint64_t nbits, cons
 #ifndef NDFL_TREC_BATCH
 #define NDFL_TREC_BATCH 4       // table records claimed per atomic
 #endif
+namespace wv {
+// ---- escape-prefix literal blocks, one lane per block (round 6) ------------------------------------
+// What DEFLATE encoders produce for incompressible data: a literal/length code of 255 literals of 8
+// bits (254, 252: 2^k prefixes left) with the few longer codes -- end of block, a rare literal or
+// length -- under the remaining all-ones prefix.  In wave form that is the count pass's costliest case:
+// the codes never resynchronise from a wrong bit phase, so every round decodes all 8 phases
+// (round_decode_phased, ~1.2 ms of wave time per 64 KiB block, a quarter of the pass on the bench
+// corpus).  Decoded serially by ONE lane it needs no speculation at all, and "is any of the next 8
+// bytes an escape prefix" covers 8 tokens in a few VALU operations.  A wave takes up to 64 such chains
+// (a flat group; ndfl_inflate_hdr_kernel lists them), builds each block's tables and table record in
+// turn as usual, keeps per lane a 64-entry escape table (the code under the prefix, from the next 6
+// bits), and then every lane decodes its own block, writing exactly the round records the wave decode
+// would write (the same round geometry; each lane segment from the first token boundary at or past
+// its nominal start -- the emit passes check every one) and the chain's result.  Whatever it cannot
+// finish this way -- an error, the input's end, a chain that continues past its first block, more
+// than NDFL_FLAT_OTHER_MAX tokens that need the full tables -- goes back to the wave decode, from the
+// chain's start.
+#ifndef NDFL_FLAT_OTHER_MAX
+#define NDFL_FLAT_OTHER_MAX 64          // tokens per block decoded through the global table record
+#endif
+#ifndef NDFL_FLAT_K
+#define NDFL_FLAT_K 4                   // steps between the input rings' phase points
+#endif
+#ifndef NDFL_FLAT_PRIO
+#define NDFL_FLAT_PRIO 1                // the group's decode at raised wave priority (s_setprio 3)
+#endif
+#ifdef NDFL_FLAT_PROF
+__device__ unsigned long long g_flat_prof[4];
+#endif
+constexpr uint32_t FLAT_ESC_WORD = 64;  // escape tables in the stage from this word (the build's scratch below)
+static_assert(FLAT_ESC_WORD + 64 * 64 / 4 <= SW * 64, "flat escape tables in the stage");
+
+// escape entry for the stream bits x following a block's all-ones (8 - kk)-bit prefix: code length |
+// kind << 4 (kind 0 a literal, 1 end of block), or 0 (a length code, a reserved symbol, a code longer
+// than the 6 bits cover: the full tables decide)
+__device__ __forceinline__ uint32_t flat_esc_entry(const TabsG& t, uint32_t kk, uint32_t x) {
+    const uint32_t pl = 8 - kk;
+    const uint32_t w = ((1u << pl) - 1u) | (x << pl);
+    uint32_t e = t.lit[w & ((1u << LB) - 1u)];
+    uint32_t len, kind;
+    if (e >> 31) {                                  // a single literal (no pair: the code has >= 9 bits)
+        len = e & 15; kind = 0;
+    } else {
+        if (!(e & 31)) e = long_lit(e, w, t);
+        len = e & 31;
+        const uint32_t k = (e >> 9) & 3;
+        kind = k == K_LIT ? 0u : k == K_EOB ? 1u : 2u;
+    }
+    return (kind < 2 && len > pl && len <= pl + 6) ? (len | (kind << 4)) : 0u;
+}
+
+// One flat group (flist[0, n), n <= 64).  Returns the number of chains left to the wave decode, listed
+// in redo[] (LDS).  All lanes call.
+__device__ __forceinline__ uint32_t count_flat_group(const In& in, const uint32_t* flist, uint32_t n,
+                                                     const uint64_t* cands, uint32_t ncand, uint64_t limit,
+                                                     uint64_t stop_all, ChainRes* res, const SegPool& pool,
+                                                     const HdrRec* hrec, Shared& S, uint32_t* stw, int lane,
+                                                     uint32_t* redo, uint32_t& tb_next, uint32_t& tb_end) {
+    lu8* escs = (lu8*)((lu32*)stw + FLAT_ESC_WORD);        // lane j's entries at escs[j * 64]
+    // 1. the blocks' tables one after the other; lane k keeps block k's fields
+    uint32_t my_c = 0, my_brec = NOREC, my_kk = 0;
+    uint64_t my_d0 = 0;
+    bool my_ok = false, my_final = false, my_ed = false;
+    for (uint32_t k = 0; k < n; k++) {
+        const uint32_t c = flist[k];
+        const HdrRec* hr = hrec + c;
+        uint32_t* lw = (uint32_t*)S.lens;
+        lw[lane] = hr->lens[lane];
+        if (lane < 16) lw[64 + lane] = hr->lens[64 + lane];
+        if (lane == 0) hdr_to_shared(hr->h, S);
+        const uint32_t kk = hr->flat - 1u;
+        __syncthreads();
+        bool ed;
+        const int te = build_tables(S, lane, ed, stw);
+        uint32_t brec = NOREC;
+        if (!te) {
+            if (c < pool.nslot && pool.nbt) {
+                if (tb_next >= tb_end) {
+                    uint32_t b = 0;
+                    if (lane == 0) b = atomicAdd(pool.bctr, (uint32_t)NDFL_TREC_BATCH);
+                    b = __builtin_amdgcn_readfirstlane(b);
+                    tb_next = b; tb_end = b + NDFL_TREC_BATCH;
+                }
+                brec = tb_next++;
+                if (brec < pool.nbt) {
+                    uint4* dst = (uint4*)(pool.bt + (uint64_t)brec * BT_BYTES);
+                    const uint4* src = (const uint4*)&S.t;
+                    for (uint32_t q = (uint32_t)lane; q < sizeof(Tabs) / 16; q += 64) dst[q] = src[q];
+                    if (lane == 0) {
+                        uint64_t* h = (uint64_t*)(pool.bt + (uint64_t)brec * BT_BYTES + sizeof(Tabs));
+                        h[0] = cands[c]; h[1] = S.h_d0;
+                        uint32_t* h32 = (uint32_t*)(h + 2);
+                        h32[0] = S.h_bfinal; h32[1] = S.h_btype; h32[2] = ed ? 1u : 0u;
+                        h32[3] = ((1u << (8 - kk)) - 1u) * 0x01010101u;    // (the escape prefix mask)
+                    }
+                } else {
+                    brec = NOREC;
+                }
+            }
+            const TabsG tg{S.t.lit, S.t.dst, S.t.lx, S.t.dx};
+            escs[k * 64 + lane] = (uint8_t)flat_esc_entry(tg, kk, (uint32_t)lane);
+        }
+        if ((uint32_t)lane == k) {
+            my_c = c; my_ok = !te; my_d0 = S.h_d0; my_final = S.h_bfinal != 0; my_ed = ed; my_brec = brec; my_kk = kk;
+        }
+        __syncthreads();                        // (the next block's header and tables overwrite these)
+    }
+    // 2. the rounds each block needs, claimed for the group at once: a round covers MAX_SPAN bits
+    // unless a header candidate ends it first (+1: the last round may end past the next candidate)
+    const bool active = (uint32_t)lane < n && my_ok;
+    uint32_t ci = my_c;
+    uint64_t cv = active ? cands[ci] : NONE;
+    auto after = [&](uint64_t b) {
+        while (cv <= b) { ci++; cv = ci < ncand ? cands[ci] : NONE; }
+        return min(cv, limit);
+    };
+    uint32_t nr = 0;
+    if (active) {
+        const uint64_t e0 = after(my_d0);
+        nr = (uint32_t)min<uint64_t>((e0 > my_d0 ? (e0 - my_d0 + MAX_SPAN - 1) / MAX_SPAN : 1) + 1, 1024);
+    }
+    const uint32_t rpre = (uint32_t)wave_excl_u64(nr, lane), rtot = (uint32_t)wave_sum_u64(nr);
+    uint32_t rb = 0;
+    if (lane == 0 && rtot) rb = atomicAdd(pool.ctr, rtot);
+    rb = __builtin_amdgcn_readfirstlane(rb);
+    // 3. every lane decodes its block alone.  A step is a token (up to 8 literals), a segment switch,
+    // or a round's start or end.  The input comes through a ring of 24 words per lane in LDS, in the
+    // tables' place (three slots of 8 words; word row r of lane j at ring[r * 64 + j]: no bank
+    // conflicts), refilled at phase points every FLAT_K steps, all lanes at once: a lane that left its
+    // oldest slot writes the next slot's words, loaded into registers at the previous phase point, and
+    // loads the slot after.  Those registers are touched at phase points only -- a lane refilling while
+    // the others step made the wave wait for the newest load at every step (8 ms per group).
+    bool ok = false;
+    uint64_t total = 0, endpos = 0;
+    uint32_t status = ST_BOUNDARY, next_idx = 0xFFFFFFFFu;
+    if (active) {
+        const uint32_t pl = 8 - my_kk, M4 = ((1u << pl) - 1u) * 0x01010101u;
+        bool recording = my_c < pool.nslot;
+        uint32_t rnext = rb + rpre, rlast = rnext + nr;
+        uint32_t brec = my_brec, others = 0;
+        // positions relative to an origin at a multiple of 8 words before the block's data (u32)
+        const uint64_t o64 = (my_d0 >> 8) << 8;
+        const uint64_t og4 = o64 >> 7;                  // (its 16-byte group)
+        const uint32_t nbo = (uint32_t)min<uint64_t>(in.nbits - min(in.nbits, o64), 0xFFFFFF00ull);
+        uint32_t pos = (uint32_t)(my_d0 - o64);
+        lu32* ring = (lu32*)&S.t + lane;
+        uint32_t fw = (pos >> 5) & ~7u;                 // the ring holds words [fw - 24, fw)
+#pragma unroll
+        for (uint32_t i = 0; i < 24; i += 4) {
+            const u32x4 v = in.ld4(og4 + ((fw + i) >> 2));
+            ring[i * 64] = v.x; ring[(i + 1) * 64] = v.y; ring[(i + 2) * 64] = v.z; ring[(i + 3) * 64] = v.w;
+        }
+        fw += 24;
+        uint32_t frow = 0;                              // the ring row of word fw
+        u32x4 ra = in.ld4(og4 + (fw >> 2)), rb = in.ld4(og4 + (fw >> 2) + 1);
+        // the round [rs, E) in the wave decode's geometry (make_geo, lane_seg); segment j: the tokens
+        // starting in [s_j, s_{j+1}) (s_0 = r0, s_64 = re), relative to the round's word-aligned base
+        uint32_t base = 0, r0 = 0, re = 0, per = 0, pw = 0, nbr = 0, idx = NOREC, j = 0, p = 0, jst = 0, bytes = 0, sn = 0;
+        uint64_t* ps = nullptr;                         // the round record's starts and counts, its meta
+        uint32_t* pc = nullptr;
+        uint4* mq = nullptr;
+        uint32_t* link = pool.head + my_c;              // where the next round record's index goes
+        uint32_t st = 0;                                // 0 a round starts at pos, 1 in a round, 2 EOB, 3 back
+        // the group is the pass's longest job: it takes the SIMD's issue slots first
+        if (NDFL_FLAT_PRIO) __builtin_amdgcn_s_setprio(3);
+        // the round's records: segment j ends the block (EOB) or the round (j = 63)
+        auto end_round = [&](bool eob) {
+            if (ps) {
+                const uint64_t ex = o64 + base + p;
+                ps[j] = o64 + base + jst;
+                pc[j] = bytes;
+                for (uint32_t jj = j + 1; jj < 64; jj++) { ps[jj] = ex; pc[jj] = 0; }
+                // (the fields as two 16-byte and one 8-byte stores of values at hand: a SegMeta built in
+                // registers was partly spilled, and its reload waited for the rings' loads in flight)
+                uint32_t kf = eob ? (uint32_t)T_EOB : (uint32_t)T_EXIT;
+                asm volatile("" : "+v"(kf));            // (materialised here, not a spilled constant)
+                mq[0] = make_uint4(eob ? j : 64u, kf, 0u, NOREC);
+                mq[1] = make_uint4((uint32_t)ex, (uint32_t)(ex >> 32), (uint32_t)ex, (uint32_t)(ex >> 32));
+                *(uint2*)(mq + 2) = make_uint2(pw, brec);
+                *(uint64_t*)((uint2*)(mq + 2) + 1) = o64 + base + r0;
+                *link = idx;                            // (the chain's head, then the previous round's next)
+                link = (uint32_t*)mq + 3;
+                brec = NOREC;                           // (only the block's first round names its tables)
+            }
+            total += bytes;
+            pos = base + p;
+        };
+        // segment j's record, and the next segment's start
+        auto next_seg = [&]() {
+            if (ps) { ps[j] = o64 + base + jst; pc[j] = bytes; }
+            total += bytes;
+            j++; jst = p; bytes = 0;
+            sn = j < 63 ? min(r0 + (j + 1) * per, re) : re;
+        };
+#ifdef NDFL_FLAT_PROF
+        unsigned long long fp_ph = 0, fp_t0 = clock64(), fp_n = 0;
+#endif
+        while (st < 2) {
+            {   // phase point
+#ifdef NDFL_FLAT_PROF
+                const unsigned long long fp_a = clock64();
+#endif
+                const uint32_t cw = (st == 1 ? base + p : pos) >> 5;
+                if (cw + 16 >= fw) {
+                    ring[frow * 64] = ra.x; ring[(frow + 1) * 64] = ra.y; ring[(frow + 2) * 64] = ra.z;
+                    ring[(frow + 3) * 64] = ra.w; ring[(frow + 4) * 64] = rb.x; ring[(frow + 5) * 64] = rb.y;
+                    ring[(frow + 6) * 64] = rb.z; ring[(frow + 7) * 64] = rb.w;
+                    fw += 8;
+                    frow = frow == 16 ? 0u : frow + 8;
+                    ra = in.ld4(og4 + (fw >> 2)); rb = in.ld4(og4 + (fw >> 2) + 1);
+                }
+#ifdef NDFL_FLAT_PROF
+                asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+                fp_ph += clock64() - fp_a;
+                fp_n++;
+#endif
+            }
+            for (uint32_t k = 0; k < NDFL_FLAT_K && st < 2; k++) {
+                if (st == 0) {
+                    const uint64_t rsa = o64 + pos;
+                    uint64_t E = min(after(rsa), rsa + MAX_SPAN);
+                    if (E <= rsa) E = rsa + 1;
+                    base = pos & ~31u;
+                    r0 = pos - base; re = (uint32_t)(E - o64) - base;
+                    pw = max((uint32_t)NDFL_PW_MIN, ((re - r0 + 63) / 64 + 31) / 32); per = pw * 32;
+                    nbr = nbo - min(nbo, base);
+                    idx = NOREC;
+                    if (recording) {
+                        if (rnext >= rlast) {           // (a header candidate inside the block: more rounds)
+                            rnext = atomicAdd(pool.ctr, 8u);
+                            rlast = rnext + 8;
+                        }
+                        if (rnext < pool.nrec) idx = rnext++;
+                        else recording = false;
+                    }
+                    ps = idx != NOREC ? pool.start + (uint64_t)idx * 64 : nullptr;
+                    pc = idx != NOREC ? pool.cnt + (uint64_t)idx * 64 : nullptr;
+                    mq = idx != NOREC ? (uint4*)(pool.meta + idx) : nullptr;
+                    j = 0; p = r0; jst = r0; bytes = 0;
+                    sn = min(r0 + per, re);
+                    st = 1;
+                    continue;
+                }
+                if (p >= sn) {                          // (segments left empty at a round's end)
+                    if (j == 63) { end_round(false); st = 0; }      // (exit63 = p)
+                    else next_seg();
+                    continue;
+                }
+                const uint32_t ap = base + p, cw = ap >> 5;
+                if (cw + 2 >= fw) break;                // (the ring is not that far yet: next phase point)
+                uint32_t rr0 = frow + 24 - (fw - cw);   // (fw - cw in 3..24)
+                rr0 = rr0 >= 24 ? rr0 - 24 : rr0;
+                const uint32_t rr1 = rr0 == 23 ? 0u : rr0 + 1, rr2 = rr1 == 23 ? 0u : rr1 + 1;
+                const uint32_t w0 = ring[rr0 * 64], w1 = ring[rr1 * 64], w2 = ring[rr2 * 64];
+                const uint32_t sh = ap & 31u;
+                const uint32_t lo = __builtin_amdgcn_alignbit(w1, w0, sh), hi = __builtin_amdgcn_alignbit(w2, w1, sh);
+                const uint32_t q = (sn - p + 7) >> 3, qi = (nbr - min(nbr, p)) >> 3;
+                const uint32_t t = min(min(esc_index(lo, hi, M4), q), qi);
+                if (t) {                                // t literals of 8 bits
+                    bytes += t;
+                    p += 8 * t;
+                } else {
+                    // (the lane index recomputed here: a value kept from outside the loop was spilled,
+                    // and its reload waited for the rings' loads in flight)
+                    uint32_t ln;
+                    asm volatile("v_mbcnt_lo_u32_b32 %0, -1, 0\n\tv_mbcnt_hi_u32_b32 %0, -1, %0" : "=v"(ln));
+                    const uint32_t ent = escs[ln * 64 + ((lo >> pl) & 63u)], len = ent & 15u;
+                    if ((lo & (M4 & 0xFFu)) == (M4 & 0xFFu) && ent && p + len <= nbr) {
+                        p += len;
+                        if (ent >> 4) { end_round(true); st = 2; continue; }
+                        bytes++;
+                    } else {
+                        // through the block's full tables (global table record)
+                        if (my_brec == NOREC || ++others > NDFL_FLAT_OTHER_MAX) { st = 3; continue; }
+                        const uint32_t* tb = (const uint32_t*)(pool.bt + (uint64_t)my_brec * BT_BYTES);
+                        const TabsG tg{tb, tb + (1u << LB), tb + offsetof(Tabs, lx) / 4, tb + offsetof(Tabs, dx) / 4};
+                        uint32_t pp = 0;
+                        Tok tk;
+                        tok_e<true>(lo, hi, tg.lit[lo & ((1u << LB) - 1u)], pp, tg, my_ed, sn - p, nbr - min(nbr, p), tk);
+                        if (tk.kind == K_EOB) { p += pp; end_round(true); st = 2; continue; }
+                        if (tk.kind != K_LIT && tk.kind != K_LEN) { st = 3; continue; }
+                        bytes += tk.n;
+                        p += pp;
+                    }
+                }
+                // the token(s) started before sn: a segment (or the round) ends at the first boundary past it
+                if (p >= sn) {
+                    if (j == 63) { end_round(false); st = 0; }
+                    else next_seg();
+                }
+            }
+        }
+        if (NDFL_FLAT_PRIO) __builtin_amdgcn_s_setprio(0);
+#ifdef NDFL_FLAT_PROF
+        if (lane == 0) {       // (lane 0's view: its loop cycles, of them at phase points, phase points)
+            atomicAdd(&g_flat_prof[0], clock64() - fp_t0); atomicAdd(&g_flat_prof[1], fp_ph); atomicAdd(&g_flat_prof[2], fp_n);
+        }
+#endif
+        if (st == 2) {
+            // the chain's end: the final block, or a header candidate (or the range end) next
+            const uint64_t cur = o64 + pos;
+            if (my_final) { status = ST_FINAL; endpos = cur; ok = true; }
+            else if (cur >= stop_all) { status = ST_BOUNDARY; endpos = cur; ok = true; }
+            else {
+                while (cv < cur) { ci++; cv = ci < ncand ? cands[ci] : NONE; }
+                next_idx = ci;
+                if (cv == cur) { status = ST_BOUNDARY; endpos = cur; ok = true; }
+            }
+        }
+    }
+    if (ok) {
+        ChainRes o;
+        o.end_bit = endpos; o.out_count = total; o.status = status; o.reason = 0; o.next = next_idx; o.pad = 0;
+        o.bnd_bit = 0; o.bnd_cnt = 0;
+        res[my_c] = o;
+    }
+    // 4. the rest back to the wave decode
+    const bool rd = (uint32_t)lane < n && !ok;
+    const uint64_t rm = __ballot(rd);
+    if (rd) redo[__popcll(rm & ((1ull << lane) - 1ull))] = my_c;
+    __syncthreads();
+    return (uint32_t)__popcll(rm);
+}
+}  // namespace wv
+
 extern "C" __global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(NDFL_COUNT_WPE)))
 ndfl_inflate_count_wave_kernel(const uint32_t* w, uint64_t nwords, uint64_t nbits, const uint64_t* starts,
                                const uint64_t* stops, uint32_t nchains, const uint64_t* cands, uint32_t ncand,
                                uint64_t limit, ChainRes* res, uint32_t* stats, uint64_t slot_base, SegPool pool,
                                uint32_t* ticket, wv::PhArr* ph_all, const uint32_t* order, uint64_t stop_all,
-                               const wv::HdrRec* hrec, const uint32_t* nord) {
+                               const wv::HdrRec* hrec, const uint32_t* nord, const uint32_t* flist,
+                               const uint32_t* nflat) {
     using namespace wv;
     __shared__ __attribute__((aligned(16))) Shared S;
-    if (nord) nchains = *nord;                  // (stored-header aliases left out of the order)
+    if (nord) nchains = *nord;                  // (stored-header aliases and flat chains left out of the order)
     __shared__ Stage stg;
     __shared__ uint32_t s_ticket;
+    __shared__ uint32_t s_redo[64];             // a flat group's chains left to the wave decode
     const int lane = threadIdx.x;
     PhArr* ph = ph_all + blockIdx.x;
     const In in{w, nwords, nbits};
@@ -1854,12 +2290,32 @@ ndfl_inflate_count_wave_kernel(const uint32_t* w, uint64_t nwords, uint64_t nbit
     // round and table records are claimed in batches per wave (one contended atomic per batch
     // instead of one per round; unused slots of a batch stay unused)
     uint32_t rb_next = 0, rb_end = 0, tb_next = 0, tb_end = 0;
+    // tickets [0, ngroups) are flat groups of up to 64 chains (count_flat_group), the rest index order[]
+    const uint32_t nfl = (nflat && hrec && slot_base == 0) ? *nflat : 0u, ngroups = (nfl + 63) / 64;
+    uint32_t nredo = 0;
     for (;;) {
-    __syncthreads();
-    if (lane == 0) s_ticket = atomicAdd(ticket, 1u);
-    __syncthreads();
-    if (s_ticket >= nchains) break;
-    const uint32_t c = order[s_ticket];
+    uint32_t c;
+    if (nredo) {
+        c = s_redo[--nredo];
+    } else {
+        __syncthreads();
+        if (lane == 0) s_ticket = atomicAdd(ticket, 1u);
+        __syncthreads();
+        const uint32_t tk = s_ticket;
+        if (tk >= ngroups + nchains) break;
+        if (tk < ngroups) {
+            const uint32_t g0 = tk * 64;
+            const uint64_t tf0 = stats ? wall_clock64() : 0;
+            nredo = count_flat_group(in, flist + g0, min(64u, nfl - g0), cands, ncand, limit, stop_all, res, pool, hrec,
+                                     S, stg.w, lane, s_redo, tb_next, tb_end);
+            if (stats && lane == 0) {                   // (ticket words 5, 6: chains sent back, group wave time)
+                atomicAdd(ticket + 5, nredo);
+                atomicAdd((unsigned long long*)(ticket + 6), (unsigned long long)(wall_clock64() - tf0));
+            }
+            continue;
+        }
+        c = order[tk - ngroups];
+    }
     const uint64_t start = starts[c], stop = stops ? stops[c] : stop_all;
     uint64_t cur = start, total = 0, endpos = start;
     uint32_t status = ST_BOUNDARY, reason = 0, nslow = 0, nfix = 0, nround = 0, next_idx = 0xFFFFFFFFu;
@@ -1916,6 +2372,7 @@ ndfl_inflate_count_wave_kernel(const uint32_t* w, uint64_t nwords, uint64_t nbit
         if (te) { status = ST_ERROR; reason = (uint32_t)te; endpos = d0; break; }
         // literal/length codes mostly of one length 8 resynchronise rarely: phase-mapped rounds
         bool phased = false;
+        uint32_t esc4 = 0;
         {
             uint32_t n8 = 0;
             for (uint32_t q = 0; q < 5; q++) {
@@ -1923,6 +2380,7 @@ ndfl_inflate_count_wave_kernel(const uint32_t* w, uint64_t nwords, uint64_t nbit
                 n8 += (uint32_t)__popcll(__ballot(sy < 288 && S.lens[sy] == 8));
             }
             phased = n8 >= 192;
+            if (phased && NDFL_PHASE_ESC) esc4 = flat8_mask(S.t, lane);
         }
         // the block's tables and header fields for the emit pass (a table record)
         uint32_t brec = NOREC;
@@ -1942,7 +2400,8 @@ ndfl_inflate_count_wave_kernel(const uint32_t* w, uint64_t nwords, uint64_t nbit
                     uint64_t* h = (uint64_t*)(pool.bt + (uint64_t)brec * BT_BYTES + sizeof(Tabs));
                     h[0] = cur; h[1] = d0;
                     uint32_t* h32 = (uint32_t*)(h + 2);
-                    h32[0] = S.h_bfinal; h32[1] = S.h_btype; h32[2] = ed ? 1u : 0u; h32[3] = phased ? 1u : 0u;
+                    h32[0] = S.h_bfinal; h32[1] = S.h_btype; h32[2] = ed ? 1u : 0u;
+                    h32[3] = phased ? (esc4 ? esc4 : 1u) : 0u;      // (emit: 4-literal steps / escape scan)
                 }
             } else {
                 brec = NOREC;
@@ -1959,7 +2418,7 @@ ndfl_inflate_count_wave_kernel(const uint32_t* w, uint64_t nwords, uint64_t nbit
             Geo g;
             if (phased) {
                 const uint64_t t0p = pc ? wall_clock64() : 0;
-                round_decode_phased(in, S.t, ed, rs, E, S, stg, lane, r, ft, nfix, g);
+                round_decode_phased(in, S.t, ed, rs, E, S, stg, lane, r, ft, nfix, g, esc4);
                 if (pc) pc->phmap += wall_clock64() - t0p;
             } else {
                 const uint32_t ns0 = nslow;
@@ -2411,6 +2870,7 @@ ndfl_inflate_emit_fast_kernel(const uint32_t* w, uint64_t nwords, uint64_t nbits
         const uint32_t* h32 = (const uint32_t*)(h + 2);
         const bool bfinal = h32[0] != 0, ed = h32[2] != 0;
         const bool ph8 = NDFL_EMIT_JUMP && h32[3] != 0;     // mostly 8-bit literal codes
+        const uint32_t esc4 = h32[3] > 1 ? h32[3] : 0u;     // escape-prefix literal block (phase_multi_esc)
         __syncthreads();
         bool block_done = false, chain_done = false;
         while (!block_done) {
@@ -2459,7 +2919,35 @@ ndfl_inflate_emit_fast_kernel(const uint32_t* w, uint64_t nwords, uint64_t nbits
                 using PH = decltype(ph);
                 while (live && pos < end) {
                     Tok tk;
-                    if (PH::value && fast && bb.nb >= 34 && pos + 24 < end) {
+                    if (PH::value && fast && esc4) {
+                        // escape-prefix literal block: up to 8 literals, to the first escape byte
+                        const uint32_t lo = (uint32_t)bb.buf, hi = (uint32_t)(bb.buf >> 32);
+                        const uint32_t t = min(min(esc_index(lo, hi, esc4), bb.nb >> 3), (end - pos + 7) >> 3);
+                        if (t) {
+                            uint32_t b[8];
+#pragma unroll
+                            for (uint32_t i = 0; i < 8; i++)
+                                b[i] = (T.lit[(i < 4 ? lo >> (8 * i) : hi >> (8 * (i - 4))) & 0xFFu] >> 9) & 0xFFu;
+                            const uint32_t v0 = b[0] | (b[1] << 8) | (b[2] << 16) | (b[3] << 24);
+                            const uint32_t v1 = b[4] | (b[5] << 8) | (b[6] << 16) | (b[7] << 24);
+                            const uint32_t n0 = min(t, 4u);
+                            wr_lit(wr, gout, n0 == 4 ? v0 : v0 & ((1u << (8 * n0)) - 1u), n0);
+                            if (t > 4) wr_lit(wr, gout, t == 8 ? v1 : v1 & ((1u << (8 * (t - 4))) - 1u), t - 4);
+                            n += t;
+                            lsp = true;
+                            lastb = t > 4 ? (v1 >> (8 * (t - 5))) & 0xFFu : (v0 >> (8 * (t - 1))) & 0xFFu;
+                            lastok = true;
+                            // (a 64-bit shift by 64 is undefined: the hardware shifts by 0)
+                            bb.buf = t < 8 ? bb.buf >> (8 * t) : 0ull;
+                            bb.nb -= 8 * t;
+                            bb.pos += 8 * t;
+                            bb_refill(bb, v);
+                            pos = bb.pos;
+                            fast = pos < lim;
+                            continue;
+                        }
+                    }
+                    if (PH::value && fast && !esc4 && bb.nb >= 34 && pos + 24 < end) {
                         // four 8-bit literal codes at once (independent table reads at 0, 8, 16, 24 bits;
                         // the lane's end is a token boundary, so none of the four passes it)
                         const uint32_t lo = (uint32_t)bb.buf, hi = (uint32_t)(bb.buf >> 32);

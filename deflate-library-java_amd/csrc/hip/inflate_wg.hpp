@@ -228,7 +228,8 @@ __device__ void round_decode_wg(const In& in, const Tabs& t, bool ed, uint64_t r
 // Phase-mapped round over 64W lanes (round_decode_phased, the maps composed across the waves).
 template <int W>
 __device__ void round_decode_phased_wg(const In& in, const Tabs& t, bool ed, uint64_t rs, uint64_t E, WgX<W>& X,
-                                       Stage* stg, Seg& out, uint32_t& first_term, uint32_t& nfix, Geo& g, uint32_t& par) {
+                                       Stage* stg, Seg& out, uint32_t& first_term, uint32_t& nfix, Geo& g, uint32_t& par,
+                                       uint32_t esc4) {
     const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
     const uint32_t L = threadIdx.x;
     g = make_geo_w<W>(in, rs, E);
@@ -243,7 +244,8 @@ __device__ void round_decode_phased_wg(const In& in, const Tabs& t, bool ed, uin
     uint32_t fbl = 0, fbh = 0;
     {
         PhOut P[8];
-        phase_multi<8>(v, t, ed, nb, s, e, P);         // (past e: empty, ends at s + f)
+        if (esc4) phase_multi_esc<8>(v, t, ed, nb, s, e, esc4, P);
+        else phase_multi<8>(v, t, ed, nb, s, e, P);    // (past e: empty, ends at s + f)
 #pragma unroll
         for (uint32_t h = 0; h < 8; h++) {
             endv[h] = P[h].end; cntv[h] = P[h].cnt; fbcv[h] = P[h].fbc; krv[h] = P[h].kr;
@@ -310,7 +312,13 @@ __device__ void round_decode_phased_wg(const In& in, const Tabs& t, bool ed, uin
             if (L == j) {
                 const uint32_t st = j ? X.exit_[j - 1] : s;
                 uint32_t en, cn, kr, fb, fbc;
-                phase_run(v, t, ed, nb, st, e, en, cn, kr, fb, fbc);
+                if (esc4) {
+                    PhOut P1[1];
+                    phase_multi_esc<1>(v, t, ed, nb, st, e, esc4, P1);
+                    en = P1[0].end; cn = P1[0].cnt; kr = P1[0].kr;
+                } else {
+                    phase_run(v, t, ed, nb, st, e, en, cn, kr, fb, fbc);
+                }
                 r.start = st; r.end = en; r.cnt = cn; r.kind = kr >> 5; r.reason = kr & 31u;
                 X.exit_[L] = en;
                 X.kind_[L] = (uint8_t)r.kind;
@@ -333,7 +341,7 @@ ndfl_inflate_count_wg_kernel(const uint32_t* w, uint64_t nwords, uint64_t nbits,
                              const uint64_t* stops, uint32_t nchains, const uint64_t* cands, uint32_t ncand,
                              uint64_t limit, ChainRes* res, uint32_t* stats, uint64_t slot_base, SegPool pool,
                              uint32_t* ticket, wv::PhArr* ph_all, const uint32_t* order, uint64_t stop_all,
-                             const wv::HdrRec* hrec, const uint32_t* nord) {
+                             const wv::HdrRec* hrec, const uint32_t* nord, const uint32_t*, const uint32_t*) {
     using namespace wv;
     __shared__ __attribute__((aligned(16))) Shared S;
     if (nord) nchains = *nord;                  // (stored-header aliases left out of the order)
@@ -411,6 +419,7 @@ ndfl_inflate_count_wg_kernel(const uint32_t* w, uint64_t nwords, uint64_t nbits,
             }
             phased = n8 >= 192;
         }
+        const uint32_t esc4 = (phased && NDFL_PHASE_ESC) ? flat8_mask(S.t, lane) : 0u;
         uint32_t brec = NOREC;
         if (recording && pool.nbt) {
             if (tid == 0) {
@@ -430,7 +439,8 @@ ndfl_inflate_count_wg_kernel(const uint32_t* w, uint64_t nwords, uint64_t nbits,
                     uint64_t* h = (uint64_t*)(pool.bt + (uint64_t)brec * BT_BYTES + sizeof(Tabs));
                     h[0] = cur; h[1] = d0;
                     uint32_t* h32 = (uint32_t*)(h + 2);
-                    h32[0] = S.h_bfinal; h32[1] = S.h_btype; h32[2] = ed ? 1u : 0u; h32[3] = phased ? 1u : 0u;
+                    h32[0] = S.h_bfinal; h32[1] = S.h_btype; h32[2] = ed ? 1u : 0u;
+                    h32[3] = phased ? (esc4 ? esc4 : 1u) : 0u;
                 }
             } else {
                 brec = NOREC;
@@ -445,7 +455,7 @@ ndfl_inflate_count_wg_kernel(const uint32_t* w, uint64_t nwords, uint64_t nbits,
             uint32_t ft;
             Geo g;
             if (phased) {
-                round_decode_phased_wg<W>(in, S.t, ed, rs, E, X, stg, r, ft, nfix, g, par);
+                round_decode_phased_wg<W>(in, S.t, ed, rs, E, X, stg, r, ft, nfix, g, par, esc4);
             } else {
                 uint32_t nsl = 0;
                 round_decode_wg<W>(in, S.t, ed, rs, E, X, stg, r, ft, nsl, nfix, ph, g);

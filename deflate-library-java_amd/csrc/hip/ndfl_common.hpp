@@ -9,7 +9,7 @@
 
 // Switches of a context, read once from the environment when the context is created
 // (ndfl_ctx_create).  None is needed in production: they select the decoder's hand-over paths for
-// the tests (EMIT_FAST, NO_BT, NO_ALIAS, COUNT_W, TEST_SEGFLIP), statistics for profiling (STATS, HOST_TIMES,
+// the tests (EMIT_FAST, NO_BT, NO_ALIAS, COUNT_W, FLAT, TEST_SEGFLIP), statistics for profiling (STATS, HOST_TIMES,
 // LZ_STATS), and the few A/B alternatives still measured against the defaults.
 struct Knobs {
     bool stats = false;          // NDFL_STATS: per-pass counters and phase clocks to stderr
@@ -26,6 +26,7 @@ struct Knobs {
     bool lz_stats = false;       // NDFL_LZ_STATS
     bool lz_chain = false;       // NDFL_LZ_SEARCH=chain: the round-3 hash-chain LZ77 search
     int lz_lead = -1;            // NDFL_LZ_LEAD: parse-driven search lead-in (-1: default)
+    bool flat = true;            // NDFL_FLAT=0: escape-prefix literal blocks counted in wave form too
     bool test_segflip = false;   // NDFL_TEST_SEGFLIP: one count-pass record's byte count perturbed
                                  //   before the emit pass (the emit-side check must fail the decode)
     void read() {
@@ -43,15 +44,16 @@ struct Knobs {
         lz_chain = se && !strcmp(se, "chain");
         lz_lead = num("NDFL_LZ_LEAD", -1);
         test_segflip = on("NDFL_TEST_SEGFLIP");
+        flat = num("NDFL_FLAT", 1) != 0;
     }
     // the effective switches, one line (printed by ndfl_ctx_create when stats are on)
     void print(FILE* f) const {
         fprintf(f, "[ndfl] context knobs: stats=%d host_times=%d host_link=%d no_hdrrec=%d emit_fast=%d no_bt=%d "
                    "no_alias=%d count_w=%u deflate_pf=%d deflate_profile=%d deflate_fused=%d lz_stats=%d "
-                   "lz_search=%s lz_lead=%d test_segflip=%d\n",
+                   "lz_search=%s lz_lead=%d test_segflip=%d flat=%d\n",
                 (int)stats, (int)host_times, (int)host_link, (int)no_hdrrec, (int)emit_fast, (int)no_bt,
                 (int)no_alias, count_w, (int)deflate_pf, (int)deflate_profile, (int)deflate_fused, (int)lz_stats,
-                lz_chain ? "chain" : "parse", lz_lead, (int)test_segflip);
+                lz_chain ? "chain" : "parse", lz_lead, (int)test_segflip, (int)flat);
     }
 };
 

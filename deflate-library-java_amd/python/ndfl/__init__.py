@@ -258,10 +258,10 @@ class Context:
 
     def timings(self):
         """{'deflate', 'inflate_find', 'inflate_count', 'inflate_emit', 'inflate_span'} in ms."""
-        arr = (ctypes.c_double * 8)()
-        load().ndfl_ctx_timings(self._h, arr, 8)
+        arr = (ctypes.c_double * 9)()
+        load().ndfl_ctx_timings(self._h, arr, 9)
         keys = ["deflate", "inflate_find", "inflate_count", "inflate_emit", "inflate_span", "inflate_chains",
-                "inflate_repairs", "inflate_candidates"]
+                "inflate_repairs", "inflate_candidates", "inflate_flat_chains"]
         return dict(zip(keys, list(arr)))
 
     # -- raw C-ABI wrappers ------------------------------------------------------------------

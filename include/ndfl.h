@@ -94,7 +94,8 @@ int ndfl_ctx_set_stream(ndfl_ctx* ctx, void* hip_stream);
 double ndfl_ctx_last_kernel_ms(ndfl_ctx* ctx);
 /* Device-time breakdown of the last calls (ms): [0] deflate kernel, [1] inflate finder,
  * [2] inflate count, [3] inflate emit, [4] inflate device span, [5] linked chains, [6] repaired
- * boundaries, [7] header candidates. */
+ * boundaries, [7] header candidates, [8] chains whose first block the count pass decoded one lane
+ * per block (escape-prefix literal codes).  Returns the number of entries written (<= 9). */
 int ndfl_ctx_timings(ndfl_ctx* ctx, double* ms, int n);
 /* The reserved symbol behind the last ndfl_inflate / ndfl_inflate_range that returned
  * NDFL_RESERVED_LENGTH_SYMBOL (286 or 287) or NDFL_RESERVED_DISTANCE_SYMBOL (30 or 31), else -1:
