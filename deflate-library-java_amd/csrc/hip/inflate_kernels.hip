@@ -1471,7 +1471,10 @@ static int inflate_devlink(InflateScratch& S, hipStream_t s, const uint32_t* d_w
     // header records, and the chains whose first block is counted by one lane (flat groups: the
     // one-wave count kernel only); those leave the count order
     const bool hrec_on = !S.knobs.no_hdrrec;
-    const bool flat_on = hrec_on && W == 1 && S.knobs.flat;
+    // (a flat group decodes its 64 blocks one lane each: ~7 ms of latency however few the chains, so
+    // only a pass long enough to hide it takes them -- the bench's 66,770 chains; one rank's 8,191 at
+    // 8 GPUs counts its incompressible blocks in wave form, by escape scans)
+    const bool flat_on = hrec_on && W == 1 && S.knobs.flat && nrep >= S.knobs.flat_min;
     uint32_t* d_flist = nullptr;
     uint32_t* d_fflag = nullptr;
     if (hrec_on) {
@@ -1516,8 +1519,10 @@ static int inflate_devlink(InflateScratch& S, hipStream_t s, const uint32_t* d_w
             cnt[st]++; tsum[st] += t; tmax[st] = std::max<uint64_t>(tmax[st], t); blk[st] += cr[k].pad & 0xFFFFu;
         }
         if (flat_on) {
-            uint32_t fw[4] = {0, 0, 0, 0};
-            INF_CHK(hipMemcpy(fw, (uint32_t*)S.d_cticket + 4, 16, hipMemcpyDeviceToHost));
+            uint32_t fw[12] = {0};
+            INF_CHK(hipMemcpy(fw, (uint32_t*)S.d_cticket + 4, 48, hipMemcpyDeviceToHost));
+            fprintf(stderr, "[ndfl] count flat groups sent back: (unused) %u, full-table tokens %u, "
+                    "error %u, chain goes on %u, table %u\n", fw[7], fw[8], fw[9], fw[10], fw[11]);
             const unsigned long long gt = (unsigned long long)fw[2] | ((unsigned long long)fw[3] << 32);
             fprintf(stderr, "[ndfl] count flat groups: %u chains in %u groups, %u sent back to the wave decode, "
                     "group wave time %.3f ms mean\n", fw[0], (fw[0] + 63) / 64, fw[1], fw[0] ? gt * 1e-5 / ((fw[0] + 63) / 64) : 0.0);

@@ -2002,7 +2002,8 @@ __device__ __forceinline__ uint32_t count_flat_group(const In& in, const uint32_
                                                      const uint64_t* cands, uint32_t ncand, uint64_t limit,
                                                      uint64_t stop_all, ChainRes* res, const SegPool& pool,
                                                      const HdrRec* hrec, Shared& S, uint32_t* stw, int lane,
-                                                     uint32_t* redo, uint32_t& tb_next, uint32_t& tb_end) {
+                                                     uint32_t* redo, uint32_t& tb_next, uint32_t& tb_end,
+                                                     uint32_t* whys) {
     lu8* escs = (lu8*)((lu32*)stw + FLAT_ESC_WORD);        // lane j's entries at escs[j * 64]
     // 1. the blocks' tables one after the other; lane k keeps block k's fields
     uint32_t my_c = 0, my_brec = NOREC, my_kk = 0;
@@ -2066,6 +2067,14 @@ __device__ __forceinline__ uint32_t count_flat_group(const In& in, const uint32_
         const uint64_t e0 = after(my_d0);
         nr = (uint32_t)min<uint64_t>((e0 > my_d0 ? (e0 - my_d0 + MAX_SPAN - 1) / MAX_SPAN : 1) + 1, 1024);
     }
+    // the next candidates after the first (a false candidate inside the block ends a round early;
+    // loaded here, not in the loop)
+    uint64_t cv1 = NONE, cv2 = NONE, cv3 = NONE;
+    if (active) {
+        cv1 = ci + 1 < ncand ? cands[ci + 1] : NONE;
+        cv2 = ci + 2 < ncand ? cands[ci + 2] : NONE;
+        cv3 = ci + 3 < ncand ? cands[ci + 3] : NONE;
+    }
     const uint32_t rpre = (uint32_t)wave_excl_u64(nr, lane), rtot = (uint32_t)wave_sum_u64(nr);
     uint32_t rb = 0;
     if (lane == 0 && rtot) rb = atomicAdd(pool.ctr, rtot);
@@ -2079,7 +2088,7 @@ __device__ __forceinline__ uint32_t count_flat_group(const In& in, const uint32_
     // the others step made the wave wait for the newest load at every step (8 ms per group).
     bool ok = false;
     uint64_t total = 0, endpos = 0;
-    uint32_t status = ST_BOUNDARY, next_idx = 0xFFFFFFFFu;
+    uint32_t status = ST_BOUNDARY, next_idx = 0xFFFFFFFFu, why = active ? 4u : 5u;   // (why a chain goes back)
     if (active) {
         const uint32_t pl = 8 - my_kk, M4 = ((1u << pl) - 1u) * 0x01010101u;
         bool recording = my_c < pool.nslot;
@@ -2165,7 +2174,17 @@ __device__ __forceinline__ uint32_t count_flat_group(const In& in, const uint32_
             for (uint32_t k = 0; k < NDFL_FLAT_K && st < 2; k++) {
                 if (st == 0) {
                     const uint64_t rsa = o64 + pos;
-                    uint64_t E = min(after(rsa), rsa + MAX_SPAN);
+                    // (the next candidate was loaded before the loop; a round passing it -- a candidate
+                    // inside the block -- goes back to the wave decode: a load here would make every
+                    // round start wait for the rings' loads in flight)
+                    if (cv <= rsa) { cv = cv1; cv1 = cv2; cv2 = cv3; cv3 = NONE; ci++; }
+                    if (cv <= rsa) {                    // (rare: more false candidates in the block)
+                        while (cv <= rsa) { ci++; cv = ci < ncand ? cands[ci] : NONE; }
+                        cv1 = ci + 1 < ncand ? cands[ci + 1] : NONE;
+                        cv2 = ci + 2 < ncand ? cands[ci + 2] : NONE;
+                        cv3 = ci + 3 < ncand ? cands[ci + 3] : NONE;
+                    }
+                    uint64_t E = min(min(cv, limit), rsa + MAX_SPAN);
                     if (E <= rsa) E = rsa + 1;
                     base = pos & ~31u;
                     r0 = pos - base; re = (uint32_t)(E - o64) - base;
@@ -2201,31 +2220,33 @@ __device__ __forceinline__ uint32_t count_flat_group(const In& in, const uint32_
                 const uint32_t w0 = ring[rr0 * 64], w1 = ring[rr1 * 64], w2 = ring[rr2 * 64];
                 const uint32_t sh = ap & 31u;
                 const uint32_t lo = __builtin_amdgcn_alignbit(w1, w0, sh), hi = __builtin_amdgcn_alignbit(w2, w1, sh);
+                // (the escape entry read at once, whether needed or not: its latency overlaps the scan;
+                // the lane index recomputed: a value kept from outside the loop was spilled, and its
+                // reload waited for the rings' loads in flight)
+                uint32_t ln;
+                asm volatile("v_mbcnt_lo_u32_b32 %0, -1, 0\n\tv_mbcnt_hi_u32_b32 %0, -1, %0" : "=v"(ln));
+                const uint32_t ent = escs[ln * 64 + ((lo >> pl) & 63u)];
                 const uint32_t q = (sn - p + 7) >> 3, qi = (nbr - min(nbr, p)) >> 3;
                 const uint32_t t = min(min(esc_index(lo, hi, M4), q), qi);
                 if (t) {                                // t literals of 8 bits
                     bytes += t;
                     p += 8 * t;
                 } else {
-                    // (the lane index recomputed here: a value kept from outside the loop was spilled,
-                    // and its reload waited for the rings' loads in flight)
-                    uint32_t ln;
-                    asm volatile("v_mbcnt_lo_u32_b32 %0, -1, 0\n\tv_mbcnt_hi_u32_b32 %0, -1, %0" : "=v"(ln));
-                    const uint32_t ent = escs[ln * 64 + ((lo >> pl) & 63u)], len = ent & 15u;
+                    const uint32_t len = ent & 15u;
                     if ((lo & (M4 & 0xFFu)) == (M4 & 0xFFu) && ent && p + len <= nbr) {
                         p += len;
                         if (ent >> 4) { end_round(true); st = 2; continue; }
                         bytes++;
                     } else {
                         // through the block's full tables (global table record)
-                        if (my_brec == NOREC || ++others > NDFL_FLAT_OTHER_MAX) { st = 3; continue; }
+                        if (my_brec == NOREC || ++others > NDFL_FLAT_OTHER_MAX) { st = 3; why = 2; continue; }
                         const uint32_t* tb = (const uint32_t*)(pool.bt + (uint64_t)my_brec * BT_BYTES);
                         const TabsG tg{tb, tb + (1u << LB), tb + offsetof(Tabs, lx) / 4, tb + offsetof(Tabs, dx) / 4};
                         uint32_t pp = 0;
                         Tok tk;
                         tok_e<true>(lo, hi, tg.lit[lo & ((1u << LB) - 1u)], pp, tg, my_ed, sn - p, nbr - min(nbr, p), tk);
                         if (tk.kind == K_EOB) { p += pp; end_round(true); st = 2; continue; }
-                        if (tk.kind != K_LIT && tk.kind != K_LEN) { st = 3; continue; }
+                        if (tk.kind != K_LIT && tk.kind != K_LEN) { st = 3; why = 3; continue; }
                         bytes += tk.n;
                         p += pp;
                     }
@@ -2263,6 +2284,7 @@ __device__ __forceinline__ uint32_t count_flat_group(const In& in, const uint32_
     }
     // 4. the rest back to the wave decode
     const bool rd = (uint32_t)lane < n && !ok;
+    if (whys && rd) atomicAdd(&whys[why], 1u);
     const uint64_t rm = __ballot(rd);
     if (rd) redo[__popcll(rm & ((1ull << lane) - 1ull))] = my_c;
     __syncthreads();
@@ -2307,7 +2329,7 @@ ndfl_inflate_count_wave_kernel(const uint32_t* w, uint64_t nwords, uint64_t nbit
             const uint32_t g0 = tk * 64;
             const uint64_t tf0 = stats ? wall_clock64() : 0;
             nredo = count_flat_group(in, flist + g0, min(64u, nfl - g0), cands, ncand, limit, stop_all, res, pool, hrec,
-                                     S, stg.w, lane, s_redo, tb_next, tb_end);
+                                     S, stg.w, lane, s_redo, tb_next, tb_end, stats ? ticket + 10 : nullptr);
             if (stats && lane == 0) {                   // (ticket words 5, 6: chains sent back, group wave time)
                 atomicAdd(ticket + 5, nredo);
                 atomicAdd((unsigned long long*)(ticket + 6), (unsigned long long)(wall_clock64() - tf0));

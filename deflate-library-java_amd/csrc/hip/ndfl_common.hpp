@@ -27,6 +27,7 @@ struct Knobs {
     bool lz_chain = false;       // NDFL_LZ_SEARCH=chain: the round-3 hash-chain LZ77 search
     int lz_lead = -1;            // NDFL_LZ_LEAD: parse-driven search lead-in (-1: default)
     bool flat = true;            // NDFL_FLAT=0: escape-prefix literal blocks counted in wave form too
+    uint32_t flat_min = 49152;   // NDFL_FLAT_MIN: chains to count at least for flat groups (their latency)
     bool test_segflip = false;   // NDFL_TEST_SEGFLIP: one count-pass record's byte count perturbed
                                  //   before the emit pass (the emit-side check must fail the decode)
     void read() {
@@ -45,15 +46,16 @@ struct Knobs {
         lz_lead = num("NDFL_LZ_LEAD", -1);
         test_segflip = on("NDFL_TEST_SEGFLIP");
         flat = num("NDFL_FLAT", 1) != 0;
+        flat_min = (uint32_t)num("NDFL_FLAT_MIN", 49152);
     }
     // the effective switches, one line (printed by ndfl_ctx_create when stats are on)
     void print(FILE* f) const {
         fprintf(f, "[ndfl] context knobs: stats=%d host_times=%d host_link=%d no_hdrrec=%d emit_fast=%d no_bt=%d "
                    "no_alias=%d count_w=%u deflate_pf=%d deflate_profile=%d deflate_fused=%d lz_stats=%d "
-                   "lz_search=%s lz_lead=%d test_segflip=%d flat=%d\n",
+                   "lz_search=%s lz_lead=%d test_segflip=%d flat=%d flat_min=%u\n",
                 (int)stats, (int)host_times, (int)host_link, (int)no_hdrrec, (int)emit_fast, (int)no_bt,
                 (int)no_alias, count_w, (int)deflate_pf, (int)deflate_profile, (int)deflate_fused, (int)lz_stats,
-                lz_chain ? "chain" : "parse", lz_lead, (int)test_segflip, (int)flat);
+                lz_chain ? "chain" : "parse", lz_lead, (int)test_segflip, (int)flat, flat_min);
     }
 };
 

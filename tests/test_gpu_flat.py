@@ -23,9 +23,10 @@ pytestmark = pytest.mark.gpu
 
 def _ctx(flat):
     """A context with the flat groups on or off and one wave per chain (NDFL_COUNT_W=1: streams this
-    small would otherwise be counted four waves per chain, a kernel without flat groups)."""
+    small would otherwise be counted four waves per chain, a kernel without flat groups), flat groups
+    at any stream size (NDFL_FLAT_MIN=0)."""
     import ndfl
-    env = {"NDFL_FLAT": str(flat), "NDFL_COUNT_W": "1"}
+    env = {"NDFL_FLAT": str(flat), "NDFL_COUNT_W": "1", "NDFL_FLAT_MIN": "0"}
     old = {k: os.environ.get(k) for k in env}
     os.environ.update(env)
     try:
