@@ -2207,14 +2207,14 @@ __device__ __forceinline__ uint32_t count_flat_group(const In& in, const uint32_
                     st = 1;
                     continue;
                 }
-                if (p >= sn) {                          // (segments left empty at a round's end)
-                    if (j == 63) { end_round(false); st = 0; }      // (exit63 = p)
-                    else next_seg();
-                    continue;
-                }
+                // One step, branch-free on its common path (a divergent branch per case made every step
+                // pay for the cases of the other 63 lanes): a token (up to 8 literals, or one escape
+                // literal) when the lane stands before its segment's end and the ring holds its window,
+                // then the segment switch if the lane has reached the end.  End of block, the round's
+                // end and the full-table tokens branch.
                 const uint32_t ap = base + p, cw = ap >> 5;
-                if (cw + 2 >= fw) break;                // (the ring is not that far yet: next phase point)
-                uint32_t rr0 = frow + 24 - (fw - cw);   // (fw - cw in 3..24)
+                const bool tk_ok = p < sn && cw + 2 < fw;
+                uint32_t rr0 = frow + 24 - min(fw - cw, 24u);
                 rr0 = rr0 >= 24 ? rr0 - 24 : rr0;
                 const uint32_t rr1 = rr0 == 23 ? 0u : rr0 + 1, rr2 = rr1 == 23 ? 0u : rr1 + 1;
                 const uint32_t w0 = ring[rr0 * 64], w1 = ring[rr1 * 64], w2 = ring[rr2 * 64];
@@ -2225,37 +2225,40 @@ __device__ __forceinline__ uint32_t count_flat_group(const In& in, const uint32_
                 // reload waited for the rings' loads in flight)
                 uint32_t ln;
                 asm volatile("v_mbcnt_lo_u32_b32 %0, -1, 0\n\tv_mbcnt_hi_u32_b32 %0, -1, %0" : "=v"(ln));
-                const uint32_t ent = escs[ln * 64 + ((lo >> pl) & 63u)];
-                const uint32_t q = (sn - p + 7) >> 3, qi = (nbr - min(nbr, p)) >> 3;
-                const uint32_t t = min(min(esc_index(lo, hi, M4), q), qi);
-                if (t) {                                // t literals of 8 bits
-                    bytes += t;
-                    p += 8 * t;
-                } else {
-                    const uint32_t len = ent & 15u;
-                    if ((lo & (M4 & 0xFFu)) == (M4 & 0xFFu) && ent && p + len <= nbr) {
-                        p += len;
-                        if (ent >> 4) { end_round(true); st = 2; continue; }
-                        bytes++;
-                    } else {
-                        // through the block's full tables (global table record)
-                        if (my_brec == NOREC || ++others > NDFL_FLAT_OTHER_MAX) { st = 3; why = 2; continue; }
-                        const uint32_t* tb = (const uint32_t*)(pool.bt + (uint64_t)my_brec * BT_BYTES);
-                        const TabsG tg{tb, tb + (1u << LB), tb + offsetof(Tabs, lx) / 4, tb + offsetof(Tabs, dx) / 4};
-                        uint32_t pp = 0;
-                        Tok tk;
-                        tok_e<true>(lo, hi, tg.lit[lo & ((1u << LB) - 1u)], pp, tg, my_ed, sn - p, nbr - min(nbr, p), tk);
-                        if (tk.kind == K_EOB) { p += pp; end_round(true); st = 2; continue; }
-                        if (tk.kind != K_LIT && tk.kind != K_LEN) { st = 3; why = 3; continue; }
-                        bytes += tk.n;
-                        p += pp;
-                    }
+                const uint32_t ent = escs[ln * 64 + ((lo >> pl) & 63u)], len = ent & 15u;
+                const uint32_t q = (sn - min(sn, p) + 7) >> 3, qi = (nbr - min(nbr, p)) >> 3;
+                const uint32_t t = tk_ok ? min(min(esc_index(lo, hi, M4), q), qi) : 0u;
+                const bool esc = tk_ok && t == 0 && (lo & (M4 & 0xFFu)) == (M4 & 0xFFu) && ent && p + len <= nbr;
+                const bool eob = esc && (ent >> 4);
+                p += t ? 8 * t : esc ? len : 0u;
+                bytes += t ? t : (esc && !eob) ? 1u : 0u;
+                if (eob) { end_round(true); st = 2; continue; }
+                if (tk_ok && t == 0 && !esc) {
+                    // through the block's full tables (global table record)
+                    if (my_brec == NOREC || ++others > NDFL_FLAT_OTHER_MAX) { st = 3; why = 2; continue; }
+                    const uint32_t* tb = (const uint32_t*)(pool.bt + (uint64_t)my_brec * BT_BYTES);
+                    const TabsG tg{tb, tb + (1u << LB), tb + offsetof(Tabs, lx) / 4, tb + offsetof(Tabs, dx) / 4};
+                    uint32_t pp = 0;
+                    Tok tk;
+                    tok_e<true>(lo, hi, tg.lit[lo & ((1u << LB) - 1u)], pp, tg, my_ed, sn - p, nbr - min(nbr, p), tk);
+                    if (tk.kind == K_EOB) { p += pp; end_round(true); st = 2; continue; }
+                    if (tk.kind != K_LIT && tk.kind != K_LEN) { st = 3; why = 3; continue; }
+                    bytes += tk.n;
+                    p += pp;
                 }
-                // the token(s) started before sn: a segment (or the round) ends at the first boundary past it
+                // the token(s) started before sn: a segment (or the round) ends at the first boundary
+                // past it (an empty segment at a round's end switches without a token)
                 if (p >= sn) {
-                    if (j == 63) { end_round(false); st = 0; }
-                    else next_seg();
+                    if (j == 63) { end_round(false); st = 0; continue; }
+                    if (ps) { ps[j] = o64 + base + jst; pc[j] = bytes; }
                 }
+                const bool sw = p >= sn;
+                total += sw ? bytes : 0u;
+                j += sw ? 1u : 0u;
+                jst = sw ? p : jst;
+                bytes = sw ? 0u : bytes;
+                sn = sw ? (j < 63 ? min(r0 + (j + 1) * per, re) : re) : sn;
+                if (!tk_ok && !sw) break;               // (the ring is not that far yet: next phase point)
             }
         }
         if (NDFL_FLAT_PRIO) __builtin_amdgcn_s_setprio(0);
