@@ -2204,9 +2204,9 @@ __device__ __forceinline__ uint32_t count_flat_group(const In& in, const uint32_
                     mq = idx != NOREC ? (uint4*)(pool.meta + idx) : nullptr;
                     j = 0; p = r0; jst = r0; bytes = 0;
                     sn = min(r0 + per, re);
-                    st = 1;
-                    continue;
+                    st = 1;                             // (and the round's first step at once)
                 }
+                if (st != 1) continue;
                 // One step, branch-free on its common path (a divergent branch per case made every step
                 // pay for the cases of the other 63 lanes): a token (up to 8 literals, or one escape
                 // literal) when the lane stands before its segment's end and the ring holds its window,
@@ -2232,33 +2232,38 @@ __device__ __forceinline__ uint32_t count_flat_group(const In& in, const uint32_
                 const bool eob = esc && (ent >> 4);
                 p += t ? 8 * t : esc ? len : 0u;
                 bytes += t ? t : (esc && !eob) ? 1u : 0u;
-                if (eob) { end_round(true); st = 2; continue; }
+                bool ended = eob;                       // (the block, a full-table error or the round)
                 if (tk_ok && t == 0 && !esc) {
                     // through the block's full tables (global table record)
-                    if (my_brec == NOREC || ++others > NDFL_FLAT_OTHER_MAX) { st = 3; why = 2; continue; }
-                    const uint32_t* tb = (const uint32_t*)(pool.bt + (uint64_t)my_brec * BT_BYTES);
-                    const TabsG tg{tb, tb + (1u << LB), tb + offsetof(Tabs, lx) / 4, tb + offsetof(Tabs, dx) / 4};
-                    uint32_t pp = 0;
-                    Tok tk;
-                    tok_e<true>(lo, hi, tg.lit[lo & ((1u << LB) - 1u)], pp, tg, my_ed, sn - p, nbr - min(nbr, p), tk);
-                    if (tk.kind == K_EOB) { p += pp; end_round(true); st = 2; continue; }
-                    if (tk.kind != K_LIT && tk.kind != K_LEN) { st = 3; why = 3; continue; }
-                    bytes += tk.n;
-                    p += pp;
+                    if (my_brec == NOREC || ++others > NDFL_FLAT_OTHER_MAX) {
+                        st = 3; why = 2;
+                    } else {
+                        const uint32_t* tb = (const uint32_t*)(pool.bt + (uint64_t)my_brec * BT_BYTES);
+                        const TabsG tg{tb, tb + (1u << LB), tb + offsetof(Tabs, lx) / 4, tb + offsetof(Tabs, dx) / 4};
+                        uint32_t pp = 0;
+                        Tok tk;
+                        tok_e<true>(lo, hi, tg.lit[lo & ((1u << LB) - 1u)], pp, tg, my_ed, sn - p, nbr - min(nbr, p), tk);
+                        if (tk.kind == K_LIT || tk.kind == K_LEN) bytes += tk.n;
+                        else if (tk.kind == K_EOB) ended = true;
+                        else { st = 3; why = 3; }
+                        p += pp;
+                    }
+                    ended = ended || st == 3;
                 }
                 // the token(s) started before sn: a segment (or the round) ends at the first boundary
                 // past it (an empty segment at a round's end switches without a token)
-                if (p >= sn) {
-                    if (j == 63) { end_round(false); st = 0; continue; }
-                    if (ps) { ps[j] = o64 + base + jst; pc[j] = bytes; }
+                const bool rend = !ended && p >= sn && j == 63;
+                if (ended || rend) {
+                    if (st != 3) { end_round(!rend); st = rend ? 0u : 2u; }
+                } else {
+                    const bool sw = p >= sn;
+                    if (sw && ps) { ps[j] = o64 + base + jst; pc[j] = bytes; }
+                    total += sw ? bytes : 0u;
+                    j += sw ? 1u : 0u;
+                    jst = sw ? p : jst;
+                    bytes = sw ? 0u : bytes;
+                    sn = sw ? (j < 63 ? min(r0 + (j + 1) * per, re) : re) : sn;
                 }
-                const bool sw = p >= sn;
-                total += sw ? bytes : 0u;
-                j += sw ? 1u : 0u;
-                jst = sw ? p : jst;
-                bytes = sw ? 0u : bytes;
-                sn = sw ? (j < 63 ? min(r0 + (j + 1) * per, re) : re) : sn;
-                if (!tk_ok && !sw) break;               // (the ring is not that far yet: next phase point)
             }
         }
         if (NDFL_FLAT_PRIO) __builtin_amdgcn_s_setprio(0);
